@@ -1,0 +1,146 @@
+#!/usr/bin/env python
+"""Headline benchmark: whole-job tokens/s pretraining GPT-2-small (124M) at seq 1024, bf16.
+
+Contract (driver):  python bench.py --gpus N --steps K --warmup W
+  * N = 1: runs in-process on cuda:0;  N > 1: launched by torch.distributed.run,
+    one rank per GPU, RCCL data parallel (RANK/LOCAL_RANK/WORLD_SIZE from env).
+  * W untimed warmup steps, then EXACTLY K timed optimizer steps bracketed by a
+    barrier + device synchronize on both sides; the time is the MAX over ranks.
+  * rank 0 prints ONE JSON line.
+Every timed step is a full training step: synthetic tokens streamed by the
+native loader (pinned, side-stream H2D), forward, backward, bucketed RCCL
+all-reduce overlapped with backward, fused AdamW on fp32 masters, zero_grad.
+Weights are random-init GPT-2-small (124M, tied embeddings, V=50304);
+``--backend torch`` runs the same model on stock PyTorch ops (SDPA,
+F.layer_norm, F.cross_entropy, torch AdamW-equivalent math) as the measured
+reference-equivalent baseline.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "tokens/sec (whole node) pretraining GPT-2-small seq1024 at 1/2/4/8 MI355X"
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--model", default="gpt2-small")
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PLLM_BENCH_BATCH", "16")),
+                    help="micro-batch (sequences) per GPU")
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
+    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--grad-clip", type=float, default=1.0)
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    import torch
+    import torch.distributed as dist
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.data import TokenLoader, ensure_synthetic_shard
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.parallel.dp import DataParallelEngine
+    from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
+    from pretraining_llm_amd.utils.dist import init_distributed
+
+    di = init_distributed("nccl", "cuda")
+    world = di.world_size
+    if args.gpus != world and di.is_master:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
+    dev = di.device
+    ops.set_backend(args.backend)
+    if args.backend == "auto":
+        ops._lib.require()  # the HIP path must be the one that runs: fail loudly if the extension is missing
+
+    torch.manual_seed(1234)
+    mcfg = get_preset(args.model)
+    if args.seq != mcfg.context_length:
+        mcfg = mcfg.replace(context_length=max(args.seq, mcfg.context_length))
+    model = GPT(mcfg).to(device=dev, dtype=torch.bfloat16)
+    opt = FlatAdamW(model, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
+                    max_grad_norm=args.grad_clip)
+    engine = DataParallelEngine(opt, bucket_mb=args.bucket_mb)
+
+    B, T = args.batch, args.seq
+    n_tok = max(4_000_000, 4 * B * (T + 1))
+    shard = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"pllm_bench_{mcfg.vocab_size}_{n_tok}_r{di.rank}.bin")
+    ensure_synthetic_shard(shard, n_tok, mcfg.vocab_size, seed=di.rank, fast=True)
+    loader = TokenLoader(shard, B, T, 0, 1, seed=1000 + di.rank, device=dev)
+
+    def step():
+        x, y = loader.next()
+        _, loss = model(x, y, return_logits=False)
+        loss.backward()
+        scale = engine.finish_grad_sync()
+        opt.step(grad_scale=scale)
+        opt.zero_grad()
+        return loss
+
+    model.train()
+    for i in range(args.warmup):
+        loss = step()
+        if args.verbose and di.is_master:
+            torch.cuda.synchronize()
+            print(f"[bench] warmup {i} loss {float(loss):.4f}", file=sys.stderr)
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    final_loss = float(loss)
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    tokens = world * B * T * args.steps
+    tps = tokens / elapsed
+    flops_tok = mcfg.flops_per_token(T)
+    if di.is_master:
+        rec = {
+            "metric": METRIC,
+            "value": round(tps, 1),
+            "unit": "tokens/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1000 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16",
+            "data": "synthetic (native token loader over a generated uint16 shard), random-init weights",
+            "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
+                       "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "backend": args.backend,
+                       "tokens_per_step": B * T * world},
+            "mfu": round(tps / world * flops_tok / 2.5e15, 4),
+            "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),
+            "final_loss": round(final_loss, 4),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+        }
+        print(json.dumps(rec), flush=True)
+    loader.close()
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,397 @@
+// torch op registration for the gfx950 kernels (namespace torch.ops.pllm).
+//
+// Every op checks device/dtype/shape contracts on the host BEFORE launching
+// (a wrong shape must fail here, never fault on the GPU) and launches on the
+// current HIP stream, so the ops compose with torch streams and hipGraph capture.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include "kernels.h"
+
+using at::Tensor;
+
+namespace {
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_gpu(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_bf16(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, name, " must be bfloat16, got ", t.scalar_type());
+}
+void check_contig(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+void check_aligned16(const Tensor& t, const char* name) {
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
+}
+const void* opt_ptr(const std::optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+
+// ---------------------------------------------------------------- norms
+std::vector<Tensor> norm_fwd(const Tensor& x, const std::optional<Tensor>& res, const Tensor& w,
+                             const std::optional<Tensor>& b, double eps, bool rms) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  TORCH_CHECK(x.dim() == 2, "norm_fwd expects [N, C]");
+  const int64_t N = x.size(0), C = x.size(1);
+  TORCH_CHECK(C % 8 == 0 && C <= 4096, "norm: C must be a multiple of 8 and <= 4096, got ", C);
+  check_bf16(w, "weight");
+  TORCH_CHECK(w.numel() == C && w.is_contiguous(), "norm weight shape");
+  if (b) {
+    check_bf16(*b, "bias");
+    TORCH_CHECK(b->numel() == C && b->is_contiguous(), "norm bias shape");
+  }
+  Tensor s;
+  if (res) {
+    check_bf16(*res, "residual");
+    check_contig(*res, "residual");
+    TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
+    s = at::empty_like(x);
+  } else {
+    s = x;
+  }
+  Tensor y = at::empty_like(x);
+  auto f32 = x.options().dtype(at::kFloat);
+  Tensor mean = at::empty({N}, f32), rstd = at::empty({N}, f32);
+  if (N > 0)
+    pllm::norm_fwd(x.data_ptr(), opt_ptr(res), w.data_ptr(), opt_ptr(b), y.data_ptr(), res ? s.data_ptr() : nullptr,
+                   mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)N, (int)C, (float)eps, rms, cur_stream());
+  return {y, s, mean, rstd};
+}
+
+std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& mean,
+                             const Tensor& rstd, const std::optional<Tensor>& ds, bool has_bias, bool rms) {
+  check_bf16(dy, "dy");
+  check_bf16(s, "s");
+  check_contig(dy, "dy");
+  check_contig(s, "s");
+  TORCH_CHECK(dy.sizes() == s.sizes() && dy.dim() == 2, "norm_bwd shapes");
+  const int64_t N = dy.size(0), C = dy.size(1);
+  if (ds) {
+    check_bf16(*ds, "ds");
+    check_contig(*ds, "ds");
+    TORCH_CHECK(ds->sizes() == dy.sizes(), "ds shape");
+  }
+  Tensor dx = at::empty_like(dy);
+  Tensor dw = at::empty({C}, w.options());
+  Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
+  const int G = pllm::norm_bwd_grid((int)N);
+  auto f32 = dy.options().dtype(at::kFloat);
+  Tensor dwp = at::empty({G, C}, f32);
+  Tensor dbp = has_bias ? at::empty({G, C}, f32) : Tensor();
+  if (N > 0) {
+    pllm::norm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                   opt_ptr(ds), dx.data_ptr(), dwp.data_ptr<float>(), has_bias ? dbp.data_ptr<float>() : nullptr,
+                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, cur_stream());
+  } else {
+    dw.zero_();
+    if (has_bias) db.zero_();
+  }
+  if (!has_bias) return {dx, dw};
+  return {dx, dw, db};
+}
+
+// ---------------------------------------------------------------- activations
+Tensor act_fwd(const Tensor& x, int64_t op) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  TORCH_CHECK(x.numel() % 8 == 0, "activation numel must be a multiple of 8");
+  Tensor y = at::empty_like(x);
+  if (x.numel()) pllm::act_fwd((int)op, x.data_ptr(), y.data_ptr(), x.numel(), cur_stream());
+  return y;
+}
+Tensor act_bwd(const Tensor& dy, const Tensor& xin, int64_t op) {
+  check_bf16(dy, "dy");
+  check_bf16(xin, "x");
+  check_contig(dy, "dy");
+  check_contig(xin, "x");
+  TORCH_CHECK(dy.numel() == xin.numel() && dy.numel() % 8 == 0, "activation bwd shapes");
+  Tensor dx = at::empty_like(dy);
+  if (dy.numel()) pllm::act_bwd((int)op, dy.data_ptr(), xin.data_ptr(), dx.data_ptr(), dy.numel(), cur_stream());
+  return dx;
+}
+Tensor swiglu_fwd(const Tensor& gu) {
+  check_bf16(gu, "gate_up");
+  check_contig(gu, "gate_up");
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(F2 % 16 == 0, "swiglu: last dim must be 2F with F % 8 == 0");
+  auto sizes = gu.sizes().vec();
+  sizes.back() = F2 / 2;
+  Tensor y = at::empty(sizes, gu.options());
+  const int64_t rows = gu.numel() / F2;
+  if (rows) pllm::swiglu_fwd(gu.data_ptr(), y.data_ptr(), rows, (int)(F2 / 2), cur_stream());
+  return y;
+}
+Tensor swiglu_bwd(const Tensor& dy, const Tensor& gu) {
+  check_bf16(dy, "dy");
+  check_bf16(gu, "gate_up");
+  check_contig(dy, "dy");
+  check_contig(gu, "gate_up");
+  const int64_t F2 = gu.size(-1);
+  TORCH_CHECK(dy.size(-1) * 2 == F2 && dy.numel() * 2 == gu.numel(), "swiglu bwd shapes");
+  Tensor dgu = at::empty_like(gu);
+  const int64_t rows = gu.numel() / F2;
+  if (rows) pllm::swiglu_bwd(dy.data_ptr(), gu.data_ptr(), dgu.data_ptr(), rows, (int)(F2 / 2), cur_stream());
+  return dgu;
+}
+
+// packed rows [..., n_heads_total * D]; rotates the first n_rot heads; T = positions per sequence
+Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_heads_total, int64_t n_rot, int64_t T,
+            int64_t pos_offset, bool inverse, bool inplace) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "rope tables must be fp32");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous(), "rope tables contiguous");
+  const int64_t W = x.size(-1);
+  TORCH_CHECK(W % n_heads_total == 0, "rope: width not divisible by heads");
+  const int64_t D = W / n_heads_total;
+  TORCH_CHECK(D % 16 == 0, "rope: head dim must be a multiple of 16");
+  TORCH_CHECK(cos.size(-1) == D / 2 && cos.size(0) >= T + pos_offset, "rope: table shape");
+  const int64_t rows = x.numel() / W;
+  TORCH_CHECK(rows % T == 0, "rope: rows must be a multiple of T");
+  Tensor out = inplace ? x : at::empty_like(x);
+  if (rows)
+    pllm::rope(x.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), rows, (int)T,
+               (int)n_heads_total, (int)n_rot, (int)D, (int)pos_offset, inverse, cur_stream());
+  return out;
+}
+
+void scale_(Tensor& x, const Tensor& s) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() == 1 && s.is_cuda(), "scale must be a 1-element fp32 GPU tensor");
+  TORCH_CHECK(x.numel() % 8 == 0, "scale_: numel % 8");
+  if (x.numel()) pllm::scale_bf16(x.data_ptr(), s.data_ptr<float>(), x.numel(), cur_stream());
+}
+
+// ---------------------------------------------------------------- cross entropy
+// returns per-row losses (fp32, 0 for ignored rows); if dlogits is given it is
+// overwritten with d(mean loss)/dlogits (it may alias logits).
+Tensor cross_entropy(const Tensor& logits, const Tensor& targets, const std::optional<Tensor>& dlogits,
+                     int64_t ignore_index) {
+  check_bf16(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] with unit column stride");
+  const int64_t N = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(logits.stride(0) % 8 == 0 && V % 8 == 0, "cross_entropy: V and row stride must be multiples of 8");
+  TORCH_CHECK(V <= pllm::cross_entropy_max_vocab(), "cross_entropy: vocab too large for the register-resident kernel");
+  check_aligned16(logits, "logits");
+  TORCH_CHECK(targets.is_cuda() && targets.numel() == N, "targets shape");
+  Tensor tg = targets.reshape({N}).to(at::kLong).contiguous();
+  if (dlogits) {
+    check_bf16(*dlogits, "dlogits");
+    TORCH_CHECK(dlogits->sizes() == logits.sizes() && dlogits->strides() == logits.strides(), "dlogits layout");
+  }
+  Tensor loss = at::empty({N}, logits.options().dtype(at::kFloat));
+  Tensor inv_n = (tg != ignore_index).sum().to(at::kFloat).clamp_min(1.0).reciprocal().reshape({1});
+  if (N)
+    pllm::cross_entropy(logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(), (int)N, (int)V, (int)ignore_index,
+                        loss.data_ptr<float>(), dlogits ? dlogits->data_ptr() : nullptr, inv_n.data_ptr<float>(),
+                        cur_stream());
+  return loss;
+}
+
+// ---------------------------------------------------------------- optimizer
+void adamw_(Tensor& param, Tensor& master, Tensor& m, Tensor& v, const Tensor& grad, double lr, double b1, double b2,
+            double eps, double wd, int64_t step, double grad_scale, const std::optional<Tensor>& scale,
+            const std::optional<Tensor>& wd_mask) {
+  const int64_t n = master.numel();
+  TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
+              "adamw: master/m/v must be fp32");
+  TORCH_CHECK(m.numel() == n && v.numel() == n && grad.numel() == n, "adamw: sizes");
+  TORCH_CHECK(master.is_contiguous() && m.is_contiguous() && v.is_contiguous() && grad.is_contiguous(), "adamw: contiguous");
+  TORCH_CHECK(n % 8 == 0, "adamw: flat size must be a multiple of 8");
+  const bool gf32 = grad.scalar_type() == at::kFloat;
+  TORCH_CHECK(gf32 || grad.scalar_type() == at::kBFloat16, "adamw: grad must be fp32 or bf16");
+  void* pp = nullptr;
+  if (param.defined() && param.numel()) {
+    check_bf16(param, "param");
+    TORCH_CHECK(param.numel() == n && param.is_contiguous(), "adamw: param size");
+    pp = param.data_ptr();
+  }
+  for (auto* t : {&master, &m, &v}) check_aligned16(*t, "adamw buffer");
+  check_aligned16(grad, "grad");
+  const float* sp = nullptr;
+  if (scale) {
+    TORCH_CHECK(scale->scalar_type() == at::kFloat && scale->numel() == 1 && scale->is_cuda(), "adamw scale");
+    sp = scale->data_ptr<float>();
+  }
+  const uint8_t* wm = nullptr;
+  if (wd_mask) {
+    TORCH_CHECK(wd_mask->scalar_type() == at::kByte && wd_mask->is_cuda() && wd_mask->is_contiguous(), "wd_mask: uint8 GPU");
+    TORCH_CHECK(wd_mask->numel() * 64 >= n, "wd_mask: one byte per 64 elements");
+    wm = wd_mask->data_ptr<uint8_t>();
+  }
+  if (n)
+    pllm::adamw_flat(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), gf32, n,
+                     (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)grad_scale, sp, wm,
+                     cur_stream());
+}
+
+Tensor sumsq(const Tensor& x) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "sumsq: contiguous, numel % 8");
+  const bool f32 = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || x.scalar_type() == at::kBFloat16, "sumsq dtype");
+  const int G = pllm::sumsq_blocks(x.numel());
+  Tensor part = at::empty({G}, x.options().dtype(at::kFloat));
+  if (x.numel()) pllm::sumsq(x.data_ptr(), f32, x.numel(), part.data_ptr<float>(), cur_stream());
+  else part.zero_();
+  return part.sum();
+}
+
+// ---------------------------------------------------------------- embedding
+Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const std::optional<Tensor>& wpe, int64_t pos_offset) {
+  check_bf16(wte, "wte");
+  TORCH_CHECK(idx.is_cuda() && idx.dim() == 2, "idx must be [B, T] on GPU");
+  const int64_t C = wte.size(1), T = idx.size(1);
+  TORCH_CHECK(C % 8 == 0 && wte.is_contiguous(), "embedding: C % 8");
+  if (wpe) {
+    check_bf16(*wpe, "wpe");
+    TORCH_CHECK(wpe->size(1) == C && wpe->size(0) >= T + pos_offset && wpe->is_contiguous(), "wpe shape");
+  }
+  Tensor ix = idx.to(at::kLong).contiguous();
+  Tensor out = at::empty({idx.size(0), T, C}, wte.options());
+  if (ix.numel())
+    pllm::embedding_fwd(ix.data_ptr<int64_t>(), wte.data_ptr(), opt_ptr(wpe), out.data_ptr(), ix.numel(), (int)T, (int)C,
+                        (int)pos_offset, cur_stream());
+  return out;
+}
+
+std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V, int64_t n_pos, bool has_wpe) {
+  check_bf16(dx, "dx");
+  check_contig(dx, "dx");
+  const int64_t Bn = idx.size(0), T = idx.size(1), C = dx.size(-1);
+  TORCH_CHECK(dx.numel() == Bn * T * C, "embedding bwd shape");
+  auto flat = idx.reshape({-1}).to(at::kInt);
+  auto sr = flat.sort(/*stable=*/true, 0, false);
+  Tensor sorted = std::get<0>(sr).contiguous(), perm = std::get<1>(sr).to(at::kInt).contiguous();
+  Tensor dwte = at::zeros({V, C}, dx.options());
+  Tensor dwpe = has_wpe ? at::zeros({n_pos, C}, dx.options()) : Tensor();
+  if (Bn * T)
+    pllm::embedding_bwd(dx.data_ptr(), sorted.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), dwte.data_ptr(),
+                        has_wpe ? dwpe.data_ptr() : nullptr, Bn * T, (int)Bn, (int)T, (int)C, cur_stream());
+  if (!has_wpe) return {dwte};
+  return {dwte, dwpe};
+}
+
+// ---------------------------------------------------------------- attention
+void check_head_view(const Tensor& t, const char* name, int64_t D) {
+  check_bf16(t, name);
+  TORCH_CHECK(t.dim() == 4, name, " must be [B, T, H, D]");
+  TORCH_CHECK(t.size(3) == D && t.stride(3) == 1, name, ": head dim must be innermost/contiguous");
+  TORCH_CHECK(t.stride(2) % 8 == 0 && t.stride(1) % 8 == 0 && t.stride(0) % 8 == 0, name, ": strides must be multiples of 8");
+  check_aligned16(t, name);
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal, double scale) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 64 or 128, got ", D);
+  check_head_view(q, "q", D);
+  check_head_view(k, "k", D);
+  check_head_view(v, "v", D);
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), S = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == S && v.size(2) == Hkv, "k/v shape");
+  TORCH_CHECK(H % Hkv == 0, "H % Hkv");
+  TORCH_CHECK(!causal || S >= T, "causal attention needs S >= T");
+  Tensor o = at::empty({B, T, H, D}, q.options());
+  Tensor lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
+  AttnFwdArgs a{};
+  a.q = (const uint16_t*)q.data_ptr();
+  a.k = (const uint16_t*)k.data_ptr();
+  a.v = (const uint16_t*)v.data_ptr();
+  a.o = (uint16_t*)o.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.B = B; a.H = H; a.Hkv = Hkv; a.T = T; a.S = S; a.D = D;
+  a.q_sb = q.stride(0); a.q_st = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_st = v.stride(1); a.v_sh = v.stride(2);
+  a.o_sb = o.stride(0); a.o_st = o.stride(1); a.o_sh = o.stride(2);
+  a.scale = (float)scale;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.causal = causal ? 1 : 0;
+  if (B * T * H > 0 && S > 0) pllm::attn_fwd(a, cur_stream());
+  return {o, lse};
+}
+
+// dq/dk/dv are written into caller-provided views (e.g. slices of a packed dQKV buffer)
+void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
+              Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale) {
+  const int64_t D = q.size(3);
+  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 64 or 128");
+  for (auto& pr : std::vector<std::pair<const Tensor*, const char*>>{
+           {&dout, "dout"}, {&q, "q"}, {&k, "k"}, {&v, "v"}, {&o, "o"}, {&dq, "dq"}, {&dk, "dk"}, {&dv, "dv"}})
+    check_head_view(*pr.first, pr.second, D);
+  const int64_t B = q.size(0), T = q.size(1), H = q.size(2), S = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(), "attn bwd q-side shapes");
+  TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes() && v.sizes() == k.sizes(), "attn bwd kv-side shapes");
+  TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse shape");
+  auto f32 = q.options().dtype(at::kFloat);
+  Tensor delta = at::empty({B, H, T}, f32);
+  Tensor dq_acc = at::empty({B, T, H, D}, f32);
+  AttnBwdArgs a{};
+  a.q = (const uint16_t*)q.data_ptr();
+  a.k = (const uint16_t*)k.data_ptr();
+  a.v = (const uint16_t*)v.data_ptr();
+  a.o = (const uint16_t*)o.data_ptr();
+  a.dO = (const uint16_t*)dout.data_ptr();
+  a.lse = lse.data_ptr<float>();
+  a.delta = delta.data_ptr<float>();
+  a.dq_acc = dq_acc.data_ptr<float>();
+  a.dq = (uint16_t*)dq.data_ptr();
+  a.dk = (uint16_t*)dk.data_ptr();
+  a.dv = (uint16_t*)dv.data_ptr();
+  a.B = B; a.H = H; a.Hkv = Hkv; a.T = T; a.S = S; a.D = D;
+  a.q_sb = q.stride(0); a.q_st = q.stride(1); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_st = v.stride(1); a.v_sh = v.stride(2);
+  a.o_sb = o.stride(0); a.o_st = o.stride(1); a.o_sh = o.stride(2);
+  a.do_sb = dout.stride(0); a.do_st = dout.stride(1); a.do_sh = dout.stride(2);
+  a.dq_sb = dq.stride(0); a.dq_st = dq.stride(1); a.dq_sh = dq.stride(2);
+  a.dk_sb = dk.stride(0); a.dk_st = dk.stride(1); a.dk_sh = dk.stride(2);
+  a.dv_sb = dv.stride(0); a.dv_st = dv.stride(1); a.dv_sh = dv.stride(2);
+  a.scale = (float)scale;
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  a.causal = causal ? 1 : 0;
+  if (B * T * H > 0 && S > 0) pllm::attn_bwd(a, cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(pllm, m) {
+  m.def("norm_fwd(Tensor x, Tensor? residual, Tensor weight, Tensor? bias, float eps, bool rms) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms) -> Tensor[]");
+  m.def("act_fwd(Tensor x, int op) -> Tensor");
+  m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
+  m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
+  m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
+  m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse, bool inplace) -> Tensor");
+  m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
+  m.def("cross_entropy(Tensor logits, Tensor targets, Tensor? dlogits, int ignore_index) -> Tensor");
+  m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask) -> ()");
+  m.def("sumsq(Tensor x) -> Tensor");
+  m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
+  m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe) -> Tensor[]");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
+  m.impl("norm_fwd", norm_fwd);
+  m.impl("norm_bwd", norm_bwd);
+  m.impl("act_fwd", act_fwd);
+  m.impl("act_bwd", act_bwd);
+  m.impl("swiglu_fwd", swiglu_fwd);
+  m.impl("swiglu_bwd", swiglu_bwd);
+  m.impl("rope", rope);
+  m.impl("scale_", scale_);
+  m.impl("cross_entropy", cross_entropy);
+  m.impl("adamw_", adamw_);
+  m.impl("sumsq", sumsq);
+  m.impl("embedding_fwd", embedding_fwd);
+  m.impl("embedding_bwd", embedding_bwd);
+  m.impl("attn_fwd", attn_fwd);
+  m.impl("attn_bwd", attn_bwd);
+}

@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (CDNA4, MI355X) kernels.
+//
+// Conventions used by every kernel in this directory:
+//  * wave64: lane = threadIdx.x & 63, reductions use 64-wide shuffles;
+//  * bf16 tensors are moved 16 bytes per lane (8 x bf16) whenever the row
+//    length allows it (cdna_hip_programming.md Guideline 13);
+//  * f32 -> bf16 conversion is a plain __bf16 cast (hipcc emits
+//    v_cvt_pk_bf16_f32, round-to-nearest-even, NaN-preserving);
+//  * no torch headers here: the .hip files compile in seconds and the torch
+//    glue lives in bindings.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PLLM_DEV __device__ __forceinline__
+
+typedef __bf16 bf16;
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));   // 8 x bf16 MFMA fragment
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+PLLM_DEV float bf2f(uint16_t u) { return __uint_as_float(((uint32_t)u) << 16); }
+PLLM_DEV float bf2f(bf16 b) { return (float)b; }
+PLLM_DEV uint16_t f2bf_bits(float f) {
+  bf16 b = (bf16)f;
+  return *reinterpret_cast<uint16_t*>(&b);
+}
+// two floats -> packed bf16x2 in one dword (lo in bits 0..15)
+PLLM_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  return (uint32_t)f2bf_bits(lo) | ((uint32_t)f2bf_bits(hi) << 16);
+}
+PLLM_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+PLLM_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// 8 bf16 <-> 8 floats through one 16-byte vector
+PLLM_DEV void unpack8(const u32x4& v, float* f) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = lo_bf(v[i]);
+    f[2 * i + 1] = hi_bf(v[i]);
+  }
+}
+PLLM_DEV u32x4 pack8(const float* f) {
+  u32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = pack_bf16x2(f[2 * i], f[2 * i + 1]);
+  return v;
+}
+PLLM_DEV u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+PLLM_DEV void st16(void* p, const u32x4& v) { *reinterpret_cast<u32x4*>(p) = v; }
+PLLM_DEV u32x4 ld16_nt(const void* p) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+}
+PLLM_DEV void st16_nt(void* p, const u32x4& v) {
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+}
+
+// ---- wave64 / block reductions -------------------------------------------
+PLLM_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PLLM_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum over NW waves through a small LDS scratch (NW <= 16).
+template <int NW>
+PLLM_DEV float block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = 0.f;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+template <int NW>
+PLLM_DEV float block_max(float v, float* scratch) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) scratch[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) r = fmaxf(r, scratch[i]);
+  __syncthreads();
+  return r;
+}
+
+// Bijective XCD-aware remap of a 1-D block id (cdna_hip_programming.md §5, T1):
+// blocks that the dispatcher deals to the same XCD (id % 8) get a contiguous
+// range of logical ids, so neighbouring tiles share that XCD's L2.
+PLLM_DEV int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
+}
+
+#define PLLM_CHECK_LAUNCH() (void)hipGetLastError()

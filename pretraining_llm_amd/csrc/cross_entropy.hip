@@ -1,0 +1,119 @@
+// Fused softmax cross-entropy, forward + backward in one pass (gfx950).
+//
+// Reference: F.cross_entropy(logits.view(B*T, V), targets.view(B*T)) in fp32
+// under autocast (src/models/transformer.py:72-77).  Here one workgroup of
+// 512 threads owns one row of bf16 logits; the row (V = 50304 -> 98 KiB) stays
+// in registers (CH chunks of 8 bf16 per lane), so the logits are read from HBM
+// exactly once and, in training, overwritten in place by
+//     dlogits = (softmax(x) - onehot(t)) * inv_n          (inv_n = 1 / #valid)
+// so no probability tensor and no second logits-sized buffer ever exist.
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int CE_THREADS = 512;
+constexpr int CE_WAVES = CE_THREADS / 64;
+
+template <int CH, bool WRITE_GRAD>
+__global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restrict__ logits, int64_t ld,
+                                                         const int64_t* __restrict__ targets, int V,
+                                                         int ignore_index, float* __restrict__ loss,
+                                                         uint16_t* __restrict__ dlogits, const float* __restrict__ inv_n) {
+  __shared__ float scratch[CE_WAVES];
+  const int row = blockIdx.x;
+  const uint16_t* x = logits + (size_t)row * ld;
+  const int nch = V >> 3;
+  float v[CH][8];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = threadIdx.x + CE_THREADS * k;
+    if (c < nch) {
+      unpack8(ld16(x + c * 8), v[k]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
+    }
+  }
+  // scalar tail when V % 8 != 0
+  const int tail0 = nch * 8;
+  float tv = -INFINITY;
+  const int tj = tail0 + threadIdx.x;
+  if (tj < V) {
+    tv = bf2f(x[tj]);
+    m = fmaxf(m, tv);
+  }
+  m = block_max<CE_WAVES>(m, scratch);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = threadIdx.x + CE_THREADS * k;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[k][j] = __expf(v[k][j] - m);
+        s += v[k][j];
+      }
+    }
+  }
+  if (tj < V) {
+    tv = __expf(tv - m);
+    s += tv;
+  }
+  s = block_sum<CE_WAVES>(s, scratch);
+  const int64_t t = targets[row];
+  const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
+  if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - bf2f(x[t])) : 0.f;
+  if (!WRITE_GRAD) return;
+  __syncthreads();  // every lane has read its logits before in-place overwrite (x may alias dlogits)
+  const float scale = valid ? (*inv_n) / s : 0.f;
+  uint16_t* dx = dlogits + (size_t)row * ld;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const int c = threadIdx.x + CE_THREADS * k;
+    if (c < nch) {
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * scale;
+      if (valid && (int)(t >> 3) == c) o[t & 7] -= *inv_n;
+      st16(dx + c * 8, pack8(o));
+    }
+  }
+  if (tj < V) {
+    float o = tv * scale;
+    if (valid && tj == t) o -= *inv_n;
+    dx[tj] = f2bf_bits(o);
+  }
+}
+
+}  // namespace
+
+namespace pllm {
+
+void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
+                   float* loss, void* dlogits, const float* inv_n, hipStream_t st) {
+  const int nch = V / 8;
+  const int CH = (nch + CE_THREADS - 1) / CE_THREADS;
+  const bool g = dlogits != nullptr;
+#define L(C)                                                                                               \
+  do {                                                                                                     \
+    if (g)                                                                                                 \
+      hipLaunchKernelGGL((ce_kernel<C, true>), dim3(N), dim3(CE_THREADS), 0, st, (const uint16_t*)logits, ld, \
+                         targets, V, ignore_index, loss, (uint16_t*)dlogits, inv_n);                       \
+    else                                                                                                   \
+      hipLaunchKernelGGL((ce_kernel<C, false>), dim3(N), dim3(CE_THREADS), 0, st, (const uint16_t*)logits, ld, \
+                         targets, V, ignore_index, loss, (uint16_t*)nullptr, inv_n);                       \
+  } while (0)
+  if (CH <= 1) L(1);
+  else if (CH <= 2) L(2);
+  else if (CH <= 4) L(4);
+  else if (CH <= 8) L(8);
+  else if (CH <= 13) L(13);
+  else if (CH <= 16) L(16);
+  else L(32);
+#undef L
+}
+
+int cross_entropy_max_vocab() { return CE_THREADS * 8 * 32 + CE_THREADS; }
+
+}  // namespace pllm

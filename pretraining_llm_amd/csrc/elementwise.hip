@@ -1,0 +1,202 @@
+// Memory-bound elementwise kernels (gfx950): activations and RoPE.
+//
+// * ReLU   -- reference MLP activation (src/models/mlp.py:25,39-41)
+// * GELU   -- tanh form, GPT-2 preset
+// * SwiGLU -- Llama preset, input laid out [gate | up] along the last dim
+// * RoPE   -- rotate-half convention on the q and k heads of a packed qkv row
+//
+// Every kernel moves 16 B (8 x bf16) per lane per access and grid-strides over
+// a grid capped at 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11/13).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr float kGeluK = 0.7978845608028654f;  // sqrt(2/pi)
+constexpr float kGeluC = 0.044715f;
+
+PLLM_DEV float tanh_fast(float u) {
+  // tanh(u) = 1 - 2 / (exp(2u) + 1); saturates correctly for |u| large
+  return 1.f - 2.f / (__expf(2.f * u) + 1.f);
+}
+PLLM_DEV float gelu_f(float x) {
+  const float t = tanh_fast(kGeluK * (x + kGeluC * x * x * x));
+  return 0.5f * x * (1.f + t);
+}
+PLLM_DEV float gelu_df(float x) {
+  const float x2 = x * x;
+  const float t = tanh_fast(kGeluK * (x + kGeluC * x2 * x));
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK * (1.f + 3.f * kGeluC * x2);
+}
+PLLM_DEV float sigmoid_f(float x) { return 1.f / (1.f + __expf(-x)); }
+
+inline int ew_grid(size_t n_vec) {
+  size_t g = (n_vec + 255) / 256;
+  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+}
+
+// op: 0 relu, 1 gelu
+template <int OP>
+__global__ __launch_bounds__(256) void act_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                      size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(ld16(x + i * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = OP == 0 ? fmaxf(f[j], 0.f) : gelu_f(f[j]);
+    st16(y + i * 8, pack8(f));
+  }
+}
+
+// relu bwd takes the OUTPUT (y>0 <=> x>0), gelu bwd takes the input
+template <int OP>
+__global__ __launch_bounds__(256) void act_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ xin,
+                                                      uint16_t* __restrict__ dx, size_t nvec) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float g[8], a[8];
+    unpack8(ld16(dy + i * 8), g);
+    unpack8(ld16(xin + i * 8), a);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = OP == 0 ? (a[j] > 0.f ? g[j] : 0.f) : g[j] * gelu_df(a[j]);
+    st16(dx + i * 8, pack8(g));
+  }
+}
+
+// SwiGLU: gu [rows, 2F] -> y [rows, F];  F % 8 == 0
+__global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
+                                                         size_t rows, int F) {
+  const int fv = F >> 3;
+  const size_t nvec = rows * fv;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / fv;
+    const int c = (int)(i - r * fv);
+    float g[8], u[8];
+    unpack8(ld16(gu + r * 2 * F + c * 8), g);
+    unpack8(ld16(gu + r * 2 * F + F + c * 8), u);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = g[j] * sigmoid_f(g[j]) * u[j];
+    st16(y + r * F + c * 8, pack8(g));
+  }
+}
+
+__global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ gu,
+                                                         uint16_t* __restrict__ dgu, size_t rows, int F) {
+  const int fv = F >> 3;
+  const size_t nvec = rows * fv;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    const size_t r = i / fv;
+    const int c = (int)(i - r * fv);
+    float g[8], u[8], d[8], dg[8], du[8];
+    unpack8(ld16(gu + r * 2 * F + c * 8), g);
+    unpack8(ld16(gu + r * 2 * F + F + c * 8), u);
+    unpack8(ld16(dy + r * F + c * 8), d);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float sg = sigmoid_f(g[j]);
+      const float silu = g[j] * sg;
+      du[j] = d[j] * silu;
+      dg[j] = d[j] * u[j] * sg * (1.f + g[j] * (1.f - sg));
+    }
+    st16(dgu + r * 2 * F + c * 8, pack8(dg));
+    st16(dgu + r * 2 * F + F + c * 8, pack8(du));
+  }
+}
+
+// RoPE over the first n_rot heads of each packed row [rows, n_heads_total*D]
+// (q heads then k heads); the remaining heads (v) are copied when out != in.
+// cos/sin: fp32 [T, D/2]; row r has position (r % T) + pos_offset.
+// dir = +1 forward rotation, -1 inverse (backward).
+__global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                   const float* __restrict__ cosb, const float* __restrict__ sinb,
+                                                   size_t rows, int T, int n_heads_total, int n_rot, int D,
+                                                   int pos_offset, float dir) {
+  const int half = D >> 1;
+  const int hv = half >> 3;  // 8-element groups per half
+  const size_t W = (size_t)n_heads_total * D;
+  const size_t nwork = rows * n_heads_total * hv;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nwork; i += (size_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % hv);
+    const size_t rh = i / hv;
+    const int h = (int)(rh % n_heads_total);
+    const size_t r = rh / n_heads_total;
+    const uint16_t* src = in + r * W + (size_t)h * D;
+    uint16_t* dst = out + r * W + (size_t)h * D;
+    u32x4 lo = ld16(src + g * 8), hi = ld16(src + half + g * 8);
+    if (h < n_rot) {
+      const int t = (int)(r % T) + pos_offset;
+      float a[8], b[8], o1[8], o2[8];
+      unpack8(lo, a);
+      unpack8(hi, b);
+      const float* cp = cosb + (size_t)t * half + g * 8;
+      const float* sp = sinb + (size_t)t * half + g * 8;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float c = cp[j], s = sp[j] * dir;
+        o1[j] = a[j] * c - b[j] * s;
+        o2[j] = b[j] * c + a[j] * s;
+      }
+      st16(dst + g * 8, pack8(o1));
+      st16(dst + half + g * 8, pack8(o2));
+    } else if (dst != src) {
+      st16(dst + g * 8, lo);
+      st16(dst + half + g * 8, hi);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(uint16_t* __restrict__ x, const float* __restrict__ s, size_t nvec) {
+  const float sc = *s;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
+    float f[8];
+    unpack8(ld16(x + i * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] *= sc;
+    st16(x + i * 8, pack8(f));
+  }
+}
+
+}  // namespace
+
+namespace pllm {
+
+void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st) {
+  const size_t nv = n / 8;
+  if (op == 0)
+    hipLaunchKernelGGL(act_fwd_kernel<0>, dim3(ew_grid(nv)), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y, nv);
+  else
+    hipLaunchKernelGGL(act_fwd_kernel<1>, dim3(ew_grid(nv)), dim3(256), 0, st, (const uint16_t*)x, (uint16_t*)y, nv);
+}
+
+void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStream_t st) {
+  const size_t nv = n / 8;
+  if (op == 0)
+    hipLaunchKernelGGL(act_bwd_kernel<0>, dim3(ew_grid(nv)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)xin, (uint16_t*)dx, nv);
+  else
+    hipLaunchKernelGGL(act_bwd_kernel<1>, dim3(ew_grid(nv)), dim3(256), 0, st, (const uint16_t*)dy,
+                       (const uint16_t*)xin, (uint16_t*)dx, nv);
+}
+
+void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_fwd_kernel, dim3(ew_grid(rows * (F / 8))), dim3(256), 0, st, (const uint16_t*)gu,
+                     (uint16_t*)y, rows, F);
+}
+
+void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st) {
+  hipLaunchKernelGGL(swiglu_bwd_kernel, dim3(ew_grid(rows * (F / 8))), dim3(256), 0, st, (const uint16_t*)dy,
+                     (const uint16_t*)gu, (uint16_t*)dgu, rows, F);
+}
+
+void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
+          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st) {
+  const size_t nwork = rows * n_heads_total * (D / 16);
+  hipLaunchKernelGGL(rope_kernel, dim3(ew_grid(nwork)), dim3(256), 0, st, (const uint16_t*)in, (uint16_t*)out, cosb,
+                     sinb, rows, T, n_heads_total, n_rot, D, pos_offset, inverse ? -1.f : 1.f);
+}
+
+void scale_bf16(void* x, const float* s, size_t n, hipStream_t st) {
+  const size_t nv = n / 8;
+  hipLaunchKernelGGL(scale_kernel, dim3(ew_grid(nv)), dim3(256), 0, st, (uint16_t*)x, s, nv);
+}
+
+}  // namespace pllm

@@ -1,0 +1,73 @@
+// Host-side launch API of the gfx950 kernels.  Plain pointers + hipStream_t only,
+// so the kernel translation units never include torch headers; bindings.cpp is
+// the only file that knows about at::Tensor.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+struct AttnFwdArgs {
+  const uint16_t *q, *k, *v;
+  uint16_t* o;
+  float* lse;  // [B, H, T] natural-log LSE, may be null
+  int B, H, Hkv, T, S, D;
+  int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
+  float scale, scale_log2;
+  int causal;
+};
+
+struct AttnBwdArgs {
+  const uint16_t *q, *k, *v, *o, *dO;
+  const float* lse;
+  float* delta;   // [B, H, T] scratch
+  float* dq_acc;  // [B, T, H, D] fp32 scratch
+  uint16_t *dq, *dk, *dv;
+  int B, H, Hkv, T, S, D;
+  int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh, do_sb, do_st, do_sh;
+  int64_t dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
+  float scale, scale_log2;
+  int causal;
+};
+
+namespace pllm {
+
+// norm.hip
+void norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* s, float* mean,
+              float* rstd, int N, int C, float eps, bool rms, hipStream_t st);
+int norm_bwd_grid(int N);
+void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, hipStream_t st);
+
+// elementwise.hip (op: 0 relu, 1 gelu-tanh)
+void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st);
+void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStream_t st);
+void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st);
+void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st);
+void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
+          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st);
+void scale_bf16(void* x, const float* s, size_t n, hipStream_t st);
+
+// cross_entropy.hip
+void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
+                   float* loss, void* dlogits, const float* inv_n, hipStream_t st);
+int cross_entropy_max_vocab();
+
+// adamw.hip
+void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, size_t n,
+                float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
+                const float* scale_ptr, const uint8_t* wd_blocks, hipStream_t st);
+int sumsq_blocks(size_t n);
+void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
+
+// embedding.hip
+void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t N, int T, int C,
+                   int pos_offset, hipStream_t st);
+void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, int64_t N,
+                   int Bn, int T, int C, hipStream_t st);
+
+// attention.hip
+bool attn_supported_head_dim(int D);
+void attn_fwd(const AttnFwdArgs& a, hipStream_t st);
+void attn_bwd(const AttnBwdArgs& a, hipStream_t st);
+
+}  // namespace pllm

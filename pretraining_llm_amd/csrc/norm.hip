@@ -1,0 +1,249 @@
+// LayerNorm / RMSNorm with a fused residual add, forward and backward (gfx950).
+//
+// Reference math: nn.LayerNorm(C) with affine weight+bias applied pre-attention
+// and pre-MLP (reference src/models/transformer_block.py:28-31,44-46) and as the
+// final norm (transformer.py:37,70).  The residual adds `x + attn(...)` /
+// `x + mlp(...)` (transformer_block.py:44,46) are folded into the NEXT norm:
+//
+//   fwd:  s = x + r  (stored, bf16) ;  y = (s - mean) * rstd * w + b
+//   bwd:  dx = d(norm)/ds . dy + ds_next      (ds_next = grad of the residual stream)
+//
+// Layout / mapping: one wave64 per row, 8 bf16 (16 B) per lane per chunk, the
+// row held in registers between the two reduction passes (exact two-pass
+// variance, no E[x^2]-E[x]^2 cancellation).  dw/db are reduced per workgroup
+// into an fp32 [G, C] slab and summed by a second, column-parallel kernel, so
+// the weight gradient is deterministic (no float atomics).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
+
+template <int K>  // chunks of 8 elements per lane (C <= 512*K)
+__global__ __launch_bounds__(256) void norm_fwd_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
+    const uint16_t* __restrict__ b, uint16_t* __restrict__ y, uint16_t* __restrict__ s_out,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int C, float eps, int rms) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int nch = C >> 3;
+  const size_t base = (size_t)row * C;
+  float v[K][8];
+  float sum = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nch) {
+      u32x4 xv = ld16(x + base + c * 8);
+      unpack8(xv, v[k]);
+      if (res) {
+        float r8[8];
+        unpack8(ld16(res + base + c * 8), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[k][j] += r8[j];
+        u32x4 sv = pack8(v[k]);
+        st16(s_out + base + c * 8, sv);
+        unpack8(sv, v[k]);  // normalise exactly the bf16 value that backward will see
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[k][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[k][j] = 0.f;
+    }
+  }
+  const float invC = 1.f / (float)C;
+  float mean = 0.f;
+  if (!rms) mean = wave_sum(sum) * invC;
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float d = v[k][j] - mean;
+        sq += d * d;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(sq) * invC + eps);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nch) {
+      float w8[8], o[8];
+      unpack8(ld16(w + c * 8), w8);
+      if (b) {
+        float b8[8];
+        unpack8(ld16(b + c * 8), b8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * w8[j] + b8[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * w8[j];
+      }
+      st16(y + base + c * 8, pack8(o));
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void norm_bwd_kernel(
+    const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s, const uint16_t* __restrict__ w,
+    const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const uint16_t* __restrict__ ds,
+    uint16_t* __restrict__ dx, float* __restrict__ dw_part, float* __restrict__ db_part, int N, int C,
+    int rms) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int nch = C >> 3;
+  const float invC = 1.f / (float)C;
+  float w8[K][8], dwa[K][8], dba[K][8];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nch) unpack8(ld16(w + c * 8), w8[k]);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dwa[k][j] = 0.f;
+      dba[k][j] = 0.f;
+      if (c >= nch) w8[k][j] = 0.f;
+    }
+  }
+  for (int row = blockIdx.x * ROWS_PER_BLOCK + wid; row < N; row += gridDim.x * ROWS_PER_BLOCK) {
+    const size_t base = (size_t)row * C;
+    const float mean = rms ? 0.f : mean_in[row];
+    const float rstd = rstd_in[row];
+    float xh[K][8], g[K][8];
+    float sg = 0.f, sgx = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch) {
+        float d8[8];
+        unpack8(ld16(s + base + c * 8), xh[k]);
+        unpack8(ld16(dy + base + c * 8), d8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[k][j] = (xh[k][j] - mean) * rstd;
+          g[k][j] = d8[j] * w8[k][j];
+          sg += g[k][j];
+          sgx += g[k][j] * xh[k][j];
+          dwa[k][j] += d8[j] * xh[k][j];
+          dba[k][j] += d8[j];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xh[k][j] = g[k][j] = 0.f;
+      }
+    }
+    const float mg = rms ? 0.f : wave_sum(sg) * invC;
+    const float mgx = wave_sum(sgx) * invC;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - mg - xh[k][j] * mgx);
+        if (ds) {
+          float r8[8];
+          unpack8(ld16(ds + base + c * 8), r8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] += r8[j];
+        }
+        st16(dx + base + c * 8, pack8(o));
+      }
+    }
+  }
+  // reduce the 4 waves' dw/db partials through LDS, one slab row per block
+  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C] dw then [4][C] db
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    if (c < nch) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[wid * C + c * 8 + j] = dwa[k][j];
+        red[(4 + wid) * C + c * 8 + j] = dba[k][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    float a = red[i] + red[C + i] + red[2 * C + i] + red[3 * C + i];
+    dw_part[(size_t)blockIdx.x * C + i] = a;
+    if (db_part) {
+      float bb = red[4 * C + i] + red[5 * C + i] + red[6 * C + i] + red[7 * C + i];
+      db_part[(size_t)blockIdx.x * C + i] = bb;
+    }
+  }
+}
+
+// column sums of an fp32 [G, C] slab -> bf16 [C]
+__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, int G, int C,
+                                                         uint16_t* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int g = 0;
+  for (; g + 4 <= G; g += 4) {
+    a0 += part[(size_t)g * C + c];
+    a1 += part[(size_t)(g + 1) * C + c];
+    a2 += part[(size_t)(g + 2) * C + c];
+    a3 += part[(size_t)(g + 3) * C + c];
+  }
+  for (; g < G; ++g) a0 += part[(size_t)g * C + c];
+  out[c] = f2bf_bits((a0 + a1) + (a2 + a3));
+}
+
+}  // namespace
+
+namespace pllm {
+
+void norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* s, float* mean,
+              float* rstd, int N, int C, float eps, bool rms, hipStream_t st) {
+  dim3 grid((N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
+  const int K = (C + 511) / 512;
+#define L(KK)                                                                                           \
+  hipLaunchKernelGGL(norm_fwd_kernel<KK>, grid, block, 0, st, (const uint16_t*)x, (const uint16_t*)res, \
+                     (const uint16_t*)w, (const uint16_t*)b, (uint16_t*)y, (uint16_t*)s, mean, rstd, N, C, eps, \
+                     (int)rms)
+  if (K <= 1) L(1);
+  else if (K <= 2) L(2);
+  else if (K <= 4) L(4);
+  else L(8);
+#undef L
+}
+
+int norm_bwd_grid(int N) {
+  int g = (N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
+  return g < 1024 ? g : 1024;
+}
+
+void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms,
+              hipStream_t st) {
+  const int G = norm_bwd_grid(N);
+  const int K = (C + 511) / 512;
+  const size_t lds = (size_t)8 * C * sizeof(float);
+#define L(KK)                                                                                             \
+  hipLaunchKernelGGL(norm_bwd_kernel<KK>, dim3(G), dim3(256), lds, st, (const uint16_t*)dy, (const uint16_t*)s, \
+                     (const uint16_t*)w, mean, rstd, (const uint16_t*)ds, (uint16_t*)dx, dw_part, db_part, N, C,  \
+                     (int)rms)
+  if (K <= 1) L(1);
+  else if (K <= 2) L(2);
+  else if (K <= 4) L(4);
+  else L(8);
+#undef L
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, st, dw_part, G, C, (uint16_t*)dw);
+  if (db_part && db)
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, st, db_part, G, C, (uint16_t*)db);
+}
+
+}  // namespace pllm

@@ -1,0 +1,108 @@
+"""Autoregressive generation with a KV cache.
+
+Reference behaviour (src/models/transformer.py:96-114): loop ``max_new_tokens``
+times, crop the context to the last ``context_length`` tokens, run a FULL forward
+(no KV cache), softmax the last position and ``torch.multinomial`` one token.
+
+Here the prompt is prefilled once through the flash-attention kernel and every
+new token is a single-position step that appends its K/V to a preallocated
+cache (O(T) per token instead of O(T^2 * L)).  When the running sequence would
+exceed ``context_length`` with learned absolute positions, the reference's crop
+semantics are reproduced exactly by re-prefilling the cropped window.
+``temperature``/``top_k`` extend the reference's plain multinomial sampling
+(temperature 1, no top-k == reference).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from .. import ops
+
+
+class KVCache:
+    """Per-layer K/V buffers [B, S_max, Hkv, D] in the model's compute dtype."""
+
+    def __init__(self, n_layers: int, batch: int, max_len: int, n_kv_head: int, head_dim: int, dtype, device):
+        shape = (batch, max_len, n_kv_head, head_dim)
+        self.k = [torch.empty(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.v = [torch.empty(shape, dtype=dtype, device=device) for _ in range(n_layers)]
+        self.max_len = max_len
+
+    def update(self, layer: int, k: torch.Tensor, v: torch.Tensor, pos: int):
+        T = k.shape[1]
+        if pos + T > self.max_len:
+            raise ValueError(f"KV cache overflow: {pos + T} > {self.max_len}")
+        self.k[layer][:, pos:pos + T].copy_(k)
+        self.v[layer][:, pos:pos + T].copy_(v)
+        return self.k[layer][:, :pos + T], self.v[layer][:, :pos + T]
+
+
+@torch.no_grad()
+def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Tensor:
+    """Run tokens ``idx`` [B, T] at absolute positions pos..pos+T-1; returns logits of the last position."""
+    cfg = model.config
+    wpe = model.position_embed.weight if model.position_embed is not None else None
+    x = ops.embedding(idx, model.token_embed.weight, wpe, pos_offset=pos)
+    rope = model.rope_tables(idx.device, pos + idx.shape[1])
+    res = None
+    for i, blk in enumerate(model.attn_blocks):
+        x, res = blk.forward_cached(x, res, cache, i, pos, rope)
+    h, _ = model.layer_norm(x, res)
+    h = h[:, -1, :]
+    return torch.nn.functional.linear(h, model.head_weight, model.head_bias).float()
+
+
+def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
+                generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    """logits [B, V] (fp32) -> next token ids [B, 1]; temperature 0 = greedy."""
+    if temperature == 0.0:
+        return logits.argmax(-1, keepdim=True)
+    logits = logits / temperature
+    if top_k is not None and top_k < logits.shape[-1]:
+        v, _ = torch.topk(logits, top_k)
+        logits = logits.masked_fill(logits < v[:, [-1]], float("-inf"))
+    probs = torch.softmax(logits, dim=-1)
+    return torch.multinomial(probs, num_samples=1, generator=generator)
+
+
+@torch.no_grad()
+def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0, top_k: Optional[int] = None,
+             use_cache: bool = True, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+    was_training = model.training
+    model.eval()
+    cfg = model.config
+    ctx_len = cfg.context_length
+    learned = cfg.pos == "learned"
+    try:
+        if not use_cache:
+            for _ in range(max_new_tokens):
+                idx_cond = idx[:, -ctx_len:]
+                logits, _ = model(idx_cond)
+                nxt = sample_next(logits[:, -1, :].float(), temperature, top_k, generator)
+                idx = torch.cat([idx, nxt], dim=1)
+            return idx
+        B = idx.shape[0]
+        max_len = min(idx.shape[1] + max_new_tokens, ctx_len) if learned else idx.shape[1] + max_new_tokens
+        dtype = model.token_embed.weight.dtype
+        cache = KVCache(cfg.n_blocks, B, max(max_len, 1), cfg.n_kv_head, cfg.head_dim, dtype, idx.device)
+        window = idx[:, -ctx_len:] if learned else idx
+        logits = forward_cached(model, window, cache, 0)
+        pos = window.shape[1]
+        for step in range(max_new_tokens):
+            nxt = sample_next(logits, temperature, top_k, generator)
+            idx = torch.cat([idx, nxt], dim=1)
+            if step == max_new_tokens - 1:
+                break
+            if learned and pos >= ctx_len:
+                # reference crop semantics: positions restart at 0 for the last ctx_len tokens
+                window = idx[:, -ctx_len:]
+                logits = forward_cached(model, window, cache, 0)
+                pos = window.shape[1]
+            else:
+                logits = forward_cached(model, nxt, cache, pos)
+                pos += 1
+        return idx
+    finally:
+        model.train(was_training)

@@ -1,0 +1,255 @@
+"""Decoder-only transformer LM built on the fused gfx950 ops.
+
+Reference parity (Flink-ddd/pretraining-llm):
+* ``Transformer.forward(idx, targets) -> (logits, loss)``  -- `src/models/transformer.py:56-78`
+* ``forward_embedding`` (fixed for L>1)                      -- `transformer.py:80-94`, `transformer_block.py:49-61`
+* ``generate`` (multinomial sampling, context crop)           -- `transformer.py:96-114`, here with a KV cache
+* module / state-dict names ``token_embed, position_embed, attn_blocks.{i}.{ln1,attn,ln2,mlp}, layer_norm,
+  lm_head, pos_idxs``                                         -- `transformer.py:34-39`
+
+MI355X-first structure (not a translation of the reference's per-head modules):
+* one packed QKV GEMM per layer (hipBLASLt) feeding a HIP flash-attention kernel that
+  reads Q/K/V strided out of it (RoPE applied in-kernel for llama);
+* the residual add is fused into the next norm kernel: blocks pass ``(hidden, residual)``
+  pairs so no standalone add kernel exists in forward or backward;
+* the LM head + cross-entropy writes dlogits during the forward (one pass over logits).
+For ``arch="ref"`` a state-dict hook splits/fuses the packed QKV weight into the
+reference's per-head ``attn.heads.{h}.{key,query,value}.weight`` (+ ``tril``) layout.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional, Tuple
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+from torch.utils.checkpoint import checkpoint
+
+from .. import ops
+from .config import ModelConfig
+
+
+class Norm(nn.Module):
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        C = cfg.n_embed
+        self.rms = cfg.norm == "rmsnorm"
+        self.eps = cfg.norm_eps
+        self.weight = nn.Parameter(torch.ones(C))
+        self.bias = None if self.rms else nn.Parameter(torch.zeros(C))
+
+    def forward(self, x, residual=None):
+        """Returns (norm(x + residual), x + residual)."""
+        if self.rms:
+            return ops.rms_norm(x, self.weight, self.eps, residual)
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual)
+
+
+class Attention(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int = 0):
+        super().__init__()
+        self.cfg = cfg
+        self.n_head, self.n_kv_head, self.head_dim = cfg.n_head, cfg.n_kv_head, cfg.head_dim
+        C = cfg.n_embed
+        qkv_out = (cfg.n_head + 2 * cfg.n_kv_head) * cfg.head_dim
+        self.qkv = nn.Linear(C, qkv_out, bias=cfg.bias and cfg.arch != "ref")
+        self.proj = nn.Linear(C, C, bias=cfg.bias) if cfg.attn_out_proj else None
+
+    def forward(self, x, rope=None):
+        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        cos, sin = rope if rope is not None else (None, None)
+        y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
+        if self.proj is not None:
+            y = F.linear(y, self.proj.weight, self.proj.bias)
+        return y
+
+    # --- KV-cache decode -------------------------------------------------
+    def forward_cached(self, x, cache, layer_idx, pos, rope=None):
+        B, T, _ = x.shape
+        H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
+        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        q = qkv[..., : H * D].view(B, T, H, D)
+        k = qkv[..., H * D:(H + Hkv) * D].view(B, T, Hkv, D)
+        v = qkv[..., (H + Hkv) * D:].view(B, T, Hkv, D)
+        if rope is not None:
+            cos, sin = rope
+            q = ops.apply_rope(q, cos, sin, pos)
+            k = ops.apply_rope(k, cos, sin, pos)
+        kc, vc = cache.update(layer_idx, k, v, pos)
+        y = ops.attention(q.contiguous(), kc, vc, causal=True)
+        y = y.reshape(B, T, H * D)
+        if self.proj is not None:
+            y = F.linear(y, self.proj.weight, self.proj.bias)
+        return y
+
+
+class MLP(nn.Module):
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        C, Fh = cfg.n_embed, cfg.ffn_hidden
+        self.kind = cfg.mlp
+        up = 2 * Fh if cfg.mlp == "swiglu" else Fh
+        self.hidden = nn.Linear(C, up, bias=cfg.bias)
+        self.proj = nn.Linear(Fh, C, bias=cfg.bias)
+
+    def forward_embedding(self, x):
+        h = F.linear(x, self.hidden.weight, self.hidden.bias)
+        if self.kind == "gelu":
+            return ops.gelu(h)
+        if self.kind == "swiglu":
+            return ops.swiglu(h)
+        return ops.relu(h)
+
+    def project_embedding(self, h):
+        return F.linear(h, self.proj.weight, self.proj.bias)
+
+    def forward(self, x):
+        return self.project_embedding(self.forward_embedding(x))
+
+
+class Block(nn.Module):
+    def __init__(self, cfg: ModelConfig, layer_idx: int = 0):
+        super().__init__()
+        self.ln1 = Norm(cfg)
+        self.attn = Attention(cfg, layer_idx)
+        self.ln2 = Norm(cfg)
+        self.mlp = MLP(cfg)
+
+    def forward(self, x, residual=None, rope=None):
+        """(x, residual) -> (mlp_out, residual_after_attn); the caller's next norm adds them."""
+        h, res = self.ln1(x, residual)
+        a = self.attn(h, rope)
+        h2, res2 = self.ln2(a, res)
+        return self.mlp(h2), res2
+
+    def forward_cached(self, x, residual, cache, layer_idx, pos, rope=None):
+        h, res = self.ln1(x, residual)
+        a = self.attn.forward_cached(h, cache, layer_idx, pos, rope)
+        h2, res2 = self.ln2(a, res)
+        return self.mlp(h2), res2
+
+    def forward_embedding(self, x, residual=None, rope=None):
+        h, res = self.ln1(x, residual)
+        a = self.attn(h, rope)
+        h2, res2 = self.ln2(a, res)
+        return self.mlp.forward_embedding(h2), res2
+
+
+class GPT(nn.Module):
+    def __init__(self, cfg: ModelConfig):
+        super().__init__()
+        self.config = cfg
+        self.context_length = cfg.context_length
+        self.N_BLOCKS = cfg.n_blocks
+        C, V = cfg.n_embed, cfg.vocab_size
+        self.token_embed = nn.Embedding(V, C)
+        self.position_embed = nn.Embedding(cfg.context_length, C) if cfg.pos == "learned" else None
+        self.attn_blocks = nn.ModuleList([Block(cfg, i) for i in range(cfg.n_blocks)])
+        self.layer_norm = Norm(cfg)
+        if cfg.tie_embeddings:
+            self.lm_head = None
+        else:
+            self.lm_head = nn.Linear(C, V, bias=cfg.head_bias)
+        if cfg.arch == "ref":
+            # persistent like the reference (transformer.py:39) so checkpoints match key-for-key
+            self.register_buffer("pos_idxs", torch.arange(cfg.context_length), persistent=True)
+            from .compat import install_ref_state_dict_hooks
+            install_ref_state_dict_hooks(self)
+        self._rope = None
+        self.reset_parameters()
+
+    # ------------------------------------------------------------------
+    def reset_parameters(self):
+        cfg = self.config
+        if cfg.init == "torch_default":
+            for m in self.modules():
+                if isinstance(m, (nn.Linear, nn.Embedding)):
+                    m.reset_parameters()
+            return
+        std = cfg.init_std
+        proj_std = std / math.sqrt(2 * cfg.n_blocks)
+        for name, p in self.named_parameters():
+            if p.dim() == 1:
+                if name.endswith("bias"):
+                    nn.init.zeros_(p)
+                else:
+                    nn.init.ones_(p)
+            elif name.endswith("attn.proj.weight") or name.endswith("mlp.proj.weight"):
+                nn.init.normal_(p, 0.0, proj_std)
+            else:
+                nn.init.normal_(p, 0.0, std)
+
+    @property
+    def head_weight(self):
+        return self.token_embed.weight if self.lm_head is None else self.lm_head.weight
+
+    @property
+    def head_bias(self):
+        return None if self.lm_head is None else self.lm_head.bias
+
+    def rope_tables(self, device, length: Optional[int] = None):
+        cfg = self.config
+        if cfg.pos != "rope":
+            return None
+        L = length or cfg.context_length
+        if self._rope is None or self._rope[0].device != device or self._rope[0].shape[0] < L:
+            self._rope = ops.rope_cache(L, cfg.head_dim, cfg.rope_theta, device)
+        return self._rope
+
+    def num_params(self) -> int:
+        return sum(p.numel() for p in self.parameters())
+
+    # ------------------------------------------------------------------
+    def _embed(self, idx):
+        wpe = self.position_embed.weight if self.position_embed is not None else None
+        T = idx.shape[1]
+        if T > self.config.context_length and wpe is not None:
+            raise ValueError(f"sequence length {T} > context_length {self.config.context_length}")
+        return ops.embedding(idx, self.token_embed.weight, wpe)
+
+    def _trunk(self, idx):
+        x = self._embed(idx)
+        rope = self.rope_tables(idx.device, idx.shape[1])
+        res = None
+        ckpt = self.config.activation_checkpointing and self.training and torch.is_grad_enabled()
+        for blk in self.attn_blocks:
+            if ckpt:
+                x, res = checkpoint(blk, x, res, rope, use_reentrant=False)
+            else:
+                x, res = blk(x, res, rope)
+        h, _ = self.layer_norm(x, res)
+        return h
+
+    def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None,
+                return_logits: bool = True) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        h = self._trunk(idx)
+        B, T, C = h.shape
+        if targets is None:
+            logits = F.linear(h, self.head_weight, self.head_bias)
+            return logits, None
+        if not return_logits:
+            # training hot path: LM head GEMM + fused CE that overwrites the logits with dlogits
+            return None, ops.lm_head_cross_entropy(h, self.head_weight, self.head_bias, targets)
+        logits = F.linear(h.reshape(B * T, C), self.head_weight, self.head_bias)
+        loss = ops.cross_entropy(logits, targets.reshape(B * T))
+        return logits.view(B, T, -1), loss
+
+    def forward_embedding(self, idx):
+        """(hidden, residual) of the LAST block: hidden = act(mlp.hidden(ln2(res))) [B,T,F],
+        res = post-attention residual stream [B,T,C]. Matches the reference for L=1
+        (`transformer_block.py:49-61`) and, unlike it, is well-defined for L>1."""
+        x = self._embed(idx)
+        rope = self.rope_tables(idx.device, idx.shape[1])
+        res = None
+        for blk in self.attn_blocks[:-1]:
+            x, res = blk(x, res, rope)
+        return self.attn_blocks[-1].forward_embedding(x, res, rope)
+
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def generate(self, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0,
+                 top_k: Optional[int] = None, use_cache: bool = True, generator=None) -> torch.Tensor:
+        from ..inference.generate import generate
+        return generate(self, idx, max_new_tokens, temperature=temperature, top_k=top_k,
+                        use_cache=use_cache, generator=generator)

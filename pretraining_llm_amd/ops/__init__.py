@@ -1,0 +1,374 @@
+"""Fused ops with autograd: HIP (gfx950) kernels on GPU, PyTorch reference on CPU.
+
+Every op here is a ``torch.autograd.Function`` whose forward/backward call
+``torch.ops.pllm.*`` (hand-written HIP kernels in ``pretraining_llm_amd/csrc``)
+when its inputs live on the GPU, and the reference in ``reference.py``
+otherwise.  There is no third path: a GPU tensor with a missing extension
+raises (see ``_lib.require``).
+
+``set_backend("torch")`` forces stock PyTorch ops everywhere (SDPA attention,
+F.layer_norm, F.cross_entropy in fp32 like the reference's autocast); it exists
+only to measure the stock-PyTorch baseline on the same model and
+is never selected implicitly.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from . import _lib
+from . import reference as ref
+
+_BACKEND = "auto"   # auto -> HIP for GPU tensors, reference for CPU tensors; "torch" -> stock torch always
+
+
+def set_backend(name: str):
+    global _BACKEND
+    assert name in ("auto", "torch"), name
+    _BACKEND = name
+
+
+def get_backend() -> str:
+    return _BACKEND
+
+
+@contextlib.contextmanager
+def backend(name: str):
+    old = _BACKEND
+    set_backend(name)
+    try:
+        yield
+    finally:
+        set_backend(old)
+
+
+def _hip(*ts) -> bool:
+    return _BACKEND == "auto" and _lib.use_hip(*ts)
+
+
+def _ops():
+    return _lib.require()
+
+
+# ---------------------------------------------------------------------------
+# LayerNorm / RMSNorm with optional fused residual add
+#   s = x + residual (if residual given);  y = norm(s) * w (+ b)
+#   returns (y, s).  The backward adds the residual-stream gradient (ds from
+#   the next layer) into dx in the same kernel.
+# ---------------------------------------------------------------------------
+class _NormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, eps, rms):
+        shp = x.shape
+        C = shp[-1]
+        x2 = x.reshape(-1, C)
+        r2 = residual.reshape(-1, C) if residual is not None else None
+        y, s, mean, rstd = _ops().norm_fwd(x2, r2, weight, bias, eps, rms)
+        ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.has_bias = bias is not None
+        ctx.has_res = residual is not None
+        ctx.rms = rms
+        ctx.shp = shp
+        if residual is None:
+            return y.view(shp), x  # s is x itself: hand the caller's tensor back
+        return y.view(shp), s.view(shp)
+
+    @staticmethod
+    def backward(ctx, dy, ds):
+        s, weight, mean, rstd = ctx.saved_tensors
+        C = ctx.shp[-1]
+        dy2 = dy.reshape(-1, C).contiguous()
+        ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
+        outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms)
+        dx = outs[0].view(ctx.shp)
+        dw = outs[1]
+        db = outs[2] if ctx.has_bias else None
+        return dx, (dx if ctx.has_res else None), dw, db, None, None
+
+
+def _norm_ref(x, residual, weight, bias, eps, rms):
+    s = x if residual is None else x + residual
+    if _BACKEND == "torch":
+        if rms:
+            y = F.rms_norm(s, (s.shape[-1],), weight, eps)
+        else:
+            y = F.layer_norm(s, (s.shape[-1],), weight, bias, eps)
+        return y, s
+    if rms:
+        y = ref.rms_norm(s, weight, eps)
+    else:
+        y = ref.layer_norm(s, weight, bias, eps)
+    return y, s
+
+
+def layer_norm(x, weight, bias, eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
+    if _hip(x):
+        return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
+                             weight, bias, eps, False)
+    return _norm_ref(x, residual, weight, bias, eps, False)
+
+
+def rms_norm(x, weight, eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
+    if _hip(x):
+        return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
+                             weight, None, eps, True)
+    return _norm_ref(x, residual, weight, None, eps, True)
+
+
+# ---------------------------------------------------------------------------
+# Flash attention on a packed QKV projection output.
+#   qkv: [B, T, (H + 2*Hkv) * D]   ->  out [B, T, H*D]
+# The HIP kernels read Q/K/V straight out of the packed GEMM output (strided
+# views) and write dQ/dK/dV straight into a packed gradient buffer, so no
+# split/cat copies exist on either side of the attention.
+# ---------------------------------------------------------------------------
+def _split_qkv(qkv, H, Hkv, D):
+    B, T, _ = qkv.shape
+    q = qkv[..., : H * D].view(B, T, H, D)
+    k = qkv[..., H * D: (H + Hkv) * D].view(B, T, Hkv, D)
+    v = qkv[..., (H + Hkv) * D:].view(B, T, Hkv, D)
+    return q, k, v
+
+
+class _FlashAttnPacked(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, H, Hkv, causal, scale):
+        B, T, W = qkv.shape
+        D = W // (H + 2 * Hkv)
+        q, k, v = _split_qkv(qkv, H, Hkv, D)
+        o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+        ctx.save_for_backward(qkv, o, lse)
+        ctx.cfg = (H, Hkv, D, causal, scale)
+        return o.view(B, T, H * D)
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, o, lse = ctx.saved_tensors
+        H, Hkv, D, causal, scale = ctx.cfg
+        B, T, _ = qkv.shape
+        q, k, v = _split_qkv(qkv, H, Hkv, D)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = _split_qkv(dqkv, H, Hkv, D)
+        _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale)
+        return dqkv, None, None, None, None
+
+
+class _RopePackedFn(torch.autograd.Function):
+    """Rotate the q and k heads of a packed qkv tensor (rotate-half convention)."""
+
+    @staticmethod
+    def forward(ctx, qkv, cos, sin, H, Hkv):
+        B, T, W = qkv.shape
+        out = _ops().rope(qkv.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, False, False)
+        ctx.save_for_backward(cos, sin)
+        ctx.cfg = (H, Hkv, T)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        cos, sin = ctx.saved_tensors
+        H, Hkv, T = ctx.cfg
+        d = _ops().rope(dout.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, True, False)
+        return d, None, None, None, None
+
+
+def rope_packed(qkv, cos, sin, n_head: int, n_kv_head: int):
+    if _hip(qkv):
+        return _RopePackedFn.apply(qkv, cos, sin, n_head, n_kv_head)
+    B, T, W = qkv.shape
+    D = W // (n_head + 2 * n_kv_head)
+    q, k, v = _split_qkv(qkv, n_head, n_kv_head, D)
+    q = ref.rope(q, cos[:T], sin[:T])
+    k = ref.rope(k, cos[:T], sin[:T])
+    return torch.cat([q.reshape(B, T, -1), k.reshape(B, T, -1), v.reshape(B, T, -1)], -1)
+
+
+def attention_packed(qkv, n_head: int, n_kv_head: int, causal: bool = True, scale: Optional[float] = None,
+                     rope_cos: Optional[torch.Tensor] = None, rope_sin: Optional[torch.Tensor] = None):
+    """Causal self-attention over a packed qkv tensor. RoPE (if cos/sin given) is
+    applied to the q and k heads first (rotate-half convention)."""
+    B, T, W = qkv.shape
+    D = W // (n_head + 2 * n_kv_head)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if rope_cos is not None:
+        qkv = rope_packed(qkv, rope_cos, rope_sin, n_head, n_kv_head)
+    if _hip(qkv):
+        return _FlashAttnPacked.apply(qkv, n_head, n_kv_head, causal, scale)
+    q, k, v = _split_qkv(qkv, n_head, n_kv_head, D)
+    if _BACKEND == "torch" and qkv.is_cuda:
+        # stock-PyTorch baseline path (SDPA), used only by the explicit torch backend
+        qh, kh, vh = (t.transpose(1, 2) for t in (q, k, v))
+        o = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale,
+                                           enable_gqa=(n_kv_head != n_head))
+        return o.transpose(1, 2).reshape(B, T, n_head * D)
+    o, _ = ref.attention(q, k, v, causal=causal, scale=scale)
+    return o.reshape(B, T, n_head * D)
+
+
+def attention(q, k, v, causal: bool = True, scale: Optional[float] = None, return_lse: bool = False):
+    """Unpacked attention q [B,T,H,D], k/v [B,S,Hkv,D] (forward only; used by the
+    KV-cache decode and context-parallel paths).  Queries are aligned to the end
+    of the key sequence."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _hip(q):
+        o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+    else:
+        o, lse = ref.attention(q, k, v, causal=causal, scale=scale)
+    return (o, lse) if return_lse else o
+
+
+# ---------------------------------------------------------------------------
+# activations (op ids of the HIP act kernels: 0 relu, 1 gelu-tanh)
+# ---------------------------------------------------------------------------
+class _GeluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return _ops().act_fwd(x, 1)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        return _ops().act_bwd(dy.contiguous(), x, 1)
+
+
+class _ReluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = _ops().act_fwd(x, 0)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return _ops().act_bwd(dy.contiguous(), y, 0)
+
+
+class _SwigluFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, gu):
+        ctx.save_for_backward(gu)
+        return _ops().swiglu_fwd(gu)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (gu,) = ctx.saved_tensors
+        return _ops().swiglu_bwd(dy.contiguous(), gu)
+
+
+def gelu(x):
+    if _hip(x):
+        return _GeluFn.apply(x.contiguous())
+    if _BACKEND == "torch":
+        return F.gelu(x, approximate="tanh")
+    return ref.gelu_tanh(x)
+
+
+def swiglu(gate_up):
+    if _hip(gate_up):
+        return _SwigluFn.apply(gate_up.contiguous())
+    return ref.swiglu(gate_up)
+
+
+def relu(x):
+    if _hip(x):
+        return _ReluFn.apply(x.contiguous())
+    return ref.relu(x)
+
+
+# ---------------------------------------------------------------------------
+# Embedding (token + optional learned position), deterministic backward
+# ---------------------------------------------------------------------------
+class _EmbeddingFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx, wte, wpe):
+        x = _ops().embedding_fwd(idx, wte, wpe, 0)
+        ctx.save_for_backward(idx)
+        ctx.V = wte.shape[0]
+        ctx.n_pos = 0 if wpe is None else wpe.shape[0]
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (idx,) = ctx.saved_tensors
+        outs = _ops().embedding_bwd(dx.contiguous(), idx, ctx.V, ctx.n_pos, ctx.n_pos > 0)
+        return None, outs[0], (outs[1] if ctx.n_pos > 0 else None)
+
+
+def embedding(idx, wte, wpe=None, pos_offset: int = 0):
+    if _hip(wte):
+        if pos_offset:
+            return _ops().embedding_fwd(idx.contiguous(), wte, wpe, pos_offset)
+        return _EmbeddingFn.apply(idx.contiguous(), wte, wpe)
+    return ref.embedding(idx, wte, wpe, pos_offset)
+
+
+# ---------------------------------------------------------------------------
+# LM head + fused cross entropy.  The HIP kernel computes the per-row loss AND
+# overwrites the logits buffer with d(mean loss)/dlogits in the same pass, so
+# the training step never holds probabilities or a second logits-sized buffer;
+# the backward is two GEMMs on the stored gradient.
+# ---------------------------------------------------------------------------
+class _LMHeadCEFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, weight, bias, targets, ignore_index):
+        logits = F.linear(h, weight, bias)
+        rows = _ops().cross_entropy(logits, targets, logits, ignore_index)
+        n_valid = (targets != ignore_index).sum().clamp_min(1)
+        ctx.save_for_backward(h, weight, logits)
+        ctx.has_bias = bias is not None
+        return rows.sum() / n_valid
+
+    @staticmethod
+    def backward(ctx, dloss):
+        h, weight, dlogits = ctx.saved_tensors
+        g = dloss.to(torch.float32)
+        dh = (dlogits @ weight).mul_(g.to(h.dtype)) if ctx.needs_input_grad[0] else None
+        dw = (dlogits.t() @ h).mul_(g.to(weight.dtype)) if ctx.needs_input_grad[1] else None
+        db = None
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            db = (dlogits.float().sum(0) * g).to(weight.dtype)
+        return dh, dw, db, None, None
+
+
+def lm_head_cross_entropy(h, weight, bias, targets, ignore_index: int = -100):
+    """mean CE of ``h @ weight^T + bias`` against ``targets`` without returning logits."""
+    targets = targets.reshape(-1)
+    h = h.reshape(-1, h.shape[-1])
+    if _hip(h) and torch.is_grad_enabled() and (h.requires_grad or weight.requires_grad):
+        return _LMHeadCEFn.apply(h, weight, bias, targets, ignore_index)
+    logits = F.linear(h, weight, bias)
+    return cross_entropy(logits, targets, ignore_index)
+
+
+def cross_entropy(logits, targets, ignore_index: int = -100):
+    """Mean token cross-entropy over ``logits [N, V]`` (no in-place tricks)."""
+    targets = targets.reshape(-1)
+    if _hip(logits) and not (torch.is_grad_enabled() and logits.requires_grad):
+        rows = _ops().cross_entropy(logits.contiguous(), targets, None, ignore_index)
+        return rows.sum() / (targets != ignore_index).sum().clamp_min(1)
+    return ref.cross_entropy(logits, targets, ignore_index)
+
+
+# ---------------------------------------------------------------------------
+# misc
+# ---------------------------------------------------------------------------
+def rope_cache(seq_len: int, head_dim: int, theta: float, device):
+    cos, sin = ref.rope_cos_sin(seq_len, head_dim, theta, device=device)
+    return cos.contiguous(), sin.contiguous()
+
+
+def apply_rope(x, cos, sin, pos_offset: int = 0):
+    """x [B,T,H,D] -> rotated copy (no autograd; used by decode). cos/sin index from pos_offset."""
+    if _hip(x):
+        B, T, H, D = x.shape
+        y = _ops().rope(x.contiguous().view(B, T, H * D), cos, sin, H, H, T, pos_offset, False, False)
+        return y.view(B, T, H, D)
+    T = x.shape[1]
+    return ref.rope(x, cos[pos_offset:pos_offset + T], sin[pos_offset:pos_offset + T])

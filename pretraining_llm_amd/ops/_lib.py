@@ -1,0 +1,70 @@
+"""Loader for the in-tree gfx950 HIP extension (``pretraining_llm_amd/_C.so``).
+
+The extension is built by ``pretraining_llm_amd/build.py`` with ``hipcc
+--offload-arch=gfx950`` directly (no hipify, no cpp_extension JIT) and
+registers its ops under ``torch.ops.pllm``.
+
+Policy (no silent fallback on a GPU):
+* CUDA(HIP) tensors always go to the HIP kernels.  If the extension is
+  missing when a GPU op is requested, ``require()`` raises.
+* CPU tensors use the pure-PyTorch reference implementation of the same op
+  (which is also the numerics oracle for the tests).
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+_HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SO_PATH = os.path.join(_HERE, "_C.so")
+
+_lock = threading.Lock()
+_loaded = False
+_err: str | None = None
+
+
+def load(raise_on_error: bool = False) -> bool:
+    global _loaded, _err
+    if _loaded:
+        return True
+    with _lock:
+        if _loaded:
+            return True
+        if not os.path.exists(SO_PATH):
+            _err = f"HIP extension not built: {SO_PATH} missing (run `python -m pretraining_llm_amd.build`)"
+        else:
+            try:
+                torch.ops.load_library(SO_PATH)
+                _loaded = True
+                _err = None
+            except Exception as e:  # pragma: no cover - depends on the box
+                _err = f"failed to load {SO_PATH}: {e}"
+        if not _loaded and raise_on_error:
+            raise RuntimeError(_err)
+        return _loaded
+
+
+def available() -> bool:
+    return load(False)
+
+
+def require():
+    """Return the op namespace, raising loudly if the extension is unavailable."""
+    if not _loaded:
+        load(raise_on_error=True)
+    return torch.ops.pllm
+
+
+def use_hip(*tensors) -> bool:
+    """True when the op must run on the HIP kernels (any CUDA/HIP tensor)."""
+    for t in tensors:
+        if isinstance(t, torch.Tensor) and t.is_cuda:
+            return True
+    return False
+
+
+def error() -> str | None:
+    load(False)
+    return _err

@@ -1,0 +1,164 @@
+"""Data-parallel gradient engine on RCCL (torch.distributed backend "nccl" on ROCm).
+
+Reference: ``DDP(model, device_ids=[local_rank])`` (scripts/train_transformer.py:122-123)
+with default 25 MiB buckets, a constant-buffer broadcast every other forward
+ and a sync toggle that skipped the all-reduce on odd steps
+while still stepping the optimizer (defect D5: replicas diverge).
+
+This engine instead:
+* works on the optimizer's flat gradient buffer (``FlatAdamW.flat_grad``), so a
+  bucket is a contiguous slice -> zero packing copies, one RCCL call per bucket;
+* forms buckets in REVERSE layout order (backward produces the last layers'
+  gradients first) with a small first bucket so communication starts early, and
+  launches each bucket from a post-accumulate-grad hook as soon as all its
+  parameters are ready, strictly in bucket order (identical collective order on
+  every rank), so the all-reduces run on RCCL's stream under the rest of the
+  backward;
+* sizes buckets for xGMI: each MI355X has 7 point-to-point links (~153 GB/s
+  each); a ring all-reduce moves 2(n-1)/n * S per GPU, so buckets of 32-64 MiB
+  keep per-call latency (tens of us) < 5% of transfer time while leaving
+  several buckets to pipeline behind the backward;
+* never reduces buffers (there are no mask buffers to broadcast), broadcasts
+  parameters once at construction (one flat collective), and leaves the
+  1/world averaging to the optimizer's gradient scale (no extra pass);
+* ``no_sync()`` gives correct gradient accumulation (sync only on the last
+  micro-step).
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class DataParallelEngine:
+    def __init__(self, optimizer, process_group=None, bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
+                 broadcast_params: bool = True, overlap: bool = True):
+        self.opt = optimizer
+        self.pg = process_group
+        self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.overlap = overlap
+        self.enabled = True
+        self._handles = []
+        self._hooks = []
+        flat = optimizer.flat_grad
+        esz = flat.element_size()
+        params = optimizer.params
+        # layout order of params by offset
+        order = sorted(range(len(params)), key=lambda i: optimizer.offsets[i])
+        # buckets: walk from the END of the flat buffer backwards
+        self.buckets: List[dict] = []
+        cap = int(first_bucket_mb * 2 ** 20)
+        cur: List[int] = []
+        cur_bytes = 0
+        for i in reversed(order):
+            nbytes = params[i].numel() * esz
+            cur.append(i)
+            cur_bytes += nbytes
+            if cur_bytes >= cap:
+                self._close_bucket(cur)
+                cur, cur_bytes = [], 0
+                cap = int(bucket_mb * 2 ** 20)
+        if cur:
+            self._close_bucket(cur)
+        self.param_bucket = {}
+        for b, bk in enumerate(self.buckets):
+            for i in bk["params"]:
+                self.param_bucket[i] = b
+        self._reset_counters()
+        if broadcast_params and self.world > 1:
+            dist.broadcast(optimizer.flat_param, src=self._global_src(), group=process_group)
+            optimizer.sync_master_from_params()
+        if self.world > 1 and overlap:
+            for i, p in enumerate(params):
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+
+    def _global_src(self):
+        if self.pg is None:
+            return 0
+        return dist.get_global_rank(self.pg, 0)
+
+    def _close_bucket(self, idx: List[int]):
+        opt = self.opt
+        starts = [opt.offsets[i] for i in idx]
+        ends = [opt.offsets[i] + opt.params[i].numel() for i in idx]
+        s = min(starts)
+        # extend to the aligned end of the last param segment so the bucket tiles the buffer
+        e = max(ends)
+        self.buckets.append({"params": list(idx), "start": s, "end": e})
+
+    def _reset_counters(self):
+        self._pending = [len(b["params"]) for b in self.buckets]
+        self._next_launch = 0
+        self._handles = []
+
+    def _make_hook(self, i):
+        def hook(p):
+            if not self.enabled:
+                return
+            b = self.param_bucket[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._launch_ready()
+        return hook
+
+    def _launch(self, b):
+        bk = self.buckets[b]
+        view = self.opt.flat_grad[bk["start"]:bk["end"]]
+        self._handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
+
+    def _launch_ready(self):
+        while self._next_launch < len(self.buckets) and self._pending[self._next_launch] == 0:
+            self._launch(self._next_launch)
+            self._next_launch += 1
+
+    # ------------------------------------------------------------------
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.enabled
+        self.enabled = False
+        try:
+            yield
+        finally:
+            self.enabled = old
+
+    def finish_grad_sync(self):
+        """Launch any bucket not yet launched (unused params, no-overlap mode) and wait for all.
+        Returns the gradient scale the optimizer must apply (1/world)."""
+        if self.world > 1:
+            while self._next_launch < len(self.buckets):
+                self._launch(self._next_launch)
+                self._next_launch += 1
+            for h in self._handles:
+                h.wait()
+        self._reset_counters()
+        return 1.0 / self.world
+
+    def bucket_sizes_mb(self):
+        esz = self.opt.flat_grad.element_size()
+        return [(b["end"] - b["start"]) * esz / 2 ** 20 for b in self.buckets]
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+
+
+def all_reduce_mean(t: torch.Tensor, group=None) -> torch.Tensor:
+    """Mean of a (scalar) tensor over ranks; identity when not distributed."""
+    if dist.is_initialized() and dist.get_world_size(group) > 1:
+        t = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        t /= dist.get_world_size(group)
+    return t
+
+
+@torch.no_grad()
+def params_checksum(params) -> torch.Tensor:
+    """fp64 checksum of all parameters (cross-rank replica-consistency check, catches SURVEY D5)."""
+    s = torch.zeros((), dtype=torch.float64, device=params[0].device)
+    for i, p in enumerate(params):
+        s += p.double().sum() * (1.0 + 1e-3 * (i % 97))
+    return s

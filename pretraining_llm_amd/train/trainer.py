@@ -1,0 +1,247 @@
+"""Trainer: data-parallel bf16 pretraining loop on the gfx950 kernels.
+
+Reference: scripts/train_transformer.py:35-109 (``Trainer``: LR warmup 10 % then
+constant, bf16 autocast, GradScaler, DDP with an every-other-step sync toggle,
+rank-0-only eval through the DDP wrapper, end-of-run save).
+
+Same semantics where they were intended, fixed where they were defects
+(SURVEY.md §8):
+* LR: linear warmup over ``warmup_frac`` (0.1) of ``t_train_steps`` then
+  constant (``lr_schedule='ref'``); ``'step'`` uses the reference's unused
+  ``t_lr_decay_step``/``t_lr_decayed`` keys; ``'cosine'`` decays to ``t_lr_decayed``;
+* gradient accumulation syncs once per optimizer step, never skips a sync (D5);
+* evaluation runs on ALL ranks on their own shard and the loss is all-reduced (D11);
+* logged train loss is the all-reduced mean over the log window (D16);
+* periodic atomic checkpoints + resume (model, optimizer incl. fp32 master,
+  step, data position, RNG); unwrapped keys (D7), directories created (D8);
+* NaN/inf loss guard; tokens/s and MFU in every log line.
+"""
+from __future__ import annotations
+
+import contextlib
+import math
+import os
+import time
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+from ..data import TokenLoader, ensure_synthetic_shard
+from ..models import GPT, ModelConfig, get_preset
+from ..parallel.dp import DataParallelEngine, all_reduce_mean
+from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from ..utils.dist import DistInfo, init_distributed
+from ..utils.metrics import MetricsLogger, mfu, peak_memory_gb
+from .optim import FlatAdamW, no_decay_1d
+
+
+def model_config_from(cfg: dict) -> ModelConfig:
+    preset = cfg.get("model_preset")
+    dims = {k: cfg[k] for k in ("vocab_size", "context_length", "n_embed", "n_head", "n_blocks") if k in cfg}
+    extra = {k: cfg[k] for k in ("n_kv_head", "ffn_hidden", "activation_checkpointing") if cfg.get(k) is not None}
+    if preset:
+        mc = get_preset(preset)
+        over = {k: v for k, v in {**dims, **extra}.items() if cfg.get("override_preset_dims", False) or k in extra}
+        return mc.replace(**over) if over else mc
+    from ..models.config import _ref
+    return _ref(**dims, **extra)
+
+
+def lr_at(step: int, cfg: dict) -> float:
+    total = cfg["t_train_steps"]
+    lr = cfg["t_lr"]
+    warm = cfg.get("warmup_steps")
+    if warm is None:
+        warm = total * cfg.get("warmup_frac", 0.1)
+    if warm > 0 and step < warm:
+        return lr * step / warm
+    sched = cfg.get("lr_schedule", "ref")
+    if sched == "step":
+        return cfg.get("t_lr_decayed", lr) if step >= cfg.get("t_lr_decay_step", total) else lr
+    if sched == "cosine":
+        lo = cfg.get("t_lr_decayed", 0.1 * lr)
+        frac = min(1.0, (step - warm) / max(1.0, total - warm))
+        return lo + 0.5 * (lr - lo) * (1 + math.cos(math.pi * frac))
+    return lr
+
+
+class Trainer:
+    def __init__(self, cfg: dict, dist_info: Optional[DistInfo] = None, log=print):
+        self.cfg = dict(cfg)
+        self.log = log
+        self.di = dist_info or init_distributed(self.cfg.get("ddp_backend", "auto"), self.cfg.get("device", "auto"))
+        self.device = self.di.device
+        seed = int(self.cfg.get("seed", 1337))
+        torch.manual_seed(seed)  # identical init on every rank (then broadcast for certainty)
+        self.mcfg = model_config_from(self.cfg)
+        self.seq_len = int(self.cfg.get("seq_len") or self.mcfg.context_length)
+        dtype_name = self.cfg.get("dtype", "bfloat16")
+        if self.device.type == "cpu" and not self.cfg.get("cpu_bf16", False):
+            self.dtype = torch.float32
+        else:
+            self.dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}[dtype_name]
+        self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
+        decay_filter = None if self.cfg.get("weight_decay_all", True) else no_decay_1d
+        self.opt = FlatAdamW(self.model, lr=self.cfg["t_lr"], betas=tuple(self.cfg.get("betas", (0.9, 0.999))),
+                             eps=self.cfg.get("eps", 1e-8), weight_decay=self.cfg.get("weight_decay", 0.01),
+                             decay_filter=decay_filter, max_grad_norm=self.cfg.get("max_grad_norm", 0.0))
+        self.engine = DataParallelEngine(self.opt, bucket_mb=self.cfg.get("bucket_mb", 64.0),
+                                         first_bucket_mb=self.cfg.get("first_bucket_mb", 4.0))
+        self.accum = int(self.cfg.get("grad_accum_steps", 1))
+        self.step = 0
+        self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
+        self.train_loader = self._loader(self.cfg["train_path"], seed, 0)
+        vp = self.cfg.get("val_path") or self.cfg.get("dev_path")
+        self.val_loader = self._loader(vp, seed + 1, 0, stream=1) if vp else None
+        self.flops_per_token = self.mcfg.flops_per_token(self.seq_len)
+        if self.cfg.get("resume"):
+            self.resume(self.cfg["resume"])
+
+    # ------------------------------------------------------------------
+    def _loader(self, path: str, seed: int, start: int, stream: int = 0):
+        if self.cfg.get("synthetic_data", False) or not os.path.exists(path):
+            if not self.cfg.get("synthetic_data", False) and not self.cfg.get("allow_synthetic", True):
+                raise FileNotFoundError(path)
+            n = int(self.cfg.get("synthetic_tokens", 2_000_000))
+            syn = self.cfg.get("synthetic_dir", "data/synthetic")
+            path = os.path.join(syn, f"{os.path.basename(path) or 'tokens'}.{self.mcfg.vocab_size}.{n}.bin")
+            if self.di.is_master:
+                ensure_synthetic_shard(path, n, self.mcfg.vocab_size, seed=int(self.cfg.get("seed", 1337)),
+                                       stream=stream)
+            if dist.is_initialized():
+                dist.barrier()
+        return TokenLoader(path, self.cfg["t_batch_size"], self.seq_len, self.di.rank,
+                           self.di.world_size, seed=seed, start_batch=start, device=self.device)
+
+    def lr(self, step: int) -> float:
+        return lr_at(step, self.cfg)
+
+    # ------------------------------------------------------------------
+    def train_step(self) -> torch.Tensor:
+        """One optimizer step (``grad_accum_steps`` micro-batches). Returns the mean loss (device tensor)."""
+        lr = self.lr(self.step)
+        self.opt.param_groups[0]["lr"] = lr
+        total = torch.zeros((), device=self.device, dtype=torch.float32)
+        for micro in range(self.accum):
+            x, y = self.train_loader.next()
+            ctx = self.engine.no_sync() if micro < self.accum - 1 else contextlib.nullcontext()
+            with ctx:
+                _, loss = self.model(x, y, return_logits=False)
+                loss.backward()
+            total += loss.detach().float()
+        scale = self.engine.finish_grad_sync()
+        self.opt.step(grad_scale=scale / self.accum)
+        self.opt.zero_grad()
+        self.step += 1
+        return total / self.accum
+
+    @torch.no_grad()
+    def evaluate(self, iters: Optional[int] = None) -> float:
+        if self.val_loader is None:
+            return float("nan")
+        iters = iters or int(self.cfg.get("t_eval_iters", 250))
+        self.model.eval()
+        acc = torch.zeros((), device=self.device, dtype=torch.float32)
+        for _ in range(iters):
+            x, y = self.val_loader.next()
+            _, loss = self.model(x, y, return_logits=False)
+            acc += loss.float()
+        self.model.train()
+        return float(all_reduce_mean(acc / iters))
+
+    def train(self, steps: Optional[int] = None):
+        cfg = self.cfg
+        total = steps if steps is not None else cfg["t_train_steps"]
+        log_every = int(cfg.get("log_interval", cfg.get("t_eval_steps", 1000)))
+        eval_every = int(cfg.get("t_eval_steps", 1000))
+        ckpt_every = int(cfg.get("ckpt_interval", 0))
+        tokens_per_step = cfg["t_batch_size"] * self.seq_len * self.accum * self.di.world_size
+        self.model.train()
+        window_loss = torch.zeros((), device=self.device)
+        window_n = 0
+        t0 = time.perf_counter()
+        window_steps = 0
+        last_val = float("nan")
+        while self.step < total:
+            step = self.step
+            do_eval = self.val_loader is not None and eval_every > 0 and step % eval_every == 0 and (
+                step > 0 or cfg.get("eval_at_start", True))
+            if do_eval:
+                last_val = self.evaluate()
+            loss = self.train_step()
+            window_loss += loss
+            window_n += 1
+            window_steps += 1
+            if (step % log_every == 0) or self.step == total:
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                dt = time.perf_counter() - t0
+                tl = float(all_reduce_mean(window_loss / max(1, window_n)))
+                if not math.isfinite(tl):
+                    raise FloatingPointError(f"non-finite training loss {tl} at step {step}")
+                tps = tokens_per_step * window_steps / max(dt, 1e-9)
+                rec = {"step": step, "train_loss": tl, "val_loss": last_val, "lr": self.opt.lr,
+                       "step_ms": 1000 * dt / max(1, window_steps), "tokens_per_s": tps,
+                       "tokens_per_s_per_gpu": tps / self.di.world_size,
+                       "mfu": mfu(tps / self.di.world_size, self.flops_per_token),
+                       "peak_mem_gb": peak_memory_gb(self.device)}
+                if self.opt.last_grad_norm is not None:
+                    rec["grad_norm"] = float(self.opt.last_grad_norm)
+                if self.di.is_master:
+                    self.log(f"Step {step}: Train Loss={tl:.4f}, Val Loss={last_val:.4f}, LR={self.opt.lr:.2e}, "
+                             f"Time={dt * 1000:.2f}ms, tok/s={tps:,.0f}, MFU={rec['mfu'] * 100:.1f}%")
+                self.metrics.log(rec)
+                window_loss.zero_()
+                window_n = 0
+                window_steps = 0
+                t0 = time.perf_counter()
+            if ckpt_every and self.step % ckpt_every == 0 and self.step < total:
+                self.save(self._ckpt_path(periodic=True))
+        out = cfg.get("t_out_path")
+        if out:
+            self.save(out)
+        return self
+
+    # ------------------------------------------------------------------
+    def _ckpt_path(self, periodic=False):
+        out = self.cfg.get("t_out_path", "models/transformer_B.pt")
+        if not periodic:
+            return out
+        root, ext = os.path.splitext(out)
+        return f"{root}.latest{ext or '.pt'}"
+
+    def save(self, path: str):
+        data_state = {"train_batches": self.train_loader.batches_consumed,
+                      "val_batches": self.val_loader.batches_consumed if self.val_loader else 0}
+        if self.di.is_master:
+            save_checkpoint(path, self.model, self.opt, step=self.step, config=self.cfg, data_state=data_state)
+            self.log(f"saved checkpoint to {path} (step {self.step})")
+        if dist.is_initialized():
+            dist.barrier()
+
+    def resume(self, path: str):
+        if path == "auto":
+            path = self._ckpt_path(periodic=True)
+            if not os.path.exists(path):
+                return
+        ck = load_checkpoint(path, map_location="cpu")
+        missing, unexpected = self.model.load_state_dict(ck["model_state_dict"], strict=False)
+        missing = [k for k in missing if not k.endswith("pos_idxs")]
+        if missing or unexpected:
+            raise RuntimeError(f"checkpoint mismatch: missing={missing} unexpected={unexpected}")
+        self.opt.sync_master_from_params()
+        if "optimizer_state_dict" in ck:
+            self.opt.load_state_dict(ck["optimizer_state_dict"])
+        self.step = int(ck.get("step", 0))
+        ds = ck.get("data_state", {})
+        seed = int(self.cfg.get("seed", 1337))
+        self.train_loader.close()
+        self.train_loader = self._loader(self.cfg["train_path"], seed, int(ds.get("train_batches", 0)))
+        if self.val_loader is not None:
+            vp = self.cfg.get("val_path") or self.cfg.get("dev_path")
+            self.val_loader.close()
+            self.val_loader = self._loader(vp, seed + 1, int(ds.get("val_batches", 0)), stream=1)
+        if self.di.is_master:
+            self.log(f"resumed from {path} at step {self.step}")

@@ -1,0 +1,300 @@
+"""Numerics of every gfx950 HIP kernel against a plain PyTorch fp32 reference of the same op.
+
+All tests here need the MI355X and the in-tree extension (``pretraining_llm_amd/_C.so``);
+they fail loudly if the extension is missing (no silent fallback)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext():
+    from pretraining_llm_amd.ops import _lib
+    _lib.require()
+    yield
+
+
+def _ops():
+    return torch.ops.pllm
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+# ----------------------------------------------------------------- norms
+@pytest.mark.parametrize("C", [128, 768, 1024, 2048])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_norm_fwd_bwd(C, rms, with_res):
+    from pretraining_llm_amd import ops
+    torch.manual_seed(0)
+    N = 517
+    x = torch.randn(N, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    r = torch.randn(N, C, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_res else None
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    b = None if rms else (0.1 * torch.randn(C, device=DEV)).bfloat16().requires_grad_()
+    fn = ops.rms_norm if rms else ops.layer_norm
+    if rms:
+        y, s = fn(x, w, 1e-5, r)
+    else:
+        y, s = fn(x, w, b, 1e-5, r)
+    dy = torch.randn_like(y)
+    ds = torch.randn_like(s) if with_res else None
+    outs = [y] + ([s] if with_res else [])
+    grads = [dy] + ([ds] if with_res else [])
+    torch.autograd.backward(outs, grads)
+    # fp32 reference
+    xf = x.detach().float().requires_grad_()
+    rf = r.detach().float().requires_grad_() if with_res else None
+    wf = w.detach().float().requires_grad_()
+    bf = b.detach().float().requires_grad_() if b is not None else None
+    sf = xf + rf if with_res else xf
+    sq = sf.to(torch.bfloat16).float() if with_res else sf  # kernel normalises the bf16-rounded sum
+    if rms:
+        yf = sq * torch.rsqrt(sq.pow(2).mean(-1, keepdim=True) + 1e-5) * wf
+    else:
+        yf = F.layer_norm(sq, (C,), wf, bf, 1e-5)
+    of = [yf] + ([sf] if with_res else [])
+    torch.autograd.backward(of, [g.float() for g in grads])
+    assert _rel(y, yf) < 1e-2
+    assert _rel(x.grad, xf.grad) < 2e-2
+    assert _rel(w.grad, wf.grad) < 2e-2
+    if b is not None:
+        assert _rel(b.grad, bf.grad) < 2e-2
+    if with_res:
+        assert _rel(s, sf) < 1e-2
+        assert _rel(r.grad, rf.grad) < 2e-2
+
+
+# ----------------------------------------------------------------- activations
+@pytest.mark.parametrize("kind", ["gelu", "relu"])
+def test_activation(kind):
+    from pretraining_llm_amd import ops
+    torch.manual_seed(1)
+    x = torch.randn(333, 3072, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = getattr(ops, kind)(x)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xf = x.detach().float().requires_grad_()
+    yf = F.gelu(xf, approximate="tanh") if kind == "gelu" else torch.relu(xf)
+    yf.backward(dy.float())
+    assert _rel(y, yf) < 1e-2
+    assert _rel(x.grad, xf.grad) < 1e-2
+
+
+def test_swiglu():
+    from pretraining_llm_amd import ops
+    torch.manual_seed(2)
+    gu = torch.randn(129, 2 * 688, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    y = ops.swiglu(gu)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    gf = gu.detach().float().requires_grad_()
+    g, u = gf.chunk(2, -1)
+    yf = F.silu(g) * u
+    yf.backward(dy.float())
+    assert _rel(y, yf) < 1e-2
+    assert _rel(gu.grad, gf.grad) < 1e-2
+
+
+def test_rope_packed_roundtrip():
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.ops import reference as ref
+    torch.manual_seed(3)
+    B, T, H, Hkv, D = 2, 64, 4, 2, 128
+    qkv = torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    cos, sin = ops.rope_cache(T, D, 10000.0, DEV)
+    out = ops.rope_packed(qkv, cos, sin, H, Hkv)
+    q, k, v = ops._split_qkv(qkv.detach().float(), H, Hkv, D)
+    qr, kr = ref.rope(q, cos, sin), ref.rope(k, cos, sin)
+    exp = torch.cat([qr.reshape(B, T, -1), kr.reshape(B, T, -1), v.reshape(B, T, -1)], -1)
+    assert _rel(out, exp) < 1e-2
+    g = torch.randn_like(out)
+    out.backward(g)
+    qkvf = qkv.detach().float().requires_grad_()
+    q2, k2, v2 = ops._split_qkv(qkvf, H, Hkv, D)
+    e2 = torch.cat([ref.rope(q2, cos, sin).reshape(B, T, -1), ref.rope(k2, cos, sin).reshape(B, T, -1),
+                    v2.reshape(B, T, -1)], -1)
+    e2.backward(g.float())
+    assert _rel(qkv.grad, qkvf.grad) < 1e-2
+
+
+# ----------------------------------------------------------------- cross entropy
+@pytest.mark.parametrize("V", [50304, 32000, 512])
+def test_cross_entropy_fused(V):
+    from pretraining_llm_amd import ops
+    torch.manual_seed(4)
+    N, C = 300, 256
+    h = (torch.randn(N, C, device=DEV) * 0.5).bfloat16().requires_grad_()
+    W = (torch.randn(V, C, device=DEV) * 0.05).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=DEV)
+    t[::7] = -100
+    loss = ops.lm_head_cross_entropy(h, W, None, t)
+    loss.backward()
+    hf, Wf = h.detach().float().requires_grad_(), W.detach().float().requires_grad_()
+    logits = (hf @ Wf.t()).bfloat16().float()
+    lf = F.cross_entropy(logits, t, ignore_index=-100)
+    lf.backward()
+    assert abs(loss.item() - lf.item()) < 2e-3 * max(1.0, lf.item())
+    assert _rel(h.grad, hf.grad) < 3e-2
+    assert _rel(W.grad, Wf.grad) < 3e-2
+    # forward-only path
+    with torch.no_grad():
+        l2 = ops.cross_entropy(logits.bfloat16(), t)
+    assert abs(l2.item() - lf.item()) < 2e-3 * max(1.0, lf.item())
+
+
+# ----------------------------------------------------------------- embedding
+@pytest.mark.parametrize("with_pos", [True, False])
+def test_embedding(with_pos):
+    from pretraining_llm_amd import ops
+    torch.manual_seed(5)
+    V, C, B, T = 1000, 256, 4, 96
+    wte = torch.randn(V, C, device=DEV, dtype=torch.bfloat16, requires_grad=True)
+    wpe = torch.randn(T, C, device=DEV, dtype=torch.bfloat16, requires_grad=True) if with_pos else None
+    idx = torch.randint(0, 50, (B, T), device=DEV)  # many repeats -> exercises the segmented sum
+    x = ops.embedding(idx, wte, wpe)
+    dx = torch.randn_like(x)
+    x.backward(dx)
+    wtef = wte.detach().float().requires_grad_()
+    wpef = wpe.detach().float().requires_grad_() if with_pos else None
+    xf = F.embedding(idx, wtef) + (wpef[:T] if with_pos else 0)
+    xf.backward(dx.float())
+    assert _rel(x, xf) < 1e-2
+    assert _rel(wte.grad, wtef.grad) < 1e-2
+    if with_pos:
+        assert _rel(wpe.grad, wpef.grad) < 1e-2
+    # determinism: same inputs, same bits
+    wte.grad = None
+    x2 = ops.embedding(idx, wte, wpe)
+    x2.backward(dx)
+    g1 = wte.grad.clone()
+    wte.grad = None
+    x3 = ops.embedding(idx, wte, wpe)
+    x3.backward(dx)
+    assert torch.equal(g1, wte.grad)
+
+
+# ----------------------------------------------------------------- AdamW
+def test_adamw_flat_matches_torch():
+    torch.manual_seed(6)
+    n = 4096 + 64
+    p32 = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV).bfloat16()
+    ref_p = p32.clone().requires_grad_()
+    opt = torch.optim.AdamW([ref_p], lr=1e-2, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01)
+    master, m, v = p32.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    pb = p32.bfloat16()
+    for step in range(1, 4):
+        ref_p.grad = g.float() * 0.5
+        opt.step()
+        torch.ops.pllm.adamw_(pb, master, m, v, g, 1e-2, 0.9, 0.999, 1e-8, 0.01, step, 0.5, None, None)
+    torch.cuda.synchronize()
+    assert _rel(master, ref_p.detach()) < 1e-5
+    assert _rel(pb, ref_p.detach()) < 1e-2
+
+
+def test_sumsq():
+    x = torch.randn(1 << 20, device=DEV).bfloat16()
+    s = torch.ops.pllm.sumsq(x)
+    assert abs(s.item() - x.float().pow(2).sum().item()) / x.float().pow(2).sum().item() < 1e-4
+
+
+# ----------------------------------------------------------------- attention
+def _attn_ref(q, k, v, causal, scale):
+    B, T, H, D = q.shape
+    S, Hkv = k.shape[1], k.shape[2]
+    qf, kf, vf = (t.float().transpose(1, 2) for t in (q, k, v))
+    if Hkv != H:
+        kf = kf.repeat_interleave(H // Hkv, 1)
+        vf = vf.repeat_interleave(H // Hkv, 1)
+    s = qf @ kf.transpose(-1, -2) * scale
+    if causal:
+        mask = torch.ones(T, S, dtype=torch.bool, device=q.device).tril(S - T)
+        s = s.masked_fill(~mask, float("-inf"))
+    p = torch.softmax(s, -1)
+    return (p @ vf).transpose(1, 2), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("T", [128, 200, 1024])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_fwd(D, T, causal):
+    torch.manual_seed(7)
+    B, H = 2, 4
+    q = torch.randn(B, T, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, T, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, T, H, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    o, lse = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
+    oref, lref = _attn_ref(q, k, v, causal, scale)
+    assert _rel(o, oref) < 1e-2, _rel(o, oref)
+    assert (lse - lref).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("T", [128, 192, 512])
+@pytest.mark.parametrize("gqa", [1, 2])
+def test_attention_packed_fwd_bwd(D, T, gqa):
+    from pretraining_llm_amd import ops
+    torch.manual_seed(8)
+    B, H = 2, 4
+    Hkv = H // gqa
+    qkv = (torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV) * 0.7).bfloat16().requires_grad_()
+    o = ops.attention_packed(qkv, H, Hkv, causal=True)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qkvf = qkv.detach().float().requires_grad_()
+    q, k, v = ops._split_qkv(qkvf, H, Hkv, D)
+    of, _ = _attn_ref(q, k, v, True, 1 / math.sqrt(D))
+    of = of.reshape(B, T, H * D)
+    of.backward(do.float())
+    assert _rel(o, of) < 1e-2
+    assert _rel(qkv.grad, qkvf.grad) < 2.5e-2, _rel(qkv.grad, qkvf.grad)
+    # per-part check so a wrong dq/dk/dv cannot hide in the packed norm
+    gq, gk, gv = ops._split_qkv(qkv.grad, H, Hkv, D)
+    rq, rk, rv = ops._split_qkv(qkvf.grad, H, Hkv, D)
+    for a, b in ((gq, rq), (gk, rk), (gv, rv)):
+        assert _rel(a, b) < 3e-2
+
+
+def test_attention_decode_alignment():
+    """T < S (KV-cache decode): queries aligned to the end of the keys."""
+    torch.manual_seed(9)
+    B, H, D, S = 2, 4, 64, 300
+    q = torch.randn(B, 1, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, H, D, device=DEV, dtype=torch.bfloat16)
+    o, _ = torch.ops.pllm.attn_fwd(q, k, v, True, 1 / math.sqrt(D))
+    oref, _ = _attn_ref(q, k, v, True, 1 / math.sqrt(D))
+    assert _rel(o, oref) < 1e-2
+
+
+# ----------------------------------------------------------------- whole model
+def test_model_hip_matches_reference_path():
+    """One GPT-2-tiny forward/backward on the HIP kernels vs the same model on stock torch ops."""
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.models import GPT, get_preset
+    torch.manual_seed(10)
+    cfg = get_preset("gpt2-tiny").replace(context_length=128)
+    m = GPT(cfg).to(DEV, torch.bfloat16)
+    x = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV)
+    y = torch.randint(0, cfg.vocab_size, (2, 128), device=DEV)
+    _, l1 = m(x, y, return_logits=False)
+    l1.backward()
+    g1 = {n: p.grad.float().clone() for n, p in m.named_parameters()}
+    m.zero_grad()
+    with ops.backend("torch"):
+        _, l2 = m(x, y)
+        l2.backward()
+    assert abs(l1.item() - l2.item()) < 2e-2
+    for n, p in m.named_parameters():
+        assert _rel(g1[n], p.grad) < 6e-2, n
