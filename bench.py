@@ -106,7 +106,7 @@ def main(argv=None):
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    final_loss = float(loss)
+    final_loss = float(loss.detach())
     if dist.is_initialized():
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

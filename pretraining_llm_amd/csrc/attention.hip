@@ -485,32 +485,35 @@ __global__ __launch_bounds__(256) void attn_dq_convert_kernel(AttnBwdArgs a) {
 
 namespace pllm {
 
-bool attn_supported_head_dim(int D) { return D == 64 || D == 128; }
+bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
+
+template <int D>
+static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
+  const int nqb = (a.T + 127) / 128;
+  hipLaunchKernelGGL(attn_fwd_kernel<D>, dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
+}
+
+template <int D>
+static void attn_bwd_t(const AttnBwdArgs& a, hipStream_t st) {
+  const int64_t nrows = (int64_t)a.B * a.T * a.H;
+  const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
+  const int nkb = (a.S + 127) / 128;
+  (void)hipMemsetAsync(a.dq_acc, 0, (size_t)nrows * D * sizeof(float), st);
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_kernel<D>, dim3(nkb * a.B * a.Hkv), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_dq_convert_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+}
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
-  const int nqb = (a.T + 127) / 128;
-  dim3 grid(nqb * a.B * a.H), block(256);
-  if (a.D == 64)
-    hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, block, 0, st, a);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<128>, grid, block, 0, st, a);
+  if (a.D == 32) attn_fwd_t<32>(a, st);
+  else if (a.D == 64) attn_fwd_t<64>(a, st);
+  else attn_fwd_t<128>(a, st);
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
-  const int64_t nrows = (int64_t)a.B * a.T * a.H;
-  const int CPR = a.D / 8;
-  const int pre_grid = (int)((nrows * CPR + 255) / 256);
-  const int nkb = (a.S + 127) / 128;
-  (void)hipMemsetAsync(a.dq_acc, 0, (size_t)nrows * a.D * sizeof(float), st);
-  if (a.D == 64) {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<64>, dim3(pre_grid), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwd_kernel<64>, dim3(nkb * a.B * a.Hkv), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_dq_convert_kernel<64>, dim3(pre_grid), dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(attn_bwd_pre_kernel<128>, dim3(pre_grid), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_bwd_kernel<128>, dim3(nkb * a.B * a.Hkv), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(attn_dq_convert_kernel<128>, dim3(pre_grid), dim3(256), 0, st, a);
-  }
+  if (a.D == 32) attn_bwd_t<32>(a, st);
+  else if (a.D == 64) attn_bwd_t<64>(a, st);
+  else attn_bwd_t<128>(a, st);
 }
 
 }  // namespace pllm

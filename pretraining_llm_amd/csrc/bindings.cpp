@@ -288,7 +288,7 @@ void check_head_view(const Tensor& t, const char* name, int64_t D) {
 
 std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal, double scale) {
   const int64_t D = q.size(3);
-  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 64 or 128, got ", D);
+  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128, got ", D);
   check_head_view(q, "q", D);
   check_head_view(k, "k", D);
   check_head_view(v, "v", D);
@@ -320,7 +320,7 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
               Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale) {
   const int64_t D = q.size(3);
-  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 64 or 128");
+  TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128");
   for (auto& pr : std::vector<std::pair<const Tensor*, const char*>>{
            {&dout, "dout"}, {&q, "q"}, {&k, "k"}, {&v, "v"}, {&o, "o"}, {&dq, "dq"}, {&dk, "dk"}, {&dv, "dv"}})
     check_head_view(*pr.first, pr.second, D);
