@@ -62,8 +62,11 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const std::optional<Tensor>& res, 
   return {y, s, mean, rstd};
 }
 
+// dw_acc/db_acc: if given, the weight/bias gradients are ADDED into these (e.g. views of
+// the optimizer's flat gradient buffer) and only dx is returned.
 std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& mean,
-                             const Tensor& rstd, const std::optional<Tensor>& ds, bool has_bias, bool rms) {
+                             const Tensor& rstd, const std::optional<Tensor>& ds, bool has_bias, bool rms,
+                             const std::optional<Tensor>& dw_acc, const std::optional<Tensor>& db_acc) {
   check_bf16(dy, "dy");
   check_bf16(s, "s");
   check_contig(dy, "dy");
@@ -75,9 +78,19 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
     check_contig(*ds, "ds");
     TORCH_CHECK(ds->sizes() == dy.sizes(), "ds shape");
   }
+  const bool acc = dw_acc.has_value();
+  TORCH_CHECK(!has_bias || acc == db_acc.has_value(), "norm_bwd: dw_acc and db_acc must be given together");
+  if (acc) {
+    check_bf16(*dw_acc, "dw_acc");
+    TORCH_CHECK(dw_acc->numel() == C && dw_acc->is_contiguous(), "dw_acc shape");
+    if (has_bias) {
+      check_bf16(*db_acc, "db_acc");
+      TORCH_CHECK(db_acc->numel() == C && db_acc->is_contiguous(), "db_acc shape");
+    }
+  }
   Tensor dx = at::empty_like(dy);
-  Tensor dw = at::empty({C}, w.options());
-  Tensor db = has_bias ? at::empty({C}, w.options()) : Tensor();
+  Tensor dw = acc ? *dw_acc : at::zeros({C}, w.options());
+  Tensor db = has_bias ? (acc ? *db_acc : at::zeros({C}, w.options())) : Tensor();
   const int G = pllm::norm_bwd_grid((int)N);
   auto f32 = dy.options().dtype(at::kFloat);
   Tensor dwp = at::empty({G, C}, f32);
@@ -85,11 +98,9 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   if (N > 0) {
     pllm::norm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                    opt_ptr(ds), dx.data_ptr(), dwp.data_ptr<float>(), has_bias ? dbp.data_ptr<float>() : nullptr,
-                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, cur_stream());
-  } else {
-    dw.zero_();
-    if (has_bias) db.zero_();
+                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, acc, cur_stream());
   }
+  if (acc) return {dx};
   if (!has_bias) return {dx, dw};
   return {dx, dw, db};
 }
@@ -256,23 +267,39 @@ Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const std::optional<T
   Tensor out = at::empty({idx.size(0), T, C}, wte.options());
   if (ix.numel())
     pllm::embedding_fwd(ix.data_ptr<int64_t>(), wte.data_ptr(), opt_ptr(wpe), out.data_ptr(), ix.numel(), (int)T, (int)C,
-                        (int)pos_offset, cur_stream());
+                        (int)pos_offset, wte.size(0), cur_stream());
   return out;
 }
 
-std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V, int64_t n_pos, bool has_wpe) {
+// dwte_acc/dwpe_acc: if given, gradients are ADDED into them (flat-buffer views) and
+// nothing is returned; otherwise fresh zero-initialised gradients are returned.
+std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V, int64_t n_pos, bool has_wpe,
+                                  const std::optional<Tensor>& dwte_acc, const std::optional<Tensor>& dwpe_acc) {
   check_bf16(dx, "dx");
   check_contig(dx, "dx");
   const int64_t Bn = idx.size(0), T = idx.size(1), C = dx.size(-1);
   TORCH_CHECK(dx.numel() == Bn * T * C, "embedding bwd shape");
+  TORCH_CHECK(!has_wpe || n_pos >= T, "embedding bwd: n_pos < T");
+  const bool acc = dwte_acc.has_value();
+  TORCH_CHECK(!has_wpe || acc == dwpe_acc.has_value(), "embedding_bwd: both or neither accumulation targets");
+  if (acc) {
+    check_bf16(*dwte_acc, "dwte_acc");
+    TORCH_CHECK(dwte_acc->numel() == V * C && dwte_acc->is_contiguous(), "dwte_acc shape");
+    if (has_wpe) {
+      check_bf16(*dwpe_acc, "dwpe_acc");
+      TORCH_CHECK(dwpe_acc->numel() == n_pos * C && dwpe_acc->is_contiguous(), "dwpe_acc shape");
+    }
+  }
+  TORCH_CHECK(idx.is_cuda(), "idx on GPU");
   auto flat = idx.reshape({-1}).to(at::kInt);
   auto sr = flat.sort(/*stable=*/true, 0, false);
   Tensor sorted = std::get<0>(sr).contiguous(), perm = std::get<1>(sr).to(at::kInt).contiguous();
-  Tensor dwte = at::zeros({V, C}, dx.options());
-  Tensor dwpe = has_wpe ? at::zeros({n_pos, C}, dx.options()) : Tensor();
+  Tensor dwte = acc ? *dwte_acc : at::zeros({V, C}, dx.options());
+  Tensor dwpe = has_wpe ? (acc ? *dwpe_acc : at::zeros({n_pos, C}, dx.options())) : Tensor();
   if (Bn * T)
     pllm::embedding_bwd(dx.data_ptr(), sorted.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), dwte.data_ptr(),
-                        has_wpe ? dwpe.data_ptr() : nullptr, Bn * T, (int)Bn, (int)T, (int)C, cur_stream());
+                        has_wpe ? dwpe.data_ptr() : nullptr, Bn * T, (int)Bn, (int)T, (int)C, V, cur_stream());
+  if (acc) return {};
   if (!has_wpe) return {dwte};
   return {dwte, dwpe};
 }
@@ -362,7 +389,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(pllm, m) {
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor weight, Tensor? bias, float eps, bool rms) -> Tensor[]");
-  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!)? dw_acc=None, Tensor(b!)? db_acc=None) -> Tensor[]");
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
@@ -373,7 +400,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
-  m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe) -> Tensor[]");
+  m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!)? dwte_acc=None, Tensor(b!)? dwpe_acc=None) -> Tensor[]");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale) -> ()");
 }

@@ -36,7 +36,7 @@ void norm_fwd(const void* x, const void* res, const void* w, const void* b, void
               float* rstd, int N, int C, float eps, bool rms, hipStream_t st);
 int norm_bwd_grid(int N);
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
-              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, hipStream_t st);
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate, hipStream_t st);
 
 // elementwise.hip (op: 0 relu, 1 gelu-tanh)
 void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st);
@@ -61,9 +61,9 @@ void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
 
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t N, int T, int C,
-                   int pos_offset, hipStream_t st);
+                   int pos_offset, int64_t V, hipStream_t st);
 void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, int64_t N,
-                   int Bn, int T, int C, hipStream_t st);
+                   int Bn, int T, int C, int64_t V, hipStream_t st);
 
 // attention.hip
 bool attn_supported_head_dim(int D);

@@ -185,21 +185,31 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   }
 }
 
-// column sums of an fp32 [G, C] slab -> bf16 [C]
-__global__ __launch_bounds__(256) void col_reduce_kernel(const float* __restrict__ part, int G, int C,
-                                                         uint16_t* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
-  int g = 0;
-  for (; g + 4 <= G; g += 4) {
-    a0 += part[(size_t)g * C + c];
-    a1 += part[(size_t)(g + 1) * C + c];
-    a2 += part[(size_t)(g + 2) * C + c];
-    a3 += part[(size_t)(g + 3) * C + c];
+// column sums of an fp32 [G, C] slab -> bf16 [C].  One 1024-thread block per 64
+// columns: 16 waves each sum a strided subset of the G rows (coalesced 256 B per
+// wave-row), then a fixed-order LDS combine -> deterministic.
+__global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restrict__ part, int G, int C,
+                                                          uint16_t* __restrict__ out, int accumulate) {
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, g0 = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < C) {
+    int g = g0;
+    for (; g + 16 < G; g += 32) {
+      a0 += part[(size_t)g * C + c];
+      a1 += part[(size_t)(g + 16) * C + c];
+    }
+    if (g < G) a0 += part[(size_t)g * C + c];
   }
-  for (; g < G; ++g) a0 += part[(size_t)g * C + c];
-  out[c] = f2bf_bits((a0 + a1) + (a2 + a3));
+  red[g0][lane] = a0 + a1;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][lane];
+    out[c] = f2bf_bits(accumulate ? s + bf2f(out[c]) : s);
+  }
 }
 
 }  // namespace
@@ -223,11 +233,11 @@ void norm_fwd(const void* x, const void* res, const void* w, const void* b, void
 
 int norm_bwd_grid(int N) {
   int g = (N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-  return g < 1024 ? g : 1024;
+  return g < 512 ? g : 512;
 }
 
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
-              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms,
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate,
               hipStream_t st) {
   const int G = norm_bwd_grid(N);
   const int K = (C + 511) / 512;
@@ -241,9 +251,9 @@ void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, c
   else if (K <= 4) L(4);
   else L(8);
 #undef L
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, st, dw_part, G, C, (uint16_t*)dw);
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, dw_part, G, C, (uint16_t*)dw, (int)accumulate);
   if (db_part && db)
-    hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 255) / 256), dim3(256), 0, st, db_part, G, C, (uint16_t*)db);
+    hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, db_part, G, C, (uint16_t*)db, (int)accumulate);
 }
 
 }  // namespace pllm

@@ -61,7 +61,20 @@ class ModelConfig:
     def head_dim(self) -> int:
         return self.n_embed // self.n_head
 
+    def _default_ffn(self, n_embed: int, mlp: str) -> int:
+        if mlp == "swiglu":
+            h = int(2 * (4 * n_embed) / 3)
+            return 256 * ((h + 255) // 256)
+        return 4 * n_embed
+
     def replace(self, **kw) -> "ModelConfig":
+        """dataclasses.replace that re-derives dependent defaults (n_kv_head, ffn_hidden)
+        when the fields they were derived from change and they were not set explicitly."""
+        if "n_head" in kw and "n_kv_head" not in kw and self.n_kv_head == self.n_head:
+            kw["n_kv_head"] = None
+        if ("n_embed" in kw or "mlp" in kw) and "ffn_hidden" not in kw and \
+                self.ffn_hidden == self._default_ffn(self.n_embed, self.mlp):
+            kw["ffn_hidden"] = None
         return dataclasses.replace(self, **kw)
 
     def to_dict(self) -> dict:
@@ -78,7 +91,8 @@ class ModelConfig:
         kv = self.n_kv_head * self.head_dim
         b = 1 if self.bias else 0
         per = 0
-        per += C * (C + 2 * kv) + b * (C + 2 * kv)             # qkv
+        qkv_b = b if self.arch != "ref" else 0                  # reference Head projections are bias-free
+        per += C * (C + 2 * kv) + qkv_b * (C + 2 * kv)         # qkv
         if self.attn_out_proj:
             per += C * C + b * C
         if self.mlp == "swiglu":

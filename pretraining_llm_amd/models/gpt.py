@@ -57,18 +57,18 @@ class Attention(nn.Module):
         self.proj = nn.Linear(C, C, bias=cfg.bias) if cfg.attn_out_proj else None
 
     def forward(self, x, rope=None):
-        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         cos, sin = rope if rope is not None else (None, None)
         y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is not None:
-            y = F.linear(y, self.proj.weight, self.proj.bias)
+            y = ops.linear(y, self.proj.weight, self.proj.bias)
         return y
 
     # --- KV-cache decode -------------------------------------------------
     def forward_cached(self, x, cache, layer_idx, pos, rope=None):
         B, T, _ = x.shape
         H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
-        qkv = F.linear(x, self.qkv.weight, self.qkv.bias)
+        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         q = qkv[..., : H * D].view(B, T, H, D)
         k = qkv[..., H * D:(H + Hkv) * D].view(B, T, Hkv, D)
         v = qkv[..., (H + Hkv) * D:].view(B, T, Hkv, D)
@@ -80,7 +80,7 @@ class Attention(nn.Module):
         y = ops.attention(q.contiguous(), kc, vc, causal=True)
         y = y.reshape(B, T, H * D)
         if self.proj is not None:
-            y = F.linear(y, self.proj.weight, self.proj.bias)
+            y = ops.linear(y, self.proj.weight, self.proj.bias)
         return y
 
 
@@ -94,7 +94,7 @@ class MLP(nn.Module):
         self.proj = nn.Linear(Fh, C, bias=cfg.bias)
 
     def forward_embedding(self, x):
-        h = F.linear(x, self.hidden.weight, self.hidden.bias)
+        h = ops.linear(x, self.hidden.weight, self.hidden.bias)
         if self.kind == "gelu":
             return ops.gelu(h)
         if self.kind == "swiglu":
@@ -102,7 +102,7 @@ class MLP(nn.Module):
         return ops.relu(h)
 
     def project_embedding(self, h):
-        return F.linear(h, self.proj.weight, self.proj.bias)
+        return ops.linear(h, self.proj.weight, self.proj.bias)
 
     def forward(self, x):
         return self.project_embedding(self.forward_embedding(x))
@@ -226,12 +226,12 @@ class GPT(nn.Module):
         h = self._trunk(idx)
         B, T, C = h.shape
         if targets is None:
-            logits = F.linear(h, self.head_weight, self.head_bias)
+            logits = ops.linear(h, self.head_weight, self.head_bias)
             return logits, None
         if not return_logits:
             # training hot path: LM head GEMM + fused CE that overwrites the logits with dlogits
             return None, ops.lm_head_cross_entropy(h, self.head_weight, self.head_bias, targets)
-        logits = F.linear(h.reshape(B * T, C), self.head_weight, self.head_bias)
+        logits = ops.linear(h.reshape(B * T, C), self.head_weight, self.head_bias)
         loss = ops.cross_entropy(logits, targets.reshape(B * T))
         return logits.view(B, T, -1), loss
 

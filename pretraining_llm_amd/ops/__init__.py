@@ -55,6 +55,74 @@ def _ops():
 
 
 # ---------------------------------------------------------------------------
+# Direct gradient accumulation.  When the optimizer owns a flat gradient
+# buffer (train/optim.py FlatAdamW marks its params ``_pllm_flat_grad``), the
+# backward kernels/GEMMs ADD their weight gradients straight into ``p.grad``
+# (a view of that buffer: hipBLASLt beta=1 epilogue, in-kernel read-add-write)
+# instead of returning a fresh tensor that autograd's AccumulateGrad would then
+# add in a separate pass.  ``_notify`` tells the data-parallel engine that a
+# contribution landed (it replaces the post-accumulate-grad hook for these).
+# ---------------------------------------------------------------------------
+def _acc_target(p):
+    if p is None or not getattr(p, "_pllm_flat_grad", False):
+        return None
+    g = p.grad
+    return g if g is not None else None
+
+
+def _notify(p):
+    cb = getattr(p, "_pllm_grad_ready", None)
+    if cb is not None:
+        cb()
+
+
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T + b on hipBLASLt; backward accumulates dW (beta=1 GEMM) and db in place."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        ctx.save_for_backward(x, weight)
+        ctx.w, ctx.b = weight, bias
+        return F.linear(x, weight, bias)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight = ctx.saved_tensors
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = dy @ weight
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.needs_input_grad[1]:
+            x2 = x.reshape(-1, x.shape[-1])
+            tgt = _acc_target(ctx.w)
+            if tgt is not None:
+                tgt.addmm_(dy2.t(), x2)
+                _notify(ctx.w)
+            else:
+                dw = dy2.t() @ x2
+        if ctx.b is not None and ctx.needs_input_grad[2]:
+            tgt = _acc_target(ctx.b)
+            s = _bias_grad(dy2)
+            if tgt is not None:
+                tgt.add_(s)
+                _notify(ctx.b)
+            else:
+                db = s
+        ctx.w = ctx.b = None
+        return dx, dw, db
+
+
+def _bias_grad(dy2):
+    return dy2.sum(0)
+
+
+def linear(x, weight, bias=None):
+    if _hip(x) and torch.is_grad_enabled() and weight.requires_grad:
+        return _LinearFn.apply(x, weight, bias)
+    return F.linear(x, weight, bias)
+
+
+# ---------------------------------------------------------------------------
 # LayerNorm / RMSNorm with optional fused residual add
 #   s = x + residual (if residual given);  y = norm(s) * w (+ b)
 #   returns (y, s).  The backward adds the residual-stream gradient (ds from
@@ -69,6 +137,7 @@ class _NormFn(torch.autograd.Function):
         r2 = residual.reshape(-1, C) if residual is not None else None
         y, s, mean, rstd = _ops().norm_fwd(x2, r2, weight, bias, eps, rms)
         ctx.save_for_backward(s, weight, mean, rstd)
+        ctx.w, ctx.b = weight, bias
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
         ctx.rms = rms
@@ -83,10 +152,21 @@ class _NormFn(torch.autograd.Function):
         C = ctx.shp[-1]
         dy2 = dy.reshape(-1, C).contiguous()
         ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
-        outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms)
+        tw = _acc_target(ctx.w)
+        tb = _acc_target(ctx.b) if ctx.has_bias else None
+        direct = tw is not None and (not ctx.has_bias or tb is not None)
+        if direct:
+            outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms, tw, tb)
+            dw = db = None
+            _notify(ctx.w)
+            if ctx.has_bias:
+                _notify(ctx.b)
+        else:
+            outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms)
+            dw = outs[1]
+            db = outs[2] if ctx.has_bias else None
+        ctx.w = ctx.b = None
         dx = outs[0].view(ctx.shp)
-        dw = outs[1]
-        db = outs[2] if ctx.has_bias else None
         return dx, (dx if ctx.has_res else None), dw, db, None, None
 
 
@@ -292,13 +372,25 @@ class _EmbeddingFn(torch.autograd.Function):
         ctx.save_for_backward(idx)
         ctx.V = wte.shape[0]
         ctx.n_pos = 0 if wpe is None else wpe.shape[0]
+        ctx.wte, ctx.wpe = wte, wpe
         return x
 
     @staticmethod
     def backward(ctx, dx):
         (idx,) = ctx.saved_tensors
-        outs = _ops().embedding_bwd(dx.contiguous(), idx, ctx.V, ctx.n_pos, ctx.n_pos > 0)
-        return None, outs[0], (outs[1] if ctx.n_pos > 0 else None)
+        has_pos = ctx.n_pos > 0
+        tt = _acc_target(ctx.wte)
+        tp = _acc_target(ctx.wpe) if has_pos else None
+        if tt is not None and (not has_pos or tp is not None):
+            _ops().embedding_bwd(dx.contiguous(), idx, ctx.V, ctx.n_pos, has_pos, tt, tp)
+            _notify(ctx.wte)
+            if has_pos:
+                _notify(ctx.wpe)
+            ctx.wte = ctx.wpe = None
+            return None, None, None
+        ctx.wte = ctx.wpe = None
+        outs = _ops().embedding_bwd(dx.contiguous(), idx, ctx.V, ctx.n_pos, has_pos)
+        return None, outs[0], (outs[1] if has_pos else None)
 
 
 def embedding(idx, wte, wpe=None, pos_offset: int = 0):
@@ -323,17 +415,27 @@ class _LMHeadCEFn(torch.autograd.Function):
         n_valid = (targets != ignore_index).sum().clamp_min(1)
         ctx.save_for_backward(h, weight, logits)
         ctx.has_bias = bias is not None
+        ctx.w, ctx.b = weight, bias
         return rows.sum() / n_valid
 
     @staticmethod
     def backward(ctx, dloss):
         h, weight, dlogits = ctx.saved_tensors
         g = dloss.to(torch.float32)
-        dh = (dlogits @ weight).mul_(g.to(h.dtype)) if ctx.needs_input_grad[0] else None
-        dw = (dlogits.t() @ h).mul_(g.to(weight.dtype)) if ctx.needs_input_grad[1] else None
-        db = None
+        gh = g.to(h.dtype)
+        dh = (dlogits @ weight).mul_(gh) if ctx.needs_input_grad[0] else None
+        dw = db = None
+        if ctx.needs_input_grad[1]:
+            hs = h * gh  # fold the upstream scalar into the small operand, not the [N, V] gradient
+            tgt = _acc_target(ctx.w)
+            if tgt is not None:
+                tgt.addmm_(dlogits.t(), hs)
+                _notify(ctx.w)
+            else:
+                dw = dlogits.t() @ hs
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = (dlogits.float().sum(0) * g).to(weight.dtype)
+        ctx.w = ctx.b = None
         return dh, dw, db, None, None
 
 

@@ -67,13 +67,23 @@ class DataParallelEngine:
         for b, bk in enumerate(self.buckets):
             for i in bk["params"]:
                 self.param_bucket[i] = b
+        # A parameter's gradient can land in several pieces (a tied embedding gets the LM-head
+        # GEMM and the embedding scatter; kernels that add straight into the flat buffer signal
+        # through ``p._pllm_grad_ready`` instead of autograd's post-accumulate hook).  The number
+        # of pieces per parameter is learned in the first synchronised backward (which launches
+        # every bucket at the end, no overlap); afterwards a parameter is ready when all its
+        # pieces have arrived.
+        self._expected: Optional[List[int]] = None
+        self._events = [0] * len(params)
         self._reset_counters()
         if broadcast_params and self.world > 1:
             dist.broadcast(optimizer.flat_param, src=self._global_src(), group=process_group)
             optimizer.sync_master_from_params()
         if self.world > 1 and overlap:
             for i, p in enumerate(params):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
+                h = self._make_hook(i)
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, h=h: h()))
+                p._pllm_grad_ready = h
 
     def _global_src(self):
         if self.pg is None:
@@ -90,13 +100,20 @@ class DataParallelEngine:
         self.buckets.append({"params": list(idx), "start": s, "end": e})
 
     def _reset_counters(self):
-        self._pending = [len(b["params"]) for b in self.buckets]
+        if self._expected is None:
+            self._pending = [len(b["params"]) for b in self.buckets]
+        else:
+            self._pending = [sum(1 for i in b["params"] if self._expected[i] > 0) for b in self.buckets]
+        self._events = [0] * len(self._events)
         self._next_launch = 0
         self._handles = []
 
     def _make_hook(self, i):
-        def hook(p):
+        def hook():
             if not self.enabled:
+                return
+            self._events[i] += 1
+            if self._expected is None or self._events[i] != self._expected[i]:
                 return
             b = self.param_bucket[i]
             self._pending[b] -= 1
@@ -133,6 +150,8 @@ class DataParallelEngine:
                 self._next_launch += 1
             for h in self._handles:
                 h.wait()
+            if self._expected is None and self.enabled and any(self._events):
+                self._expected = list(self._events)
         self._reset_counters()
         return 1.0 / self.world
 

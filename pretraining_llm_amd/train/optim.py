@@ -89,6 +89,7 @@ class FlatAdamW:
             seg.copy_(p.data)
             p.data = seg
             p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
+            p._pllm_flat_grad = True  # backward kernels may add straight into p.grad (ops._acc_target)
         self.master = self.flat_param.float() if pdtype != torch.float32 else self.flat_param.clone()
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
