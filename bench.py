@@ -36,12 +36,14 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--model", default="gpt2-small")
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("PLLM_BENCH_BATCH", "16")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("PLLM_BENCH_BATCH", "64")),
                     help="micro-batch (sequences) per GPU")
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-clip", type=float, default=1.0)
+    ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
+    ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -62,6 +64,10 @@ def main(argv=None):
     if args.gpus != world and di.is_master:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
     dev = di.device
+    tuned = False
+    if not args.no_tuned_gemm:
+        from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
+        tuned = enable_tuned_gemms(dev.index or 0, tune_missing=args.tune_missing and args.warmup > 0)
     ops.set_backend(args.backend)
     if args.backend == "auto":
         ops._lib.require()  # the HIP path must be the one that runs: fail loudly if the extension is missing
@@ -130,7 +136,7 @@ def main(argv=None):
             "data": "synthetic (native token loader over a generated uint16 shard), random-init weights",
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
                        "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "backend": args.backend,
-                       "tokens_per_step": B * T * world},
+                       "tokens_per_step": B * T * world, "tuned_gemms": tuned},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),
             "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),
             "final_loss": round(final_loss, 4),

@@ -268,8 +268,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   constexpr int BK = C::BK, BQ = C::BQ, QS = C::QS, KS = C::KS, DSS = C::DSS, CPR = C::CPR;
   constexpr int QLPT = C::QLPT, KLPT = C::KLPT;
   constexpr int NKS = D / 16, NDB = D / 32;
-  constexpr int WPD = 4 / NDB;            // waves sharing one d-block in the dQ product
-  constexpr int DQ_KEYS = BK / WPD;       // keys summed per wave in the dQ product
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
   __shared__ float rowc[2 * BQ];          // -lse/scale, -delta
   uint16_t* Kl = smem;
@@ -416,24 +414,28 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
       }
     }
     __syncthreads();
-    // dQ[q, d] += dS[q, keys] K[keys, d]   (this wave: one d-block, DQ_KEYS keys)
-    {
-      const int db = w % NDB, kh = w / NDB;
+    // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one d-block per wave
+    // (waves w < NDB), summed over all BK keys on chip and stored with plain stores into the
+    // key block's slab; attn_dq_reduce_kernel sums the slabs in a fixed order (deterministic,
+    // and no fp32 atomics: they were the floor of the first version of this kernel).
+    if (w < NDB) {
+      const int db = w;
       f32x16 acc = zero16();
 #pragma unroll
-      for (int ks = 0; ks < DQ_KEYS / 16; ++ks) {
-        const int kr0 = kh * DQ_KEYS + ks * 16 + 8 * hh + tq;
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const int kr0 = ks * 16 + 8 * hh + tq;
         const uint16_t* sa = Sl + kr0 * DSS + 16 * g1 + 4 * tp;
         const uint16_t* kbp = Kl + kr0 * KS + db * 32 + 16 * g1 + 4 * tp;
         const bf16x8 A = cat_tr(ds_tr(sa), ds_tr(sa + 4 * DSS));
         const bf16x8 Bf = cat_tr(ds_tr(kbp), ds_tr(kbp + 4 * KS));
         acc = mfma32(A, Bf, acc);
       }
-      float* dq = a.dq_acc + (((int64_t)b * a.T) * a.H + h) * D + db * 32 + r;
+      const int64_t slab = (int64_t)a.B * a.T * a.H * D;
+      float* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + db * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = q0 + acc_row(i, hh);
-        if (q < a.T) atomicAdd(dq + (int64_t)q * a.H * D, acc[i]);
+        if (q < a.T) dq[(int64_t)q * a.H * D] = acc[i];
       }
     }
   }
@@ -457,10 +459,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   }
 }
 
-// dq (bf16, strided) = dq_acc (fp32 [B,T,H,D]) * scale
+// dq (bf16, strided) = scale * sum over contributing key blocks of the fp32 slabs
+// [nkb][B,T,H,D]; under the causal mask row t only reads blocks kb <= (t+off)/BK
+// (the others were never written for it).
 template <int D>
-__global__ __launch_bounds__(256) void attn_dq_convert_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   constexpr int CPR = D / 8;
+  constexpr int BK = BwdCfg<D>::BK;
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t row = gid / CPR;
   const int c = (int)(gid % CPR);
@@ -470,14 +475,23 @@ __global__ __launch_bounds__(256) void attn_dq_convert_kernel(AttnBwdArgs a) {
   const int64_t bt = row / a.H;
   const int t = (int)(bt % a.T);
   const int b = (int)(bt / a.T);
-  const f32x4* src = reinterpret_cast<const f32x4*>(a.dq_acc + row * D + c * 8);
-  f32x4 x0 = src[0], x1 = src[1];
-  float f[8];
+  const int nkb = (a.S + BK - 1) / BK;
+  int kmax = nkb - 1;
+  if (a.causal) kmax = min(kmax, (t + a.S - a.T) / BK);
+  const int64_t slab = nrows * D;
+  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const float* src = a.dq_acc + row * D + c * 8;
+  for (int kb = 0; kb <= kmax; ++kb) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(src + kb * slab);
+    const f32x4 x0 = p[0], x1 = p[1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    f[j] = x0[j] * a.scale;
-    f[4 + j] = x1[j] * a.scale;
+    for (int j = 0; j < 4; ++j) {
+      f[j] += x0[j];
+      f[4 + j] += x1[j];
+    }
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] *= a.scale;
   st16(a.dq + b * a.dq_sb + (int64_t)t * a.dq_st + (int64_t)h * a.dq_sh + c * 8, pack8(f));
 }
 
@@ -498,10 +512,9 @@ static void attn_bwd_t(const AttnBwdArgs& a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
   const int nkb = (a.S + 127) / 128;
-  (void)hipMemsetAsync(a.dq_acc, 0, (size_t)nrows * D * sizeof(float), st);
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(attn_bwd_kernel<D>, dim3(nkb * a.B * a.Hkv), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_dq_convert_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_dq_reduce_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {

@@ -357,7 +357,9 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse shape");
   auto f32 = q.options().dtype(at::kFloat);
   Tensor delta = at::empty({B, H, T}, f32);
-  Tensor dq_acc = at::empty({B, T, H, D}, f32);
+  // per-key-block dQ partial slabs (attention.hip: plain stores + ordered reduce, no atomics)
+  const int64_t nkb = (S + 127) / 128;
+  Tensor dq_acc = at::empty({nkb, B, T, H, D}, f32);
   AttnBwdArgs a{};
   a.q = (const uint16_t*)q.data_ptr();
   a.k = (const uint16_t*)k.data_ptr();
