@@ -66,7 +66,8 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const std::optional<Tensor>& res, 
 // the optimizer's flat gradient buffer) and only dx is returned.
 std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& mean,
                              const Tensor& rstd, const std::optional<Tensor>& ds, bool has_bias, bool rms,
-                             const std::optional<Tensor>& dw_acc, const std::optional<Tensor>& db_acc) {
+                             const std::optional<Tensor>& dw_acc, const std::optional<Tensor>& db_acc,
+                             const std::optional<Tensor>& xb_acc) {
   check_bf16(dy, "dy");
   check_bf16(s, "s");
   check_contig(dy, "dy");
@@ -95,14 +96,44 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   auto f32 = dy.options().dtype(at::kFloat);
   Tensor dwp = at::empty({G, C}, f32);
   Tensor dbp = has_bias ? at::empty({G, C}, f32) : Tensor();
+  Tensor xbp;
+  if (xb_acc) {  // fused bias gradient of the producer of x: accumulated into xb_acc
+    check_bf16(*xb_acc, "xb_acc");
+    TORCH_CHECK(xb_acc->numel() == C && xb_acc->is_contiguous(), "xb_acc shape");
+    xbp = at::empty({G, C}, f32);
+  }
   if (N > 0) {
     pllm::norm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                    opt_ptr(ds), dx.data_ptr(), dwp.data_ptr<float>(), has_bias ? dbp.data_ptr<float>() : nullptr,
-                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, acc, cur_stream());
+                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, acc,
+                   xb_acc ? xbp.data_ptr<float>() : nullptr, xb_acc ? xb_acc->data_ptr() : nullptr, true,
+                   cur_stream());
   }
   if (acc) return {dx};
   if (!has_bias) return {dx, dw};
   return {dx, dw, db};
+}
+
+// column sums of dy [..., C] (bias gradient); added into out_acc if given, else returned
+Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
+  check_bf16(dy, "dy");
+  check_contig(dy, "dy");
+  const int64_t C = dy.size(-1);
+  const int64_t N = C ? dy.numel() / C : 0;
+  TORCH_CHECK(C % 8 == 0, "bias_grad: C % 8");
+  Tensor out;
+  if (out_acc) {
+    check_bf16(*out_acc, "out_acc");
+    TORCH_CHECK(out_acc->numel() == C && out_acc->is_contiguous(), "out_acc shape");
+    out = *out_acc;
+  } else {
+    out = at::zeros({C}, dy.options());
+  }
+  if (N > 0) {
+    Tensor part = at::empty({pllm::colsum_groups((int)N), C}, dy.options().dtype(at::kFloat));
+    pllm::bias_grad(dy.data_ptr(), (int)N, (int)C, part.data_ptr<float>(), out.data_ptr(), true, cur_stream());
+  }
+  return out;
 }
 
 // ---------------------------------------------------------------- activations
@@ -124,6 +155,27 @@ Tensor act_bwd(const Tensor& dy, const Tensor& xin, int64_t op) {
   if (dy.numel()) pllm::act_bwd((int)op, dy.data_ptr(), xin.data_ptr(), dx.data_ptr(), dy.numel(), cur_stream());
   return dx;
 }
+// activation backward + bias gradient of the producing linear layer (column sums of dx),
+// added into bias_acc; returns dx
+Tensor act_bwd_bias(const Tensor& dy, const Tensor& xin, int64_t op, Tensor& bias_acc) {
+  check_bf16(dy, "dy");
+  check_bf16(xin, "x");
+  check_contig(dy, "dy");
+  check_contig(xin, "x");
+  check_bf16(bias_acc, "bias_acc");
+  const int64_t C = dy.size(-1);
+  TORCH_CHECK(dy.sizes() == xin.sizes() && C % 8 == 0, "act_bwd_bias shapes");
+  TORCH_CHECK(bias_acc.numel() == C && bias_acc.is_contiguous(), "bias_acc shape");
+  const int64_t N = dy.numel() / C;
+  Tensor dx = at::empty_like(dy);
+  if (N > 0) {
+    Tensor part = at::empty({pllm::colsum_groups((int)N), C}, dy.options().dtype(at::kFloat));
+    pllm::act_bwd_bias((int)op, dy.data_ptr(), xin.data_ptr(), dx.data_ptr(), (int)N, (int)C, part.data_ptr<float>(),
+                       bias_acc.data_ptr(), true, cur_stream());
+  }
+  return dx;
+}
+
 Tensor swiglu_fwd(const Tensor& gu) {
   check_bf16(gu, "gate_up");
   check_contig(gu, "gate_up");
@@ -391,9 +443,11 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(pllm, m) {
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor weight, Tensor? bias, float eps, bool rms) -> Tensor[]");
-  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!)? dw_acc=None, Tensor(b!)? db_acc=None) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!)? dw_acc=None, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor[]");
+  m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
+  m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse, bool inplace) -> Tensor");
@@ -410,8 +464,10 @@ TORCH_LIBRARY(pllm, m) {
 TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("norm_fwd", norm_fwd);
   m.impl("norm_bwd", norm_bwd);
+  m.impl("bias_grad", bias_grad);
   m.impl("act_fwd", act_fwd);
   m.impl("act_bwd", act_bwd);
+  m.impl("act_bwd_bias", act_bwd_bias);
   m.impl("swiglu_fwd", swiglu_fwd);
   m.impl("swiglu_bwd", swiglu_bwd);
   m.impl("rope", rope);

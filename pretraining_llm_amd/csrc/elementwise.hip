@@ -62,6 +62,44 @@ __global__ __launch_bounds__(256) void act_bwd_kernel(const uint16_t* __restrict
   }
 }
 
+// Activation backward that also produces the bias gradient of the linear layer
+// feeding the activation (= column sums of dx), in the same pass over dy:
+// grid = (512-column panels, row groups); per-block column partials -> fp32 slab.
+template <int OP>
+__global__ __launch_bounds__(256) void act_bwd_colsum_kernel(const uint16_t* __restrict__ dy,
+                                                             const uint16_t* __restrict__ xin, uint16_t* __restrict__ dx,
+                                                             int N, int C, float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c8 = blockIdx.x * 64 + lane;
+  const int nch = C >> 3;
+  const int rows_per = (N + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 < nch) {
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const size_t off = (size_t)r * C + c8 * 8;
+      float g[8], a[8];
+      unpack8(ld16(dy + off), g);
+      unpack8(ld16(xin + off), a);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) g[j] = OP == 0 ? (a[j] > 0.f ? g[j] : 0.f) : g[j] * gelu_df(a[j]);
+      const u32x4 o = pack8(g);
+      st16(dx + off, o);
+      unpack8(o, g);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += g[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][lane * 8 + j] = acc[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.x * 512 + i;
+    if (c < C) part[(size_t)blockIdx.y * C + c] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 // SwiGLU: gu [rows, 2F] -> y [rows, F];  F % 8 == 0
 __global__ __launch_bounds__(256) void swiglu_fwd_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ y,
                                                          size_t rows, int F) {
@@ -175,6 +213,19 @@ void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStr
   else
     hipLaunchKernelGGL(act_bwd_kernel<1>, dim3(ew_grid(nv)), dim3(256), 0, st, (const uint16_t*)dy,
                        (const uint16_t*)xin, (uint16_t*)dx, nv);
+}
+
+void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int C, float* part, void* bias_grad,
+                  bool accumulate, hipStream_t st) {
+  const int G = colsum_groups(N);
+  dim3 grid((C + 511) / 512, G);
+  if (op == 0)
+    hipLaunchKernelGGL(act_bwd_colsum_kernel<0>, grid, dim3(256), 0, st, (const uint16_t*)dy, (const uint16_t*)xin,
+                       (uint16_t*)dx, N, C, part);
+  else
+    hipLaunchKernelGGL(act_bwd_colsum_kernel<1>, grid, dim3(256), 0, st, (const uint16_t*)dy, (const uint16_t*)xin,
+                       (uint16_t*)dx, N, C, part);
+  col_reduce(part, G, C, bias_grad, accumulate, st);
 }
 
 void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st) {

@@ -35,12 +35,22 @@ namespace pllm {
 void norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* s, float* mean,
               float* rstd, int N, int C, float eps, bool rms, hipStream_t st);
 int norm_bwd_grid(int N);
+// xb_part/xb: optional column sums of dx (bias grad of the layer that produced x)
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
-              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate, hipStream_t st);
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate,
+              float* xb_part, void* xb, bool xb_accumulate, hipStream_t st);
+// fp32 [G, C] slab -> bf16 [C] column sums (optionally added into out)
+void col_reduce(const float* part, int G, int C, void* out, bool accumulate, hipStream_t st);
+// bias gradient = column sums of a bf16 [N, C] matrix; part: fp32 [colsum_groups(N), C] workspace
+int colsum_groups(int N);
+void bias_grad(const void* x, int N, int C, float* part, void* out, bool accumulate, hipStream_t st);
 
 // elementwise.hip (op: 0 relu, 1 gelu-tanh)
 void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st);
 void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStream_t st);
+// activation backward + fused bias gradient (column sums of dx) of the producing linear layer
+void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int C, float* part, void* bias_grad,
+                  bool accumulate, hipStream_t st);
 void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st);
 void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st);
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,

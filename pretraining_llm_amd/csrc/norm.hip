@@ -94,52 +94,74 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
   }
 }
 
-template <int K>
+
+// Backward.  One wave per row, rows strided over a <=512-block grid; the NEXT
+// row's operands are loaded before the current row is processed, so each wave
+// keeps two rows of loads in flight (the loop is latency-bound otherwise).
+// Per-block column partials of dw, db and (XB) of dx itself are combined across
+// the 4 waves through LDS and written to fp32 [G, C] slabs; col_reduce_kernel
+// finishes them.  The dx column sums are the bias gradient of the linear layer
+// that produced x (attention output projection / MLP down projection), fused
+// here instead of a separate pass over dy.
+template <int K, bool XB>
 __global__ __launch_bounds__(256) void norm_bwd_kernel(
     const uint16_t* __restrict__ dy, const uint16_t* __restrict__ s, const uint16_t* __restrict__ w,
     const float* __restrict__ mean_in, const float* __restrict__ rstd_in, const uint16_t* __restrict__ ds,
-    uint16_t* __restrict__ dx, float* __restrict__ dw_part, float* __restrict__ db_part, int N, int C,
-    int rms) {
+    uint16_t* __restrict__ dx, float* __restrict__ dw_part, float* __restrict__ db_part,
+    float* __restrict__ xb_part, int N, int C, int rms) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int nch = C >> 3;
   const float invC = 1.f / (float)C;
-  float w8[K][8], dwa[K][8], dba[K][8];
+  const u32x4 zero4 = {0u, 0u, 0u, 0u};
+  u32x4 wr[K];
+  float dwa[K][8], dba[K][8], xba[K][8];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
     const int c = lane + 64 * k;
-    if (c < nch) unpack8(ld16(w + c * 8), w8[k]);
+    wr[k] = c < nch ? ld16(w + c * 8) : zero4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      dwa[k][j] = 0.f;
-      dba[k][j] = 0.f;
-      if (c >= nch) w8[k][j] = 0.f;
-    }
+    for (int j = 0; j < 8; ++j) dwa[k][j] = dba[k][j] = xba[k][j] = 0.f;
   }
-  for (int row = blockIdx.x * ROWS_PER_BLOCK + wid; row < N; row += gridDim.x * ROWS_PER_BLOCK) {
+  const int stride = gridDim.x * ROWS_PER_BLOCK;
+  int row = blockIdx.x * ROWS_PER_BLOCK + wid;
+  u32x4 cs[K], cd[K], cr[K];
+  float cmean = 0.f, crstd = 0.f;
+  auto load = [&](int r, u32x4* S, u32x4* Dy, u32x4* R, float& mu, float& rs) {
+    const size_t base = (size_t)r * C;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      const bool in = c < nch;
+      S[k] = in ? ld16(s + base + c * 8) : zero4;
+      Dy[k] = in ? ld16(dy + base + c * 8) : zero4;
+      R[k] = (in && ds) ? ld16(ds + base + c * 8) : zero4;
+    }
+    mu = rms ? 0.f : mean_in[r];
+    rs = rstd_in[r];
+  };
+  if (row < N) load(row, cs, cd, cr, cmean, crstd);
+  for (; row < N; row += stride) {
+    const int nrow = row + stride;
+    u32x4 ns[K], nd[K], nr[K];
+    float nmean = 0.f, nrstd = 0.f;
+    if (nrow < N) load(nrow, ns, nd, nr, nmean, nrstd);
     const size_t base = (size_t)row * C;
-    const float mean = rms ? 0.f : mean_in[row];
-    const float rstd = rstd_in[row];
     float xh[K][8], g[K][8];
     float sg = 0.f, sgx = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
-      const int c = lane + 64 * k;
-      if (c < nch) {
-        float d8[8];
-        unpack8(ld16(s + base + c * 8), xh[k]);
-        unpack8(ld16(dy + base + c * 8), d8);
+      float d8[8], w8[8];
+      unpack8(cs[k], xh[k]);
+      unpack8(cd[k], d8);
+      unpack8(wr[k], w8);
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          xh[k][j] = (xh[k][j] - mean) * rstd;
-          g[k][j] = d8[j] * w8[k][j];
-          sg += g[k][j];
-          sgx += g[k][j] * xh[k][j];
-          dwa[k][j] += d8[j] * xh[k][j];
-          dba[k][j] += d8[j];
-        }
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xh[k][j] = g[k][j] = 0.f;
+      for (int j = 0; j < 8; ++j) {
+        xh[k][j] = (xh[k][j] - cmean) * crstd;
+        g[k][j] = d8[j] * w8[j];
+        sg += g[k][j];
+        sgx += g[k][j] * xh[k][j];
+        dwa[k][j] += d8[j] * xh[k][j];
+        dba[k][j] += d8[j];
       }
     }
     const float mg = rms ? 0.f : wave_sum(sg) * invC;
@@ -147,42 +169,46 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int c = lane + 64 * k;
+      float o[8], r8[8];
+      unpack8(cr[k], r8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = crstd * (g[k][j] - mg - xh[k][j] * mgx) + r8[j];
+      const u32x4 ov = pack8(o);
+      if (c < nch) st16(dx + base + c * 8, ov);
+      if (XB) {
+        unpack8(ov, o);  // sum exactly the bf16 values the producer's backward sees
+#pragma unroll
+        for (int j = 0; j < 8; ++j) xba[k][j] += o[j];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      cs[k] = ns[k];
+      cd[k] = nd[k];
+      cr[k] = nr[k];
+    }
+    cmean = nmean;
+    crstd = nrstd;
+  }
+  // combine the 4 waves' partials through LDS (one quantity at a time: [4][C] floats)
+  extern __shared__ __attribute__((aligned(16))) float red[];
+  auto flush = [&](float (*acc)[8], float* part) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
       if (c < nch) {
-        float o[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = rstd * (g[k][j] - mg - xh[k][j] * mgx);
-        if (ds) {
-          float r8[8];
-          unpack8(ld16(ds + base + c * 8), r8);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) o[j] += r8[j];
-        }
-        st16(dx + base + c * 8, pack8(o));
+        for (int j = 0; j < 8; ++j) red[wid * C + c * 8 + j] = acc[k][j];
       }
     }
-  }
-  // reduce the 4 waves' dw/db partials through LDS, one slab row per block
-  extern __shared__ __attribute__((aligned(16))) float red[];  // [4][C] dw then [4][C] db
-#pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const int c = lane + 64 * k;
-    if (c < nch) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        red[wid * C + c * 8 + j] = dwa[k][j];
-        red[(4 + wid) * C + c * 8 + j] = dba[k][j];
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < C; i += blockDim.x) {
-    float a = red[i] + red[C + i] + red[2 * C + i] + red[3 * C + i];
-    dw_part[(size_t)blockIdx.x * C + i] = a;
-    if (db_part) {
-      float bb = red[4 * C + i] + red[5 * C + i] + red[6 * C + i] + red[7 * C + i];
-      db_part[(size_t)blockIdx.x * C + i] = bb;
-    }
-  }
+    __syncthreads();
+    for (int i = threadIdx.x; i < C; i += blockDim.x)
+      part[(size_t)blockIdx.x * C + i] = (red[i] + red[C + i]) + (red[2 * C + i] + red[3 * C + i]);
+    __syncthreads();
+  };
+  flush(dwa, dw_part);
+  if (db_part) flush(dba, db_part);
+  if (XB) flush(xba, xb_part);
 }
 
 // column sums of an fp32 [G, C] slab -> bf16 [C].  One 1024-thread block per 64
@@ -212,6 +238,43 @@ __global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restric
   }
 }
 
+// per-block column partial sums of a bf16 [N, C] matrix (bias gradient of a linear
+// layer whose output gradient is x).  Block = 256 threads = 4 row lanes x 64 column
+// chunks of 8 -> one 512-column panel; grid = (panels, row groups).
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const uint16_t* __restrict__ x, int N, int C,
+                                                             float* __restrict__ part) {
+  __shared__ float red[4][512];
+  const int lane = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c8 = blockIdx.x * 64 + lane;  // 8-column chunk index
+  const int nch = C >> 3;
+  const int rows_per = (N + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * rows_per, r1 = min(N, r0 + rows_per);
+  float a[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c8 < nch) {
+    int r = r0 + rl;
+    for (; r + 4 < r1; r += 8) {
+      float f[8], h[8];
+      unpack8(ld16(x + (size_t)r * C + c8 * 8), f);
+      unpack8(ld16(x + (size_t)(r + 4) * C + c8 * 8), h);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += f[j] + h[j];
+    }
+    if (r < r1) {
+      float f[8];
+      unpack8(ld16(x + (size_t)r * C + c8 * 8), f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) a[j] += f[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) red[rl][lane * 8 + j] = a[j];
+  __syncthreads();
+  for (int i = threadIdx.x; i < 512; i += 256) {
+    const int c = blockIdx.x * 512 + i;
+    if (c < C) part[(size_t)blockIdx.y * C + c] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 }  // namespace
 
 namespace pllm {
@@ -236,24 +299,42 @@ int norm_bwd_grid(int N) {
   return g < 512 ? g : 512;
 }
 
+void col_reduce(const float* part, int G, int C, void* out, bool accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, (uint16_t*)out,
+                     (int)accumulate);
+}
+
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
               void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate,
-              hipStream_t st) {
+              float* xb_part, void* xb, bool xb_accumulate, hipStream_t st) {
   const int G = norm_bwd_grid(N);
   const int K = (C + 511) / 512;
-  const size_t lds = (size_t)8 * C * sizeof(float);
-#define L(KK)                                                                                             \
-  hipLaunchKernelGGL(norm_bwd_kernel<KK>, dim3(G), dim3(256), lds, st, (const uint16_t*)dy, (const uint16_t*)s, \
-                     (const uint16_t*)w, mean, rstd, (const uint16_t*)ds, (uint16_t*)dx, dw_part, db_part, N, C,  \
-                     (int)rms)
-  if (K <= 1) L(1);
-  else if (K <= 2) L(2);
-  else if (K <= 4) L(4);
-  else L(8);
+  const size_t lds = (size_t)4 * C * sizeof(float);
+#define L(KK, XBB)                                                                                              \
+  hipLaunchKernelGGL((norm_bwd_kernel<KK, XBB>), dim3(G), dim3(256), lds, st, (const uint16_t*)dy,            \
+                     (const uint16_t*)s, (const uint16_t*)w, mean, rstd, (const uint16_t*)ds, (uint16_t*)dx, dw_part, \
+                     db_part, xb_part, N, C, (int)rms)
+  const bool xbf = xb_part != nullptr;
+  if (K <= 1) { if (xbf) L(1, true); else L(1, false); }
+  else if (K <= 2) { if (xbf) L(2, true); else L(2, false); }
+  else if (K <= 4) { if (xbf) L(4, true); else L(4, false); }
+  else { if (xbf) L(8, true); else L(8, false); }
 #undef L
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, dw_part, G, C, (uint16_t*)dw, (int)accumulate);
-  if (db_part && db)
-    hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, db_part, G, C, (uint16_t*)db, (int)accumulate);
+  col_reduce(dw_part, G, C, dw, accumulate, st);
+  if (db_part && db) col_reduce(db_part, G, C, db, accumulate, st);
+  if (xbf && xb) col_reduce(xb_part, G, C, xb, xb_accumulate, st);
+}
+
+int colsum_groups(int N) {
+  int g = N / 256;
+  return g < 1 ? 1 : (g > 256 ? 256 : g);
+}
+
+void bias_grad(const void* x, int N, int C, float* part, void* out, bool accumulate, hipStream_t st) {
+  const int G = colsum_groups(N);
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((C + 511) / 512, G), dim3(256), 0, st, (const uint16_t*)x, N, C,
+                     part);
+  col_reduce(part, G, C, out, accumulate, st);
 }
 
 }  // namespace pllm

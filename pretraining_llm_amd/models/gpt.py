@@ -39,11 +39,12 @@ class Norm(nn.Module):
         self.weight = nn.Parameter(torch.ones(C))
         self.bias = None if self.rms else nn.Parameter(torch.zeros(C))
 
-    def forward(self, x, residual=None):
-        """Returns (norm(x + residual), x + residual)."""
+    def forward(self, x, residual=None, x_bias=None):
+        """Returns (norm(x + residual), x + residual). ``x_bias``: bias of the linear that produced
+        x, whose gradient this norm's backward kernel emits (fused bias-grad, HIP path)."""
         if self.rms:
-            return ops.rms_norm(x, self.weight, self.eps, residual)
-        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual)
+            return ops.rms_norm(x, self.weight, self.eps, residual, x_bias=x_bias)
+        return ops.layer_norm(x, self.weight, self.bias, self.eps, residual, x_bias=x_bias)
 
 
 class Attention(nn.Module):
@@ -56,12 +57,12 @@ class Attention(nn.Module):
         self.qkv = nn.Linear(C, qkv_out, bias=cfg.bias and cfg.arch != "ref")
         self.proj = nn.Linear(C, C, bias=cfg.bias) if cfg.attn_out_proj else None
 
-    def forward(self, x, rope=None):
+    def forward(self, x, rope=None, fuse_out_bias: bool = False):
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         cos, sin = rope if rope is not None else (None, None)
         y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is not None:
-            y = ops.linear(y, self.proj.weight, self.proj.bias)
+            y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
         return y
 
     # --- KV-cache decode -------------------------------------------------
@@ -104,8 +105,18 @@ class MLP(nn.Module):
     def project_embedding(self, h):
         return ops.linear(h, self.proj.weight, self.proj.bias)
 
-    def forward(self, x):
-        return self.project_embedding(self.forward_embedding(x))
+    def forward(self, x, fuse_out_bias: bool = False):
+        """``fuse_out_bias``: the down-projection's bias gradient is emitted by the next norm."""
+        fuse_act = ops._hip(x) and self.kind in ("gelu", "relu") and self.hidden.bias is not None \
+            and torch.is_grad_enabled()
+        h = ops.linear(x, self.hidden.weight, self.hidden.bias, bias_grad_external=fuse_act)
+        if self.kind == "gelu":
+            a = ops.gelu(h, bias=self.hidden.bias if fuse_act else None)
+        elif self.kind == "swiglu":
+            a = ops.swiglu(h)
+        else:
+            a = ops.relu(h) if not fuse_act else ops.relu(h, bias=self.hidden.bias)
+        return ops.linear(a, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
 
 
 class Block(nn.Module):
@@ -116,12 +127,26 @@ class Block(nn.Module):
         self.ln2 = Norm(cfg)
         self.mlp = MLP(cfg)
 
-    def forward(self, x, residual=None, rope=None):
-        """(x, residual) -> (mlp_out, residual_after_attn); the caller's next norm adds them."""
-        h, res = self.ln1(x, residual)
-        a = self.attn(h, rope)
-        h2, res2 = self.ln2(a, res)
-        return self.mlp(h2), res2
+    def forward(self, x, residual=None, rope=None, x_bias=None, fuse_mlp_out_bias: bool = False):
+        """(x, residual) -> (mlp_out, residual_after_attn); the caller's next norm adds them.
+
+        Fused bias gradients (HIP path): ``x_bias`` is the bias of the layer that produced x (the
+        previous block's MLP down projection), emitted by ln1's backward; the attention output
+        projection's bias by ln2's backward; with ``fuse_mlp_out_bias`` the caller promises to pass
+        this block's ``mlp.proj.bias`` as ``x_bias`` of the next norm."""
+        fuse = ops._hip(x) and torch.is_grad_enabled() and self.attn.proj is not None \
+            and self.attn.proj.bias is not None
+        h, res = self.ln1(x, residual, x_bias=x_bias)
+        a = self.attn(h, rope, fuse_out_bias=fuse)
+        h2, res2 = self.ln2(a, res, x_bias=self.attn.proj.bias if fuse else None)
+        return self.mlp(h2, fuse_out_bias=fuse and fuse_mlp_out_bias), res2
+
+    def fused_out_bias(self, x):
+        """The bias the next norm must take as ``x_bias`` when fuse_mlp_out_bias=True (or None)."""
+        if ops._hip(x) and torch.is_grad_enabled() and self.mlp.proj.bias is not None \
+                and self.attn.proj is not None and self.attn.proj.bias is not None:
+            return self.mlp.proj.bias
+        return None
 
     def forward_cached(self, x, residual, cache, layer_idx, pos, rope=None):
         h, res = self.ln1(x, residual)
@@ -213,12 +238,14 @@ class GPT(nn.Module):
         rope = self.rope_tables(idx.device, idx.shape[1])
         res = None
         ckpt = self.config.activation_checkpointing and self.training and torch.is_grad_enabled()
+        x_bias = None  # bias of the layer that produced x (fused into the next norm's backward)
         for blk in self.attn_blocks:
             if ckpt:
-                x, res = checkpoint(blk, x, res, rope, use_reentrant=False)
+                x, res = checkpoint(blk, x, res, rope, x_bias, True, use_reentrant=False)
             else:
-                x, res = blk(x, res, rope)
-        h, _ = self.layer_norm(x, res)
+                x, res = blk(x, res, rope, x_bias, True)
+            x_bias = blk.fused_out_bias(x)
+        h, _ = self.layer_norm(x, res, x_bias=x_bias)
         return h
 
     def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None,

@@ -77,12 +77,17 @@ def _notify(p):
 
 
 class _LinearFn(torch.autograd.Function):
-    """y = x W^T + b on hipBLASLt; backward accumulates dW (beta=1 GEMM) and db in place."""
+    """y = x W^T + b on hipBLASLt; backward accumulates dW (beta=1 GEMM) and db in place.
+
+    ``bias_grad_external``: the bias gradient is produced by the consumer's backward kernel
+    (the next norm's dx column sums, or the activation backward), so this function leaves it
+    alone instead of re-reading dy."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, bias_grad_external):
         ctx.save_for_backward(x, weight)
         ctx.w, ctx.b = weight, bias
+        ctx.bias_ext = bias_grad_external
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -100,25 +105,20 @@ class _LinearFn(torch.autograd.Function):
                 _notify(ctx.w)
             else:
                 dw = dy2.t() @ x2
-        if ctx.b is not None and ctx.needs_input_grad[2]:
+        if ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext:
             tgt = _acc_target(ctx.b)
-            s = _bias_grad(dy2)
             if tgt is not None:
-                tgt.add_(s)
+                _ops().bias_grad(dy2.contiguous(), tgt)
                 _notify(ctx.b)
             else:
-                db = s
+                db = _ops().bias_grad(dy2.contiguous())
         ctx.w = ctx.b = None
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def _bias_grad(dy2):
-    return dy2.sum(0)
-
-
-def linear(x, weight, bias=None):
+def linear(x, weight, bias=None, bias_grad_external: bool = False):
     if _hip(x) and torch.is_grad_enabled() and weight.requires_grad:
-        return _LinearFn.apply(x, weight, bias)
+        return _LinearFn.apply(x, weight, bias, bias_grad_external and bias is not None)
     return F.linear(x, weight, bias)
 
 
@@ -130,14 +130,14 @@ def linear(x, weight, bias=None):
 # ---------------------------------------------------------------------------
 class _NormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, residual, weight, bias, eps, rms):
+    def forward(ctx, x, residual, weight, bias, eps, rms, x_bias):
         shp = x.shape
         C = shp[-1]
         x2 = x.reshape(-1, C)
         r2 = residual.reshape(-1, C) if residual is not None else None
         y, s, mean, rstd = _ops().norm_fwd(x2, r2, weight, bias, eps, rms)
         ctx.save_for_backward(s, weight, mean, rstd)
-        ctx.w, ctx.b = weight, bias
+        ctx.w, ctx.b, ctx.xb = weight, bias, x_bias
         ctx.has_bias = bias is not None
         ctx.has_res = residual is not None
         ctx.rms = rms
@@ -154,20 +154,29 @@ class _NormFn(torch.autograd.Function):
         ds2 = ds.reshape(-1, C).contiguous() if ds is not None else None
         tw = _acc_target(ctx.w)
         tb = _acc_target(ctx.b) if ctx.has_bias else None
+        txb = _acc_target(ctx.xb) if ctx.xb is not None else None
         direct = tw is not None and (not ctx.has_bias or tb is not None)
+        dxb = None
         if direct:
-            outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms, tw, tb)
+            outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms, tw, tb, txb)
             dw = db = None
             _notify(ctx.w)
             if ctx.has_bias:
                 _notify(ctx.b)
+            if txb is not None:
+                _notify(ctx.xb)
         else:
             outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms)
             dw = outs[1]
             db = outs[2] if ctx.has_bias else None
-        ctx.w = ctx.b = None
+            if txb is not None:
+                _ops().bias_grad(outs[0], txb)
+                _notify(ctx.xb)
+        if ctx.xb is not None and txb is None:
+            dxb = _ops().bias_grad(outs[0])
+        ctx.w = ctx.b = ctx.xb = None
         dx = outs[0].view(ctx.shp)
-        return dx, (dx if ctx.has_res else None), dw, db, None, None
+        return dx, (dx if ctx.has_res else None), dw, db, None, None, dxb
 
 
 def _norm_ref(x, residual, weight, bias, eps, rms):
@@ -185,17 +194,22 @@ def _norm_ref(x, residual, weight, bias, eps, rms):
     return y, s
 
 
-def layer_norm(x, weight, bias, eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
+def layer_norm(x, weight, bias, eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
+               x_bias: Optional[torch.Tensor] = None):
+    """(LayerNorm(x + residual), x + residual).  ``x_bias``: the bias of the linear layer that
+    produced ``x`` (created with ``bias_grad_external=True``); its gradient is the column sum of
+    dx and is produced by this norm's backward kernel (HIP path)."""
     if _hip(x):
         return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
-                             weight, bias, eps, False)
+                             weight, bias, eps, False, x_bias)
     return _norm_ref(x, residual, weight, bias, eps, False)
 
 
-def rms_norm(x, weight, eps: float = 1e-5, residual: Optional[torch.Tensor] = None):
+def rms_norm(x, weight, eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
+             x_bias: Optional[torch.Tensor] = None):
     if _hip(x):
         return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
-                             weight, None, eps, True)
+                             weight, None, eps, True, x_bias)
     return _norm_ref(x, residual, weight, None, eps, True)
 
 
@@ -306,28 +320,55 @@ def attention(q, k, v, causal: bool = True, scale: Optional[float] = None, retur
 # activations (op ids of the HIP act kernels: 0 relu, 1 gelu-tanh)
 # ---------------------------------------------------------------------------
 class _GeluFn(torch.autograd.Function):
+    """GELU(tanh); with ``bias`` (the producing linear's bias, created with
+    bias_grad_external=True) the backward kernel also emits that bias's gradient."""
+
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, bias):
         ctx.save_for_backward(x)
+        ctx.b = bias
         return _ops().act_fwd(x, 1)
 
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
-        return _ops().act_bwd(dy.contiguous(), x, 1)
+        dy = dy.contiguous()
+        b, ctx.b = ctx.b, None
+        if b is None:
+            return _ops().act_bwd(dy, x, 1), None
+        tgt = _acc_target(b)
+        if tgt is not None:
+            dx = _ops().act_bwd_bias(dy, x, 1, tgt)
+            _notify(b)
+            return dx, None
+        dx = _ops().act_bwd(dy, x, 1)
+        return dx, _ops().bias_grad(dx)
 
 
 class _ReluFn(torch.autograd.Function):
+    """ReLU (reference MLP activation); optional fused bias gradient like _GeluFn."""
+
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, bias):
         y = _ops().act_fwd(x, 0)
         ctx.save_for_backward(y)
+        ctx.b = bias
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (y,) = ctx.saved_tensors
-        return _ops().act_bwd(dy.contiguous(), y, 0)
+        dy = dy.contiguous()
+        b, ctx.b = ctx.b, None
+        if b is None:
+            return _ops().act_bwd(dy, y, 0), None
+        tgt = _acc_target(b)
+        if tgt is not None:
+            dx = _ops().act_bwd_bias(dy, y, 0, tgt)
+            _notify(b)
+            return dx, None
+        dx = _ops().act_bwd(dy, y, 0)
+        return dx, _ops().bias_grad(dx)
 
 
 class _SwigluFn(torch.autograd.Function):
@@ -342,9 +383,9 @@ class _SwigluFn(torch.autograd.Function):
         return _ops().swiglu_bwd(dy.contiguous(), gu)
 
 
-def gelu(x):
+def gelu(x, bias: Optional[torch.Tensor] = None):
     if _hip(x):
-        return _GeluFn.apply(x.contiguous())
+        return _GeluFn.apply(x.contiguous(), bias)
     if _BACKEND == "torch":
         return F.gelu(x, approximate="tanh")
     return ref.gelu_tanh(x)
@@ -356,9 +397,9 @@ def swiglu(gate_up):
     return ref.swiglu(gate_up)
 
 
-def relu(x):
+def relu(x, bias: Optional[torch.Tensor] = None):
     if _hip(x):
-        return _ReluFn.apply(x.contiguous())
+        return _ReluFn.apply(x.contiguous(), bias)
     return ref.relu(x)
 
 
