@@ -7,18 +7,23 @@
 // the gradients are written straight into the packed dQKV buffer.
 //
 // Layout choices (CDNA4, wave64):
+//  * LDS tiles are [rows][D] bf16 with NO padding and an XOR swizzle of the
+//    16-byte chunks (Img<D>): conflict-free both for ds_read_b128 row reads
+//    (MFMA operands that sum over D) and for ds_read_b64_tr_b16 transposed reads
+//    (operands that sum over rows), so one image serves both (guide §5.5 T2/T10).
 //  * forward: one workgroup = 4 waves = 128 query rows, K/V tiles of 64 keys
-//    double-buffered in LDS through registers (issue-early / write-late).
+//    double-buffered in LDS through registers (issue-early / write-late, T14).
 //    S^T = K.Q^T is computed with the QUERY on the MFMA lane, so the softmax row
 //    statistics (m, l) are per-lane scalars and the P^T accumulator is directly
-//    the B operand of O^T += V^T.P^T (no LDS round trip for P).  V^T fragments
-//    come from ds_read_b64_tr_b16 transposed reads of the row-major V tile.
+//    the B operand of O^T += V^T.P^T (no LDS round trip for P).
 //  * backward: one workgroup = 4 waves = 128 keys of one (batch, kv-head); each
 //    wave keeps dK^T/dV^T for its 32 keys in registers across all query blocks
 //    (and all query heads of a GQA group), so dK/dV need no cross-workgroup sum.
 //    S and dP are computed with the KEY on the lane and initialised with
 //    -LSE/scale and -delta, so P = exp2(c*S') and dS = P*dP' need no extra pass.
-//    dQ is summed over key blocks with fp32 atomics into a [B,T,H,D] buffer.
+//    dQ per key block is summed over its 128 keys on chip and written to a
+//    per-key-block fp32 slab; a second kernel sums the slabs in a fixed order
+//    (deterministic; the first version's fp32 atomics were its floor).
 #include "common.h"
 #include "kernels.h"
 
@@ -52,23 +57,46 @@ PLLM_DEV bf16x8 pack_frag(const f32x16& x, int s) {
   return f;
 }
 
+// ---------------------------------------------------------------------------
+// Swizzled LDS image of a [rows][W] bf16 tile (W = 32, 64 or 128 elements).
+// Chunk ch (16 B) of row r lives at chunk position ch ^ f(r):
+//   W=128 (256 B rows): f = ((r&3)<<2) | ((r>>2)&3)       (guide T10 layout (b))
+//   W=64  (128 B rows): f = bitrev3((r>>1)&7)
+//   W=32  ( 64 B rows): f = (r>>2)&3
+// For the 16-lane groups of ds_read_b128 (16 distinct rows, same chunk) and the
+// 32-lane halves of ds_read_b64_tr_b16 (4 consecutive rows x 64 contiguous bytes)
+// every f above maps the accesses to distinct 16-B bank slots.
+// ---------------------------------------------------------------------------
+template <int W>
+struct Img {
+  static PLLM_DEV int f(int r) {
+    if constexpr (W == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
+    else if constexpr (W == 64) {
+      const int b = (r >> 1) & 7;
+      return ((b & 1) << 2) | (b & 2) | ((b >> 2) & 1);
+    } else return (r >> 2) & 3;
+  }
+  // element offset of (row, col); col's 8-aligned chunk is swizzled, col&7 kept
+  static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+};
+
 // ============================================================================
 // forward
 // ============================================================================
 template <int D>
 struct FwdCfg {
   static constexpr int BM = 128, BN = 64;
-  static constexpr int KS = D + 8;    // K row stride (elements): row reads conflict-free
-  static constexpr int VS = D + 32;   // V row stride: transposed reads conflict-free
   static constexpr int CPR = D / 8;   // 16 B chunks per row
   static constexpr int LPT = BN * CPR / 256;
-  static constexpr int LDS_ELEMS = 2 * BN * KS + 2 * BN * VS;
+  static constexpr int TILE = BN * D;  // elements per K (or V) tile
+  static constexpr int LDS_ELEMS = 4 * TILE;
 };
 
 template <int D>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   using C = FwdCfg<D>;
-  constexpr int BM = C::BM, BN = C::BN, KS = C::KS, VS = C::VS, CPR = C::CPR, LPT = C::LPT;
+  using I = Img<D>;
+  constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, LPT = C::LPT, TILE = C::TILE;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
 
@@ -111,20 +139,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   };
   auto swrite = [&](int buf) {
-    uint16_t* Kb = smem + buf * BN * KS;
-    uint16_t* Vb = smem + 2 * BN * KS + buf * BN * VS;
+    uint16_t* Kb = smem + buf * TILE;
+    uint16_t* Vb = smem + 2 * TILE + buf * TILE;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
-      st16(Kb + row * KS + col * 8, kr[i]);
-      st16(Vb + row * VS + col * 8, vr[i]);
+      st16(Kb + I::off(row, col * 8), kr[i]);
+      st16(Vb + I::off(row, col * 8), vr[i]);
     }
   };
 
   f32x16 o[NDB];
 #pragma unroll
   for (int db = 0; db < NDB; ++db) o[db] = zero16();
-  float m = -INFINITY, l = 0.f;
+  float m = -INFINITY, l = 0.f;  // m: running max of RAW scores (scale applied in the exponent)
   const float c2 = a.scale_log2;
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
 
@@ -138,51 +166,58 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     if (t + 1 < ntiles) gload(t + 1);
     const int kv0 = t * BN;
     if (kv0 < wave_kv_end) {
-      const uint16_t* Kb = smem + buf * BN * KS;
-      const uint16_t* Vb = smem + 2 * BN * KS + buf * BN * VS;
+      const uint16_t* Kb = smem + buf * TILE;
+      const uint16_t* Vb = smem + 2 * TILE + buf * TILE;
       f32x16 s[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         s[kb] = zero16();
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 kf = as_frag(ld16(Kb + (kb * 32 + r) * KS + 16 * ks + 8 * hh));
+          const bf16x8 kf = as_frag(ld16(Kb + I::off(kb * 32 + r, 16 * ks + 8 * hh)));
           s[kb] = mfma32(kf, qf[ks], s[kb]);
         }
       }
       const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw0 + off);
       float mx = -INFINITY;
+      if (need_mask) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+        for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float x = s[kb][i] * c2;
-          if (need_mask) {
+          for (int i = 0; i < 16; ++i) {
             const int key = kv0 + kb * 32 + acc_row(i, hh);
-            if (key >= a.S || (a.causal && key > qi + off)) x = -INFINITY;
+            if (key >= a.S || (a.causal && key > qi + off)) s[kb][i] = -INFINITY;
+            mx = fmaxf(mx, s[kb][i]);
           }
-          s[kb][i] = x;
-          mx = fmaxf(mx, x);
+        }
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
         }
       }
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
       const float mnew = fmaxf(m, mx);
-      const float muse = mnew == -INFINITY ? 0.f : mnew;
-      const float alpha = exp2f(m - muse);
+      const float mc = mnew == -INFINITY ? 0.f : mnew * c2;
+      const float alpha = exp2f(m * c2 - mc);  // m = -inf -> 0
       float ls = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = exp2f(s[kb][i] - muse);
+          const float p = exp2f(__builtin_fmaf(s[kb][i], c2, -mc));
           s[kb][i] = p;
           ls += p;
         }
       }
       l = l * alpha + ls;
-      m = mnew;
+      // rescale O only when some lane's running max moved (rare after the first tiles)
+      if (__any(mnew != m)) {
 #pragma unroll
-      for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+        for (int db = 0; db < NDB; ++db) o[db] *= alpha;
+      }
+      m = mnew;
       bf16x8 pf[4];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
@@ -193,8 +228,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       for (int kst = 0; kst < 4; ++kst) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          const uint16_t* vb = Vb + (kst * 16 + 4 * hh + tq) * VS + db * 32 + 16 * g1 + 4 * tp;
-          const bf16x8 va = cat_tr(ds_tr(vb), ds_tr(vb + 8 * VS));
+          const int row = kst * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
+          const bf16x8 va = cat_tr(ds_tr(Vb + I::off(row, col)), ds_tr(Vb + I::off(row + 8, col)));
           o[db] = mfma32(va, pf[kst], o[db]);
         }
       }
@@ -217,7 +252,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
         *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hh) = v2;
       }
     }
-    if (hh == 0 && a.lse) a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m + log2f(lt)) * 0.69314718055994531f;
+    if (hh == 0 && a.lse) a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m * c2 + log2f(lt)) * 0.69314718055994531f;
   }
 }
 
@@ -252,30 +287,32 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 
 template <int D>
 struct BwdCfg {
-  static constexpr int BK = 128, BQ = 32;
-  static constexpr int QS = D + 8;    // Q / dO tile stride (row reads + tr reads)
-  static constexpr int KS = D + 32;   // K tile stride (tr reads only)
-  static constexpr int DSS = 32 + 8;  // dS^T image stride (keys x 32 queries)
+  static constexpr int BK = 128;
+  static constexpr int BQ = D <= 64 ? 64 : 32;  // query rows per iteration (register budget)
+  static constexpr int NQB = BQ / 32;           // 32-row MFMA sub-blocks per iteration
   static constexpr int CPR = D / 8;
   static constexpr int QLPT = (BQ * CPR + 255) / 256;
   static constexpr int KLPT = BK * CPR / 256;
-  static constexpr int LDS_ELEMS = BK * KS + 2 * BQ * QS + BK * DSS;
+  static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;
 };
 
+// D=128 keeps dK^T/dV^T (128 regs) + K/V fragments (64) + S/dP in registers: one wave per
+// SIMD with the full register file instead of spilling at the 2-waves/SIMD budget.
 template <int D>
-__global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D>;
-  constexpr int BK = C::BK, BQ = C::BQ, QS = C::QS, KS = C::KS, DSS = C::DSS, CPR = C::CPR;
+  using I = Img<D>;
+  using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
+  constexpr int BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
   constexpr int QLPT = C::QLPT, KLPT = C::KLPT;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
   __shared__ float rowc[2 * BQ];          // -lse/scale, -delta
   uint16_t* Kl = smem;
-  uint16_t* Ql = smem + BK * KS;
-  uint16_t* Ol = Ql + BQ * QS;            // dO tile
-  uint16_t* Sl = Ol + BQ * QS;            // dS^T image [key][q]
+  uint16_t* Ql = smem + BK * D;
+  uint16_t* Ol = Ql + BQ * D;             // dO tile
+  uint16_t* Sl = Ol + BQ * D;             // dS^T image [key][q]
 
-  const int nkb = (a.S + BK - 1) / BK;
   const int BH = a.B * a.Hkv;
   const int id = blockIdx.x;
   const int kb = id / BH;                 // key block 0 (most query blocks under causal) first
@@ -283,9 +320,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   const int b = bh / a.Hkv, hk = bh % a.Hkv;
   const int G = a.H / a.Hkv;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int k0 = kb * BK, key = k0 + w * 32 + r;
+  const int k0 = kb * BK, kl = w * 32 + r, key = k0 + kl;
   const int off = a.S - a.T;
-  (void)nkb;
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
@@ -301,7 +337,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
   for (int i = 0; i < KLPT; ++i) {
     const int c = tid + 256 * i, row = c / CPR, col = c % CPR, kk = k0 + row;
     u32x4 v = kk < a.S ? ld16(kp + (int64_t)kk * a.k_st + col * 8) : u32x4{0u, 0u, 0u, 0u};
-    st16(Kl + row * KS + col * 8, v);
+    st16(Kl + I::off(row, col * 8), v);
   }
 
   f32x16 dk[NDB], dv[NDB];
@@ -344,6 +380,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
     }
   };
 
+  // dQ task of this wave in each iteration: (query sub-block, d-block)
+  constexpr int NTASK = NQB * NDB;
+  const int tq_blk = w / NDB, tdb = w % NDB;
+
   if (total > 0) gload(0);
   for (int it = 0; it < total; ++it) {
     const int h = hk * G + it / per_head;
@@ -353,88 +393,82 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kernel(AttnBwdArgs a) {
     for (int i = 0; i < QLPT; ++i) {
       const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
       if (c < BQ * CPR) {
-        st16(Ql + row * QS + col * 8, qr[i]);
-        st16(Ol + row * QS + col * 8, dor[i]);
+        st16(Ql + I::off(row, col * 8), qr[i]);
+        st16(Ol + I::off(row, col * 8), dor[i]);
       }
     }
     if (tid < 2 * BQ) rowc[tid] = rc;
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 
-    // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
-    f32x16 s, dp;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      s[i] = rowc[acc_row(i, hh)];
-      dp[i] = rowc[BQ + acc_row(i, hh)];
-    }
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      const bf16x8 qa = as_frag(ld16(Ql + r * QS + 16 * ks + 8 * hh));
-      s = mfma32(qa, kf[ks], s);
-      const bf16x8 oa = as_frag(ld16(Ol + r * QS + 16 * ks + 8 * hh));
-      dp = mfma32(oa, vf[ks], dp);
-    }
     const bool need_mask = (q0 + BQ > a.T) || (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      float p = exp2f(c2 * s[i]);
-      if (need_mask) {
-        const int q = q0 + acc_row(i, hh);
-        if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
-      }
-      s[i] = p;           // P
-      dp[i] = p * dp[i];  // dS (unscaled)
-    }
-    const bf16x8 pf0 = pack_frag(s, 0), pf1 = pack_frag(s, 1);
-    const bf16x8 sf0 = pack_frag(dp, 0), sf1 = pack_frag(dp, 1);
-    // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] tiles)
+    for (int j = 0; j < NQB; ++j) {
+      // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
+      f32x16 s, dp;
 #pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        const int rowq = st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
-        const uint16_t* ob = Ol + rowq * QS + col;
-        const uint16_t* qb2 = Ql + rowq * QS + col;
-        const bf16x8 oA = cat_tr(ds_tr(ob), ds_tr(ob + 8 * QS));
-        const bf16x8 qA = cat_tr(ds_tr(qb2), ds_tr(qb2 + 8 * QS));
-        dv[db] = mfma32(oA, st ? pf1 : pf0, dv[db]);
-        dk[db] = mfma32(qA, st ? sf1 : sf0, dk[db]);
+      for (int i = 0; i < 16; ++i) {
+        s[i] = rowc[32 * j + acc_row(i, hh)];
+        dp[i] = rowc[BQ + 32 * j + acc_row(i, hh)];
       }
-    }
-    // dS^T image: lane's key row, 4 consecutive queries per 8-byte store
-    {
-      uint16_t* srow = Sl + (w * 32 + r) * DSS;
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const bf16x8 qa = as_frag(ld16(Ql + I::off(32 * j + r, 16 * ks + 8 * hh)));
+        s = mfma32(qa, kf[ks], s);
+        const bf16x8 oa = as_frag(ld16(Ol + I::off(32 * j + r, 16 * ks + 8 * hh)));
+        dp = mfma32(oa, vf[ks], dp);
+      }
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        float p = exp2f(c2 * s[i]);
+        if (need_mask) {
+          const int q = q0 + 32 * j + acc_row(i, hh);
+          if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+        }
+        s[i] = p;           // P
+        dp[i] = p * dp[i];  // dS (unscaled)
+      }
+      const bf16x8 pf0 = pack_frag(s, 0), pf1 = pack_frag(s, 1);
+      const bf16x8 sf0 = pack_frag(dp, 0), sf1 = pack_frag(dp, 1);
+      // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] images)
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+        for (int st = 0; st < 2; ++st) {
+          const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
+          const bf16x8 oA = cat_tr(ds_tr(Ol + I::off(rowq, col)), ds_tr(Ol + I::off(rowq + 8, col)));
+          const bf16x8 qA = cat_tr(ds_tr(Ql + I::off(rowq, col)), ds_tr(Ql + I::off(rowq + 8, col)));
+          dv[db] = mfma32(oA, st ? pf1 : pf0, dv[db]);
+          dk[db] = mfma32(qA, st ? sf1 : sf0, dk[db]);
+        }
+      }
+      // dS^T image: the lane's key row, 4 consecutive queries per 8-byte store
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         u32x2 v2;
         v2[0] = pack_bf16x2(dp[4 * g], dp[4 * g + 1]);
         v2[1] = pack_bf16x2(dp[4 * g + 2], dp[4 * g + 3]);
-        *reinterpret_cast<u32x2*>(srow + 8 * g + 4 * hh) = v2;
+        *reinterpret_cast<u32x2*>(Sl + IS::off(kl, 32 * j + 8 * g + 4 * hh)) = v2;
       }
     }
     __syncthreads();
-    // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one d-block per wave
-    // (waves w < NDB), summed over all BK keys on chip and stored with plain stores into the
-    // key block's slab; attn_dq_reduce_kernel sums the slabs in a fixed order (deterministic,
-    // and no fp32 atomics: they were the floor of the first version of this kernel).
-    if (w < NDB) {
-      const int db = w;
+    // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
+    // d-block) task per wave, summed over all BK keys on chip, stored into the key block's slab.
+    if (w < NTASK) {
       f32x16 acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         const int kr0 = ks * 16 + 8 * hh + tq;
-        const uint16_t* sa = Sl + kr0 * DSS + 16 * g1 + 4 * tp;
-        const uint16_t* kbp = Kl + kr0 * KS + db * 32 + 16 * g1 + 4 * tp;
-        const bf16x8 A = cat_tr(ds_tr(sa), ds_tr(sa + 4 * DSS));
-        const bf16x8 Bf = cat_tr(ds_tr(kbp), ds_tr(kbp + 4 * KS));
+        const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
+        const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
+        const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
         acc = mfma32(A, Bf, acc);
       }
       const int64_t slab = (int64_t)a.B * a.T * a.H * D;
-      float* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + db * 32 + r;
+      float* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int q = q0 + acc_row(i, hh);
+        const int q = q0 + 32 * tq_blk + acc_row(i, hh);
         if (q < a.T) dq[(int64_t)q * a.H * D] = acc[i];
       }
     }

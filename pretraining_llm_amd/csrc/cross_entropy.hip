@@ -20,20 +20,27 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
                                                          const int64_t* __restrict__ targets, int V,
                                                          int ignore_index, float* __restrict__ loss,
                                                          uint16_t* __restrict__ dlogits, const float* __restrict__ inv_n) {
+  // The row is held PACKED (bf16, 4 VGPRs per 8 logits) so a 512-thread block needs ~52
+  // VGPRs for V = 50304 and several blocks fit per CU; exp2 is recomputed in the output
+  // pass instead of being stored (VALU is idle in this HBM-bound kernel).
+  constexpr float LOG2E = 1.4426950408889634f;
   __shared__ float scratch[CE_WAVES];
   const int row = blockIdx.x;
   const uint16_t* x = logits + (size_t)row * ld;
   const int nch = V >> 3;
-  float v[CH][8];
+  u32x4 v[CH];
   float m = -INFINITY;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = threadIdx.x + CE_THREADS * k;
-    if (c < nch) {
-      unpack8(ld16(x + c * 8), v[k]);
+    v[k] = c < nch ? ld16(x + c * 8) : u32x4{0xff80ff80u, 0xff80ff80u, 0xff80ff80u, 0xff80ff80u};  // -inf
+  }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) m = fmaxf(m, v[k][j]);
-    }
+  for (int k = 0; k < CH; ++k) {
+    float f[8];
+    unpack8(v[k], f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) m = fmaxf(m, f[j]);
   }
   // scalar tail when V % 8 != 0
   const int tail0 = nch * 8;
@@ -44,44 +51,45 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
     m = fmaxf(m, tv);
   }
   m = block_max<CE_WAVES>(m, scratch);
+  const float mc = m * LOG2E;
+  // opaque to the optimiser: keeps only the packed row live across the passes
+#pragma unroll
+  for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
-    const int c = threadIdx.x + CE_THREADS * k;
-    if (c < nch) {
+    float f[8];
+    unpack8(v[k], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        v[k][j] = __expf(v[k][j] - m);
-        s += v[k][j];
-      }
-    }
+    for (int j = 0; j < 8; ++j) s += exp2f(__builtin_fmaf(f[j], LOG2E, -mc));
   }
-  if (tj < V) {
-    tv = __expf(tv - m);
-    s += tv;
-  }
+  if (tj < V) s += exp2f(__builtin_fmaf(tv, LOG2E, -mc));
   s = block_sum<CE_WAVES>(s, scratch);
+#pragma unroll
+  for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
   const int64_t t = targets[row];
   const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
   if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - bf2f(x[t])) : 0.f;
   if (!WRITE_GRAD) return;
   __syncthreads();  // every lane has read its logits before in-place overwrite (x may alias dlogits)
-  const float scale = valid ? (*inv_n) / s : 0.f;
+  const float in = *inv_n;
+  const float scale = valid ? in / s : 0.f;
   uint16_t* dx = dlogits + (size_t)row * ld;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     const int c = threadIdx.x + CE_THREADS * k;
     if (c < nch) {
-      float o[8];
+      float f[8];
+      unpack8(v[k], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = v[k][j] * scale;
-      if (valid && (int)(t >> 3) == c) o[t & 7] -= *inv_n;
-      st16(dx + c * 8, pack8(o));
+      for (int j = 0; j < 8; ++j) f[j] = exp2f(__builtin_fmaf(f[j], LOG2E, -mc)) * scale;
+      if (valid && (int)(t >> 3) == c) f[t & 7] -= in;
+      st16(dx + c * 8, pack8(f));
     }
   }
   if (tj < V) {
-    float o = tv * scale;
-    if (valid && tj == t) o -= *inv_n;
+    float o = exp2f(__builtin_fmaf(tv, LOG2E, -mc)) * scale;
+    if (valid && tj == t) o -= in;
     dx[tj] = f2bf_bits(o);
   }
 }

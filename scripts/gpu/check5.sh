@@ -2,11 +2,11 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 900 python -m pytest tests/test_kernels_gpu.py -q -x -p no:cacheprovider > gpurun_out/t5.log 2>&1
+timeout -k 10 900 python -m pytest tests/test_kernels_gpu.py -q -x -p no:cacheprovider > gpurun_out/t6.log 2>&1
 rc=$?
-tail -3 gpurun_out/t5.log
+tail -3 gpurun_out/t6.log
 if [ $rc -gt 1 ]; then echo "stopping after pytest rc=$rc"; exit $rc; fi
-if [ $rc -eq 1 ]; then grep -E "^E |FAILED" gpurun_out/t5.log | head -20; exit 1; fi
-timeout -k 10 400 python bench.py --steps 10 --warmup 3 --batch 64 > gpurun_out/b5_64.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/b5_64.log; exit 4; }
-tail -1 gpurun_out/b5_64.log | cut -c1-300
-bash scripts/gpu/prof.sh prof5 --steps 4 --warmup 2 --batch 64
+if [ $rc -eq 1 ]; then grep -E "^E |FAILED" gpurun_out/t6.log | head -20; exit 1; fi
+timeout -k 10 400 python bench.py --steps 10 --warmup 3 --batch 64 > gpurun_out/b6_64.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/b6_64.log; exit 4; }
+tail -1 gpurun_out/b6_64.log | cut -c1-300
+bash scripts/gpu/prof.sh prof6 --steps 4 --warmup 2 --batch 64
