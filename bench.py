@@ -28,6 +28,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 METRIC = "tokens/sec (whole node) pretraining GPT-2-small seq1024 at 1/2/4/8 MI355X"
+OTHER_METRIC = "tokens/sec (whole node) pretraining {model} seq{seq}"
 
 
 def parse(argv=None):
@@ -38,7 +39,8 @@ def parse(argv=None):
     ap.add_argument("--model", default="gpt2-small")
     ap.add_argument("--batch", type=int, default=int(os.environ.get("PLLM_BENCH_BATCH", "64")),
                     help="micro-batch (sequences) per GPU")
-    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--seq", type=int, default=None, help="sequence length (default: the model's context length)")
+    ap.add_argument("--act-ckpt", type=int, default=None, help="force activation checkpointing on (1) / off (0)")
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--grad-clip", type=float, default=1.0)
@@ -74,8 +76,12 @@ def main(argv=None):
 
     torch.manual_seed(1234)
     mcfg = get_preset(args.model)
+    if args.seq is None:
+        args.seq = mcfg.context_length
     if args.seq != mcfg.context_length:
         mcfg = mcfg.replace(context_length=max(args.seq, mcfg.context_length))
+    if args.act_ckpt is not None:
+        mcfg = mcfg.replace(activation_checkpointing=bool(args.act_ckpt))
     model = GPT(mcfg).to(device=dev, dtype=torch.bfloat16)
     opt = FlatAdamW(model, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
                     max_grad_norm=args.grad_clip)
@@ -122,7 +128,8 @@ def main(argv=None):
     flops_tok = mcfg.flops_per_token(T)
     if di.is_master:
         rec = {
-            "metric": METRIC,
+            "metric": METRIC if (args.model == "gpt2-small" and T == 1024) else
+            OTHER_METRIC.format(model=args.model, seq=T),
             "value": round(tps, 1),
             "unit": "tokens/s",
             "n_gpus": world,

@@ -59,6 +59,10 @@ def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_di
     loaded = _merge_tables(per_dev)
     tunable.enable(True)
     tunable.tuning_enable(bool(tune_missing))
+    if tune_missing:
+        # bound the per-shape search (hundreds of hipBLASLt/rocBLAS candidates per shape)
+        tunable.set_max_tuning_duration(int(os.environ.get("PLLM_TUNE_MS", "4")))
+        tunable.set_max_tuning_iterations(int(os.environ.get("PLLM_TUNE_ITERS", "8")))
     tunable.set_filename(base, insert_device_ordinal=True)
     if loaded:
         tunable.read_file(per_dev)
