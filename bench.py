@@ -46,6 +46,7 @@ def parse(argv=None):
     ap.add_argument("--grad-clip", type=float, default=1.0)
     ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
     ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
+    ap.add_argument("--cuda-graph", action="store_true", help="replay the whole step as one captured hipGraph")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -102,6 +103,15 @@ def main(argv=None):
         opt.zero_grad()
         return loss
 
+    if args.cuda_graph:
+        from pretraining_llm_amd.train.graph import GraphedTrainStep
+        x0, y0 = loader.next()
+        gstep = GraphedTrainStep(model, opt, engine, B, T, dev, warmup=2).capture(x0, y0, 6e-4)
+
+        def step():  # noqa: F811
+            x, y = loader.next()
+            return gstep(x, y, 6e-4)
+
     model.train()
     for i in range(args.warmup):
         loss = step()
@@ -143,7 +153,7 @@ def main(argv=None):
             "data": "synthetic (native token loader over a generated uint16 shard), random-init weights",
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
                        "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "backend": args.backend,
-                       "tokens_per_step": B * T * world, "tuned_gemms": tuned},
+                       "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph)},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),
             "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),
             "final_loss": round(final_loss, 4),

@@ -1,0 +1,62 @@
+"""Microbenchmark: weight-gradient GEMM dW[P,Q] += dY[M,P]^T X[M,Q] on MI355X,
+hand-written gfx950 kernel (torch.ops.pllm.wgrad) vs hipBLASLt/rocBLAS (torch addmm_,
+with the shipped TunableOp selections).  Interleaved rounds in one process."""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--M", type=int, default=65536)
+    ap.add_argument("--rounds", type=int, default=3)
+    args = ap.parse_args()
+    from pretraining_llm_amd.ops import _lib
+    from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
+    _lib.require()
+    enable_tuned_gemms(0)
+    dev = torch.device("cuda")
+    M = args.M
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (50304, 768)]
+    out = []
+    for P, Q in shapes:
+        torch.manual_seed(0)
+        dy = (torch.randn(M, P, device=dev) * 0.1).bfloat16()
+        x = torch.randn(M, Q, device=dev).bfloat16()
+        tgt = torch.zeros(P, Q, device=dev, dtype=torch.bfloat16)
+        # correctness on the first 4096 rows
+        r = torch.ops.pllm.wgrad(dy[:4096], x[:4096])
+        ref = dy[:4096].float().t() @ x[:4096].float()
+        rel = ((r.float() - ref).norm() / ref.norm()).item()
+        flops = 2.0 * M * P * Q
+        res = {"P": P, "Q": Q, "M": M, "rel_err": rel, "hip_us": [], "blas_us": []}
+        for _ in range(args.rounds):
+            res["hip_us"].append(1e6 * timeit(lambda: torch.ops.pllm.wgrad(dy, x, tgt)))
+            res["blas_us"].append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
+        res["hip_tflops"] = flops / (min(res["hip_us"]) * 1e-6) / 1e12
+        res["blas_tflops"] = flops / (min(res["blas_us"]) * 1e-6) / 1e12
+        print(json.dumps(res), flush=True)
+        out.append(res)
+        del dy, x, tgt
+
+
+if __name__ == "__main__":
+    main()

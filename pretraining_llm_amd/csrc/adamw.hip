@@ -7,9 +7,11 @@
 //     p *= 1 - lr*wd ;  m = b1*m + (1-b1)*g ;  v = b2*v + (1-b2)*g^2
 //     p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)
 // The reference runs this as ~5 foreach kernels over 3590 tensors plus
-// autocast weight casts every forward; here it is one launch per param group
-// over a contiguous fp32 master buffer that also writes the bf16 compute
-// weights the next forward reads (no separate cast pass).
+// autocast weight casts every forward; here it is ONE launch over a contiguous
+// fp32 master buffer that also writes the bf16 compute weights the next forward
+// reads (no separate cast pass).  Weight decay is selected per 64-element block
+// by a byte mask (parameters are 64-aligned in the flat buffer), and the step's
+// scalars can come from a device buffer so the launch can live in a hipGraph.
 #include "common.h"
 #include "kernels.h"
 
@@ -27,7 +29,13 @@ __global__ __launch_bounds__(256) void adamw_kernel(uint16_t* __restrict__ param
                                                     float b1, float b2, float eps, float wd, float inv_bc1,
                                                     float inv_sqrt_bc2, float grad_scale,
                                                     const float* __restrict__ scale_ptr,
-                                                    const uint8_t* __restrict__ wd_blocks) {
+                                                    const uint8_t* __restrict__ wd_blocks,
+                                                    const float* __restrict__ hyper) {
+  if (hyper) {  // [lr, 1/bc1, 1/sqrt(bc2)] written by the host before a graph replay
+    lr = hyper[0];
+    inv_bc1 = hyper[1];
+    inv_sqrt_bc2 = hyper[2];
+  }
   const float gs = grad_scale * (scale_ptr ? *scale_ptr : 1.f);
   const float step = lr * inv_bc1;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
@@ -117,17 +125,17 @@ namespace pllm {
 
 void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, size_t n,
                 float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
-                const float* scale_ptr, const uint8_t* wd_blocks, hipStream_t st) {
+                const float* scale_ptr, const uint8_t* wd_blocks, const float* hyper, hipStream_t st) {
   const size_t nv = n / 8;
-  const float bc1 = 1.f - powf(b1, (float)step);
-  const float bc2 = 1.f - powf(b2, (float)step);
+  const float bc1 = 1.f - powf(b1, (float)(step > 0 ? step : 1));
+  const float bc2 = 1.f - powf(b2, (float)(step > 0 ? step : 1));
   const float inv_bc1 = 1.f / bc1, inv_sqrt_bc2 = 1.f / sqrtf(bc2);
   if (grad_f32)
     hipLaunchKernelGGL(adamw_kernel<true>, dim3(grid_for(nv)), dim3(256), 0, st, (uint16_t*)param_bf16, master, m, v,
-                       grad, nv, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2, grad_scale, scale_ptr, wd_blocks);
+                       grad, nv, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2, grad_scale, scale_ptr, wd_blocks, hyper);
   else
     hipLaunchKernelGGL(adamw_kernel<false>, dim3(grid_for(nv)), dim3(256), 0, st, (uint16_t*)param_bf16, master, m,
-                       v, grad, nv, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2, grad_scale, scale_ptr, wd_blocks);
+                       v, grad, nv, lr, b1, b2, eps, wd, inv_bc1, inv_sqrt_bc2, grad_scale, scale_ptr, wd_blocks, hyper);
 }
 
 int sumsq_blocks(size_t n) { return grid_for(n / 8) < 1024 ? grid_for(n / 8) : 1024; }

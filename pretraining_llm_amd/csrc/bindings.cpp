@@ -136,6 +136,36 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
   return out;
 }
 
+// ---------------------------------------------------------------- weight-gradient GEMM
+// out[P, Q] (+)= dy[M, P]^T @ x[M, Q]; accumulates into out_acc if given, else returns a new tensor
+Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out_acc) {
+  check_bf16(dy, "dy");
+  check_bf16(x, "x");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy [M,P], x [M,Q]");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: unit column stride");
+  const int64_t M = dy.size(0), P = dy.size(1), Q = x.size(1);
+  TORCH_CHECK(P % 8 == 0 && Q % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0, "wgrad: dims % 8");
+  check_aligned16(dy, "dy");
+  check_aligned16(x, "x");
+  Tensor out;
+  if (out_acc) {
+    check_bf16(*out_acc, "out_acc");
+    TORCH_CHECK(out_acc->numel() == P * Q && out_acc->is_contiguous(), "wgrad: out_acc shape");
+    out = *out_acc;
+  } else {
+    out = at::empty({P, Q}, dy.options());
+  }
+  int S = 1, slice = 1;
+  pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
+  Tensor part = at::empty({S, P, Q}, dy.options().dtype(at::kFloat));
+  if (M > 0)
+    pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q, part.data_ptr<float>(),
+                out.data_ptr(), out_acc.has_value(), cur_stream());
+  else if (!out_acc)
+    out.zero_();
+  return out;
+}
+
 // ---------------------------------------------------------------- activations
 Tensor act_fwd(const Tensor& x, int64_t op) {
   check_bf16(x, "x");
@@ -259,7 +289,7 @@ Tensor cross_entropy(const Tensor& logits, const Tensor& targets, const std::opt
 // ---------------------------------------------------------------- optimizer
 void adamw_(Tensor& param, Tensor& master, Tensor& m, Tensor& v, const Tensor& grad, double lr, double b1, double b2,
             double eps, double wd, int64_t step, double grad_scale, const std::optional<Tensor>& scale,
-            const std::optional<Tensor>& wd_mask) {
+            const std::optional<Tensor>& wd_mask, const std::optional<Tensor>& hyper) {
   const int64_t n = master.numel();
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
               "adamw: master/m/v must be fp32");
@@ -287,9 +317,14 @@ void adamw_(Tensor& param, Tensor& master, Tensor& m, Tensor& v, const Tensor& g
     TORCH_CHECK(wd_mask->numel() * 64 >= n, "wd_mask: one byte per 64 elements");
     wm = wd_mask->data_ptr<uint8_t>();
   }
+  const float* hp = nullptr;
+  if (hyper) {  // device-side [lr, 1/bc1, 1/sqrt(bc2)] (graph-capturable step)
+    TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->is_cuda() && hyper->numel() >= 3, "adamw: hyper");
+    hp = hyper->data_ptr<float>();
+  }
   if (n)
     pllm::adamw_flat(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), gf32, n,
-                     (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)grad_scale, sp, wm,
+                     (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)grad_scale, sp, wm, hp,
                      cur_stream());
 }
 
@@ -445,6 +480,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor weight, Tensor? bias, float eps, bool rms) -> Tensor[]");
   m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!)? dw_acc=None, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor[]");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
   m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
@@ -453,7 +489,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse, bool inplace) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor? dlogits, int ignore_index) -> Tensor");
-  m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask) -> ()");
+  m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!)? dwte_acc=None, Tensor(b!)? dwpe_acc=None) -> Tensor[]");
@@ -465,6 +501,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("norm_fwd", norm_fwd);
   m.impl("norm_bwd", norm_bwd);
   m.impl("bias_grad", bias_grad);
+  m.impl("wgrad", wgrad);
   m.impl("act_fwd", act_fwd);
   m.impl("act_bwd", act_bwd);
   m.impl("act_bwd_bias", act_bwd_bias);

@@ -65,7 +65,7 @@ int cross_entropy_max_vocab();
 // adamw.hip
 void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, size_t n,
                 float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
-                const float* scale_ptr, const uint8_t* wd_blocks, hipStream_t st);
+                const float* scale_ptr, const uint8_t* wd_blocks, const float* hyper, hipStream_t st);
 int sumsq_blocks(size_t n);
 void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
 
@@ -74,6 +74,11 @@ void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* o
                    int pos_offset, int64_t V, hipStream_t st);
 void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, int64_t N,
                    int Bn, int T, int C, int64_t V, hipStream_t st);
+
+// gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
+void wgrad_plan(int M, int P, int Q, int* S, int* slice);
+void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
+           bool accumulate, hipStream_t st);
 
 // attention.hip
 bool attn_supported_head_dim(int D);

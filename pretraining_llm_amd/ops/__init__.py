@@ -100,11 +100,9 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             tgt = _acc_target(ctx.w)
+            dw = _weight_grad(dy2, x2, tgt)
             if tgt is not None:
-                tgt.addmm_(dy2.t(), x2)
                 _notify(ctx.w)
-            else:
-                dw = dy2.t() @ x2
         if ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext:
             tgt = _acc_target(ctx.b)
             if tgt is not None:
@@ -114,6 +112,28 @@ class _LinearFn(torch.autograd.Function):
                 db = _ops().bias_grad(dy2.contiguous())
         ctx.w = ctx.b = None
         return dx, dw, db, None
+
+
+import os as _os
+
+# weight-gradient GEMM engine: "hip" = hand-written split-K MFMA kernel (csrc/gemm_wgrad.hip),
+# "blas" = hipBLASLt/rocBLAS through torch (beta=1 addmm into the flat gradient)
+WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
+
+
+def _weight_grad(dy2, x2, tgt):
+    """dW = dy2^T @ x2, added into ``tgt`` when given (returns None) else returned."""
+    use_hip = WGRAD_ENGINE == "hip" and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
+    if use_hip:
+        dy2, x2 = dy2.contiguous(), x2.contiguous()
+        if tgt is not None:
+            _ops().wgrad(dy2, x2, tgt.view(dy2.shape[1], x2.shape[1]))
+            return None
+        return _ops().wgrad(dy2, x2)
+    if tgt is not None:
+        tgt.addmm_(dy2.t(), x2)
+        return None
+    return dy2.t() @ x2
 
 
 def linear(x, weight, bias=None, bias_grad_external: bool = False):
@@ -469,11 +489,9 @@ class _LMHeadCEFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             hs = h * gh  # fold the upstream scalar into the small operand, not the [N, V] gradient
             tgt = _acc_target(ctx.w)
+            dw = _weight_grad(dlogits, hs, tgt)
             if tgt is not None:
-                tgt.addmm_(dlogits.t(), hs)
                 _notify(ctx.w)
-            else:
-                dw = dlogits.t() @ hs
         if ctx.has_bias and ctx.needs_input_grad[2]:
             db = (dlogits.float().sum(0) * g).to(weight.dtype)
         ctx.w = ctx.b = None

@@ -131,11 +131,28 @@ class FlatAdamW:
         return ss.sqrt() * grad_scale
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0):
-        """One AdamW step. ``grad_scale`` multiplies the raw flat gradient (e.g. 1/world for a
-        summed all-reduce, 1/accum_steps for accumulation)."""
+    def prepare_graph_step(self, lr: float):
+        """Host half of a graph-captured step: advance the step counter and write
+        [lr, 1/bc1, 1/sqrt(bc2)] into the device buffer the captured AdamW launch reads."""
+        self.param_groups[0]["lr"] = lr
         self._sync_lr()
         self.step_count += 1
+        b1, b2 = self.betas
+        bc1 = 1.0 - b1 ** self.step_count
+        bc2 = 1.0 - b2 ** self.step_count
+        if getattr(self, "hyper", None) is None:
+            self.hyper = torch.zeros(4, dtype=torch.float32, device=self.flat_param.device)
+            self._hyper_host = torch.zeros(4, dtype=torch.float32).pin_memory()
+        self._hyper_host.copy_(torch.tensor([lr, 1.0 / bc1, 1.0 / math.sqrt(bc2), 0.0]))
+        self.hyper.copy_(self._hyper_host, non_blocking=True)
+
+    def step(self, grad_scale: float = 1.0, graph: bool = False):
+        """One AdamW step. ``grad_scale`` multiplies the raw flat gradient (e.g. 1/world for a
+        summed all-reduce, 1/accum_steps for accumulation).  ``graph=True``: the scalars come
+        from the device buffer written by ``prepare_graph_step`` (hipGraph-capturable)."""
+        if not graph:
+            self._sync_lr()
+            self.step_count += 1
         clip = None
         if self.max_grad_norm and self.max_grad_norm > 0:
             norm = self.grad_norm(grad_scale)
@@ -145,8 +162,10 @@ class FlatAdamW:
         if self.use_hip and _ops_mod.get_backend() == "auto":
             _lib.require().adamw_(self.flat_param, self.master, self.exp_avg, self.exp_avg_sq, self.flat_grad,
                                   self.lr, b1, b2, self.eps, self.weight_decay, self.step_count, grad_scale, clip,
-                                  self.wd_mask)
+                                  self.wd_mask, self.hyper if graph else None)
             return
+        if graph:
+            raise RuntimeError("graph-captured optimizer steps need the HIP AdamW kernel (bf16 params on GPU)")
         g32 = self.flat_grad.float() * grad_scale
         if clip is not None:
             g32 = g32 * clip
