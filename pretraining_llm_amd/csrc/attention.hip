@@ -16,12 +16,15 @@
 //    S^T = K.Q^T is computed with the QUERY on the MFMA lane, so the softmax row
 //    statistics (m, l) are per-lane scalars and the P^T accumulator is directly
 //    the B operand of O^T += V^T.P^T (no LDS round trip for P).
-//  * backward: one workgroup = 4 waves = 128 keys of one (batch, kv-head); each
+//  * backward: one workgroup = NW waves = 32*NW keys of one (batch, kv-head)
+//    (D<=64: 8 waves/256 keys, D=128: 4 waves/128 keys); each
 //    wave keeps dK^T/dV^T for its 32 keys in registers across all query blocks
 //    (and all query heads of a GQA group), so dK/dV need no cross-workgroup sum.
 //    S and dP are computed with the KEY on the lane and initialised with
 //    -LSE/scale and -delta, so P = exp2(c*S') and dS = P*dP' need no extra pass.
-//    dQ per key block is summed over its 128 keys on chip and written to a
+//    Under the causal mask a wave whose 32 keys all follow a 32-query sub-block
+//    skips it outright (zeros into the dS^T image), and dQ k-steps past the
+//    diagonal are skipped.  dQ per key block is summed over its keys on chip and written to a
 //    per-key-block fp32 slab; a second kernel sums the slabs in a fixed order
 //    (deterministic; the first version's fp32 atomics were its floor).
 #include "common.h"
@@ -285,25 +288,32 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
   if (row < nrows && c == 0) a.delta[((int64_t)b * a.H + h) * a.T + t] = acc;
 }
 
+// Backward tiling.  NW waves per workgroup, each owning 32 keys (BK = 32*NW keys per
+// workgroup); BQ query rows per iteration processed as NQB sub-blocks of 32.
+//   D <= 64 : 8 waves, 256 keys, 128 queries per iteration -> every dQ task (32 q x 32 d)
+//             sums all 256 keys on chip; half the dQ slabs of a 128-key block.
+//   D = 128 : 4 waves, 128 keys, 32 queries (register budget: dK^T/dV^T alone are 128 regs).
 template <int D>
 struct BwdCfg {
-  static constexpr int BK = 128;
-  static constexpr int BQ = D <= 64 ? 64 : 32;  // query rows per iteration (register budget)
-  static constexpr int NQB = BQ / 32;           // 32-row MFMA sub-blocks per iteration
+  static constexpr int NW = D <= 64 ? 8 : 4;
+  static constexpr int NT = 64 * NW;
+  static constexpr int BK = 32 * NW;
+  static constexpr int BQ = D <= 64 ? 128 : 32;
+  static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
-  static constexpr int QLPT = (BQ * CPR + 255) / 256;
-  static constexpr int KLPT = BK * CPR / 256;
+  static constexpr int QLPT = (BQ * CPR + NT - 1) / NT;
+  static constexpr int KLPT = (BK * CPR + NT - 1) / NT;
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;
 };
 
 // D=128 keeps dK^T/dV^T (128 regs) + K/V fragments (64) + S/dP in registers: one wave per
 // SIMD with the full register file instead of spilling at the 2-waves/SIMD budget.
 template <int D>
-__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D>;
   using I = Img<D>;
   using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
-  constexpr int BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
+  constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
   constexpr int QLPT = C::QLPT, KLPT = C::KLPT;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
@@ -321,6 +331,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
   const int G = a.H / a.Hkv;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int k0 = kb * BK, kl = w * 32 + r, key = k0 + kl;
+  const int kw0 = k0 + w * 32;            // first key of this wave
   const int off = a.S - a.T;
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
@@ -335,9 +346,11 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
   // whole K block into LDS for the dQ product
 #pragma unroll
   for (int i = 0; i < KLPT; ++i) {
-    const int c = tid + 256 * i, row = c / CPR, col = c % CPR, kk = k0 + row;
-    u32x4 v = kk < a.S ? ld16(kp + (int64_t)kk * a.k_st + col * 8) : u32x4{0u, 0u, 0u, 0u};
-    st16(Kl + I::off(row, col * 8), v);
+    const int c = tid + NT * i, row = c / CPR, col = c % CPR, kk = k0 + row;
+    if (c < BK * CPR) {
+      u32x4 v = kk < a.S ? ld16(kp + (int64_t)kk * a.k_st + col * 8) : u32x4{0u, 0u, 0u, 0u};
+      st16(Kl + I::off(row, col * 8), v);
+    }
   }
 
   f32x16 dk[NDB], dv[NDB];
@@ -363,7 +376,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
     const uint16_t* dop = a.dO + b * a.do_sb + (int64_t)h * a.do_sh;
 #pragma unroll
     for (int i = 0; i < QLPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, col = c % CPR, q = q0 + row;
+      const int c = tid + NT * i, row = c / CPR, col = c % CPR, q = q0 + row;
       if (c < BQ * CPR && q < a.T) {
         qr[i] = ld16(qp + (int64_t)q * a.q_st + col * 8);
         dor[i] = ld16(dop + (int64_t)q * a.do_st + col * 8);
@@ -391,7 +404,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done
 #pragma unroll
     for (int i = 0; i < QLPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
+      const int c = tid + NT * i, row = c / CPR, col = c % CPR;
       if (c < BQ * CPR) {
         st16(Ql + I::off(row, col * 8), qr[i]);
         st16(Ol + I::off(row, col * 8), dor[i]);
@@ -404,6 +417,15 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
     const bool need_mask = (q0 + BQ > a.T) || (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
+      const int qj0 = q0 + 32 * j;
+      // causal: every key of this wave lies after every query of the sub-block -> P = dS = 0
+      const bool dead = a.causal && kw0 > qj0 + 31 + off;
+      if (dead) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<u32x2*>(Sl + IS::off(kl, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
+        continue;
+      }
       // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
       f32x16 s, dp;
 #pragma unroll
@@ -422,7 +444,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
       for (int i = 0; i < 16; ++i) {
         float p = exp2f(c2 * s[i]);
         if (need_mask) {
-          const int q = q0 + 32 * j + acc_row(i, hh);
+          const int q = qj0 + acc_row(i, hh);
           if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
         }
         s[i] = p;           // P
@@ -455,9 +477,14 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave, summed over all BK keys on chip, stored into the key block's slab.
     if (w < NTASK) {
+      const int qt0 = q0 + 32 * tq_blk;
+      // causal: key steps entirely after the task's last query contribute zeros -> skip
+      int ks_end = BK / 16;
+      if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
       f32x16 acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
+        if (ks >= ks_end) break;
         const int kr0 = ks * 16 + 8 * hh + tq;
         const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
         const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
@@ -468,7 +495,7 @@ __global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwd
       float* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int q = q0 + 32 * tq_blk + acc_row(i, hh);
+        const int q = qt0 + acc_row(i, hh);
         if (q < a.T) dq[(int64_t)q * a.H * D] = acc[i];
       }
     }
@@ -535,6 +562,8 @@ namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
+int attn_bwd_key_block(int D) { return D <= 64 ? BwdCfg<64>::BK : BwdCfg<128>::BK; }
+
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + 127) / 128;
@@ -545,9 +574,9 @@ template <int D>
 static void attn_bwd_t(const AttnBwdArgs& a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
-  const int nkb = (a.S + 127) / 128;
+  const int nkb = (a.S + BwdCfg<D>::BK - 1) / BwdCfg<D>::BK;
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_kernel<D>, dim3(nkb * a.B * a.Hkv), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(attn_bwd_kernel<D>, dim3(nkb * a.B * a.Hkv), dim3(BwdCfg<D>::NT), 0, st, a);
   hipLaunchKernelGGL(attn_dq_reduce_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
 }
 

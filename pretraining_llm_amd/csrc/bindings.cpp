@@ -445,7 +445,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   auto f32 = q.options().dtype(at::kFloat);
   Tensor delta = at::empty({B, H, T}, f32);
   // per-key-block dQ partial slabs (attention.hip: plain stores + ordered reduce, no atomics)
-  const int64_t nkb = (S + 127) / 128;
+  const int64_t kbk = pllm::attn_bwd_key_block((int)D);
+  const int64_t nkb = (S + kbk - 1) / kbk;
   Tensor dq_acc = at::empty({nkb, B, T, H, D}, f32);
   AttnBwdArgs a{};
   a.q = (const uint16_t*)q.data_ptr();

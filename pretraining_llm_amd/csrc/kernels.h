@@ -82,6 +82,7 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
 
 // attention.hip
 bool attn_supported_head_dim(int D);
+int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st);
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st);
 

@@ -117,8 +117,9 @@ class _LinearFn(torch.autograd.Function):
 import os as _os
 
 # weight-gradient GEMM engine: "hip" = hand-written split-K MFMA kernel (csrc/gemm_wgrad.hip),
-# "blas" = hipBLASLt/rocBLAS through torch (beta=1 addmm into the flat gradient)
-WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
+# "blas" = hipBLASLt/rocBLAS through torch (beta=1 addmm into the flat gradient; default:
+# measured 650-985 TFLOP/s vs 460-640 for the hand-written kernel at M=65536, bench/gemm_bench.py)
+WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "blas")
 
 
 def _weight_grad(dy2, x2, tgt):

@@ -16,3 +16,5 @@ tail -1 gpurun_out/b8_$w.log | cut -c1-200
 done
 timeout -k 10 400 python bench.py --steps 10 --warmup 3 --cuda-graph > gpurun_out/b8_graph.log 2>&1 || { echo "graph bench failed"; tail -20 gpurun_out/b8_graph.log; exit 5; }
 tail -1 gpurun_out/b8_graph.log | cut -c1-200
+timeout -k 10 600 python bench/attn_bench.py > gpurun_out/attn1.log 2>&1 || { echo "attn bench failed"; tail -20 gpurun_out/attn1.log; exit 6; }
+grep -v amdgpu.ids gpurun_out/attn1.log | cut -c1-600
