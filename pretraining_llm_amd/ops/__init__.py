@@ -124,7 +124,8 @@ WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "blas")
 
 def _weight_grad(dy2, x2, tgt):
     """dW = dy2^T @ x2, added into ``tgt`` when given (returns None) else returned."""
-    use_hip = WGRAD_ENGINE == "hip" and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
+    use_hip = (WGRAD_ENGINE == "hip" and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
+               and dy2.shape[0] % 64 == 0)
     if use_hip:
         dy2, x2 = dy2.contiguous(), x2.contiguous()
         if tgt is not None:
@@ -335,6 +336,19 @@ def attention(q, k, v, causal: bool = True, scale: Optional[float] = None, retur
     else:
         o, lse = ref.attention(q, k, v, causal=causal, scale=scale)
     return (o, lse) if return_lse else o
+
+
+def attention_block_bwd(do, q, k, v, o, lse, causal: bool = True, scale: Optional[float] = None):
+    """Backward of one (query block, key block) attention product given the final output
+    ``o`` and the log-sum-exp ``lse`` [B,H,T] of the WHOLE softmax row (context-parallel
+    building block).  Returns (dq, dk, dv) in the dtype of q (HIP) or fp32 (CPU oracle)."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _hip(q):
+        dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _ops().attn_bwd(do, q, k, v, o, lse.contiguous(), dq, dk, dv, causal, scale)
+        return dq, dk, dv
+    return ref.attention_bwd(do, q, k, v, o, lse, causal=causal, scale=scale)
 
 
 # ---------------------------------------------------------------------------

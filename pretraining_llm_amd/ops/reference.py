@@ -63,6 +63,34 @@ def attention(q, k, v, causal: bool = True, scale: Optional[float] = None):
     return o.transpose(1, 2).to(q.dtype), lse
 
 
+def attention_bwd(do, q, k, v, o, lse, causal: bool = True, scale: Optional[float] = None):
+    """Flash-style backward of one attention block given the row statistics of the WHOLE
+    softmax (``lse`` [B,H,T], natural log, and the final output ``o``), so partial key
+    blocks (ring / context parallel) produce exact partial gradients.
+    Returns fp32 (dq [B,T,H,D], dk [B,S,Hkv,D], dv [B,S,Hkv,D])."""
+    B, T, H, D = q.shape
+    S, Hkv = k.shape[1], k.shape[2]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    rep = H // Hkv
+    qf, dof, of = (t.float().transpose(1, 2) for t in (q, do, o))            # B,H,T,D
+    kf = k.float().transpose(1, 2).repeat_interleave(rep, dim=1)             # B,H,S,D
+    vf = v.float().transpose(1, 2).repeat_interleave(rep, dim=1)
+    s = torch.matmul(qf, kf.transpose(-1, -2)) * scale
+    if causal:
+        mask = torch.ones(T, S, dtype=torch.bool, device=q.device).tril(diagonal=S - T)
+        s = s.masked_fill(~mask, float("-inf"))
+    p = torch.exp(s - lse.float().unsqueeze(-1))
+    dv = torch.matmul(p.transpose(-1, -2), dof)                              # B,H,S,D
+    dp = torch.matmul(dof, vf.transpose(-1, -2))
+    delta = (dof * of).sum(-1, keepdim=True)
+    ds = p * (dp - delta)
+    dq = torch.matmul(ds, kf) * scale
+    dk = torch.matmul(ds.transpose(-1, -2), qf) * scale
+    dk = dk.view(B, Hkv, rep, S, D).sum(2)
+    dv = dv.view(B, Hkv, rep, S, D).sum(2)
+    return dq.transpose(1, 2), dk.transpose(1, 2), dv.transpose(1, 2)
+
+
 def gelu_tanh(x):
     return F.gelu(x.float(), approximate="tanh").to(x.dtype)
 

@@ -4,3 +4,4 @@ from .tensor import (ColumnParallelLinear, RowParallelLinear, TensorParallelAtte
                      gather_from_tensor_parallel, head_to_seq_all_to_all, reduce_from_tensor_parallel,
                      reduce_scatter_to_sequence, scatter_to_sequence, seq_to_head_all_to_all,
                      ulysses_attention)
+from .context import ring_attention, zigzag_positions, zigzag_shard, zigzag_unshard  # noqa: F401

@@ -354,7 +354,10 @@ def test_bias_grad_kernels():
     assert _rel(b, xf.grad.sum(0)) < 1e-2
 
 
-@pytest.mark.parametrize("M,P,Q", [(1000, 200, 136), (4096, 768, 768), (2048, 512, 2304), (777, 1024, 256)])
+# (2048, 200, 136): tiles past P and Q; (4096, 768, 768) / (2048, 512, 2304): split-K slab path;
+# (1024, 4096, 4096): 256 tiles -> single slice, accumulated in the kernel epilogue
+@pytest.mark.parametrize("M,P,Q", [(2048, 200, 136), (4096, 768, 768), (2048, 512, 2304), (1024, 4096, 4096),
+                                   (640, 1024, 256)])
 def test_wgrad_kernel(M, P, Q):
     torch.manual_seed(13)
     dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
@@ -371,6 +374,8 @@ def test_wgrad_kernel(M, P, Q):
     v = big[:, 32:32 + P]
     out3 = torch.ops.pllm.wgrad(v, x)
     assert _rel(out3, v.float().t() @ x.float()) < 5e-3
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.wgrad(dy[:M - 8], x[:M - 8])  # token count must be a multiple of 64
 
 
 def test_graphed_train_step_matches_eager():
@@ -420,3 +425,33 @@ def test_graphed_train_step_matches_eager():
         o3.zero_grad()
         assert abs(lg - le.item()) < 1e-3 * max(1.0, abs(le.item())), (i, lg, le.item())
     assert eager[0] > 0
+
+
+def test_attention_block_bwd_partial_keys():
+    """Context-parallel building block: the backward of each key block, given the final
+    o/lse of the whole row, sums to the full attention gradient (HIP kernels)."""
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.ops import reference as ref
+    torch.manual_seed(21)
+    B, T, H, Hkv, D = 2, 256, 4, 2, 64
+    q = torch.randn(B, 2 * T, H, D, device=DEV).bfloat16()
+    k = torch.randn(B, 2 * T, Hkv, D, device=DEV).bfloat16()
+    v = torch.randn(B, 2 * T, Hkv, D, device=DEV).bfloat16()
+    do = torch.randn(B, 2 * T, H, D, device=DEV).bfloat16()
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = ref.attention(qf, kf, vf, causal=True)
+    of.backward(do.float())
+    # second query half: key block 0 fully visible, key block 1 = the causal diagonal
+    q2, do2 = q[:, T:], do[:, T:]
+    o0, l0 = ops.attention(q2, k[:, :T], v[:, :T], causal=False, return_lse=True)
+    o1, l1 = ops.attention(q2, k[:, T:], v[:, T:], causal=True, return_lse=True)
+    lse = torch.logaddexp(l0, l1)
+    o = (o0.float() * torch.exp(l0 - lse).transpose(1, 2).unsqueeze(-1)
+         + o1.float() * torch.exp(l1 - lse).transpose(1, 2).unsqueeze(-1)).bfloat16()
+    assert _rel(o, of[:, T:]) < 1e-2
+    g0 = ops.attention_block_bwd(do2, q2, k[:, :T], v[:, :T], o, lse, causal=False)
+    g1 = ops.attention_block_bwd(do2, q2, k[:, T:], v[:, T:], o, lse, causal=True)
+    assert _rel(g0[0].float() + g1[0].float(), qf.grad[:, T:]) < 2e-2
+    # keys of block 1 are only seen by the second query half
+    assert _rel(g1[1], kf.grad[:, T:]) < 2e-2
+    assert _rel(g1[2], vf.grad[:, T:]) < 2e-2
