@@ -145,6 +145,7 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1, "wgrad: unit column stride");
   const int64_t M = dy.size(0), P = dy.size(1), Q = x.size(1);
   TORCH_CHECK(P % 8 == 0 && Q % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0, "wgrad: dims % 8");
+  TORCH_CHECK(M % 64 == 0, "wgrad: M (tokens) must be a multiple of 64");
   check_aligned16(dy, "dy");
   check_aligned16(x, "x");
   Tensor out;
@@ -157,9 +158,10 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   }
   int S = 1, slice = 1;
   pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
-  Tensor part = at::empty({S, P, Q}, dy.options().dtype(at::kFloat));
+  Tensor part = at::empty({S > 1 ? S : 0, P, Q}, dy.options().dtype(at::kFloat));
   if (M > 0)
-    pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q, part.data_ptr<float>(),
+    pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
+                S > 1 ? part.data_ptr<float>() : nullptr,
                 out.data_ptr(), out_acc.has_value(), cur_stream());
   else if (!out_acc)
     out.zero_();

@@ -1,26 +1,29 @@
 // Weight-gradient GEMM for linear layers on gfx950 MFMA:
 //     dW[P, Q] (+)= sum_m dY[m, P] * X[m, Q]          (bf16 in, fp32 accumulate)
 // i.e. the reduction runs over the token dimension (M = batch*seq, 65536 for the
-// headline config) while the output is small (768x768 .. 3072x768).  hipBLASLt's
-// best candidates for these shapes ran at 0.40-0.82 PFLOP/s on MI355X
-// (profiles/r1_prof4*), far below its forward GEMMs, because a 768x768 output has
-// only 9 tiles of 256x256 to spread over 256 CUs.
+// headline config) while the output is small (768x768 .. 50304x768).  Both operands
+// are token-major, the "NT" case hipBLASLt serves worst: 0.39-0.99 PFLOP/s in the
+// GPT-2-small step against 1.0-1.37 for the forward GEMMs of the same shapes
+// (profiles/r1_prof5*).
 //
 // Design (CDNA4):
-//  * split-K over tokens: grid = (output tiles) x (S token slices), slice-major so
-//    the workgroups that share a slice's dY/X panels run together (L2 reuse);
-//  * workgroup tile 256x256, 4 waves each owning a 128x128 sub-tile as 4x4
-//    v_mfma_f32_32x32x16_bf16 accumulators (256 accumulator registers: one wave per
-//    SIMD with the full 512-entry register file, __launch_bounds__(256, 1));
-//  * both operands are token-major in memory, so both MFMA fragments come from
-//    ds_read_b64_tr_b16 transposed reads of swizzled [64 tokens][128] LDS images
-//    (conflict-free, see Img<128> in attention.hip);
-//  * 64-token stages double-buffered through registers: the next stage's 16 x 16-B
-//    global loads are issued before the current stage's 64 MFMAs and written to LDS
-//    after them, one barrier per stage;
-//  * fp32 partial tiles go to a [S][P][Q] slab; a reduce kernel sums the slices in a
-//    fixed order and adds the result into the bf16 gradient (the optimizer's flat
-//    buffer), so the accumulate is fused and the result is deterministic.
+//  * split-K over tokens: work item = (token slice, 256x256 output tile), slice-major,
+//    and the work items are dealt to the 8 XCDs in contiguous ranges (xcd_remap), so
+//    the tiles that share a slice's dY/X panels run on one XCD and share its L2;
+//  * 8 waves per workgroup (2 per SIMD) as 2 (P) x 4 (Q), each owning a 128x64 sub-tile
+//    as 4x2 v_mfma_f32_32x32x16_bf16 accumulators;
+//  * operands staged HBM/L2 -> LDS by global_load_lds (16 B per lane, no staging
+//    registers): 64-token stages, double-buffered, the next stage's DMA in flight under
+//    the current stage's MFMAs, one barrier per stage.  The LDS images are [64][128]
+//    halves with the XOR chunk swizzle of attention.hip's Img<128>; the DMA writes
+//    lane-linear 1-KiB pieces, so the swizzle is applied to the per-lane SOURCE
+//    address instead;
+//  * both MFMA fragments come from ds_read_b64_tr_b16 transposed reads (the reduction
+//    index is the image row);
+//  * one slice: the tile is added straight into the bf16 gradient; several: fp32
+//    partial tiles go to a [S][P][Q] slab and a reduce kernel sums the slices in a
+//    fixed order into the bf16 gradient (deterministic, accumulate fused).
+// Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include "common.h"
 #include "kernels.h"
 
@@ -37,104 +40,140 @@ PLLM_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
   s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
+// global -> LDS DMA of 16 B per lane into [m0 + 16*lane] (m0 = wave-uniform LDS byte address).
+// Written as inline asm on purpose: for the builtin, hipcc's waitcnt pass cannot tell the
+// buffer being filled from the one being read and drains the prefetch (vmcnt(0)) before
+// the first ds_read of every stage.  The caller retires these loads with an explicit
+// "s_waitcnt vmcnt(0)" ahead of the barrier that publishes the stage.
+PLLM_DEV void glds16(const void* src, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
+               "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+               : "memory", "m0");
+}
 PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
 
 // [rows][128] bf16 image, 16-B chunk ch of row r at ch ^ f(r) (conflict-free tr reads)
-PLLM_DEV int img_off(int r, int col) {
-  const int f = ((r & 3) << 2) | ((r >> 2) & 3);
-  return r * 128 + (((col >> 3) ^ f) << 3) + (col & 7);
-}
+PLLM_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+PLLM_DEV int img_off(int r, int col) { return r * 128 + (((col >> 3) ^ swz(r)) << 3) + (col & 7); }
 
-constexpr int BT = 256;          // output tile (P and Q)
-constexpr int BKM = 64;          // tokens per stage
-constexpr int HALF = BKM * 128;  // elements of one [64][128] image
-constexpr int LDS_ELEMS = 2 * 2 * 2 * HALF;  // 2 buffers x {A, B} x 2 halves
+constexpr int BT = 256;             // output tile (P and Q)
+constexpr int BKM = 64;             // tokens per stage
+constexpr int NT = 512;             // 8 waves
+constexpr int HALF = BKM * 128;     // elements of one [64][128] image
+constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 2,3 (64 KiB)
 
-__global__ __launch_bounds__(256, 1) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                       const uint16_t* __restrict__ B, int64_t ldb, int M, int P,
-                                                       int Q, int S, int slice, float* __restrict__ part) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[LDS_ELEMS];
+__global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
+                                                   const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
+                                                   int S, int slice, float* __restrict__ part,
+                                                   uint16_t* __restrict__ out, int accumulate) {
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
-  const int s = blockIdx.x / ntiles, t = blockIdx.x % ntiles;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int s = lid / ntiles, t = lid % ntiles;
   const int p0 = (t / tiles_q) * BT, q0 = (t % tiles_q) * BT;
-  const int m_begin = s * slice, m_end = min(M, m_begin + slice);
-  const int nstage = (m_end - m_begin + BKM - 1) / BKM;
+  const int m_begin = s * slice;
+  const int nstage = (min(M, m_begin + slice) - m_begin) / BKM;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int wp = w >> 1, wq = w & 1;  // wave's 128x128 sub-tile
+  const int wp = w >> 2, wq = w & 3;  // wave's 128x64 sub-tile
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
 
-  // staging: 64 rows x 256 cols per operand = 2048 16-B chunks / 256 threads = 8 each
-  u32x4 ra[8], rb[8];
-  auto gload = [&](int st) {
-    const int m0 = m_begin + st * BKM;
+  // DMA plan: 64 pieces of 1 KiB per stage (operand x half x 16 row-quads), 8 per wave.
+  // Lane l of a piece fills image row 4*quad + l/16, chunk position l%16, which holds
+  // logical chunk (l%16) ^ swz(row).  Columns past P/Q are clamped to a valid chunk:
+  // they only feed output rows/columns that are never stored.
+  const uint16_t* src[8];
+  int dst[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 8;
-      const int m = m0 + row;
-      const bool mok = m < m_end;
-      ra[i] = (mok && p0 + col < P) ? ld16(A + (int64_t)m * lda + p0 + col) : u32x4{0u, 0u, 0u, 0u};
-      rb[i] = (mok && q0 + col < Q) ? ld16(B + (int64_t)m * ldb + q0 + col) : u32x4{0u, 0u, 0u, 0u};
-    }
-  };
-  auto swrite = [&](int buf) {
-    uint16_t* base = smem + buf * 4 * HALF;
+  for (int k = 0; k < 8; ++k) {
+    const int pc = w * 8 + k, opnd = pc >> 5, half = (pc >> 4) & 1, quad = pc & 15;
+    const int row = 4 * quad + (lane >> 4);
+    const int col = half * 128 + (((lane & 15) ^ swz(row)) << 3);
+    if (opnd == 0) src[k] = A + (int64_t)(m_begin + row) * lda + min(p0 + col, P - 8);
+    else src[k] = B + (int64_t)(m_begin + row) * ldb + min(q0 + col, Q - 8);
+    dst[k] = (opnd * 2 + half) * HALF + quad * 512;
+  }
+  const int64_t astep = (int64_t)BKM * lda, bstep = (int64_t)BKM * ldb;
+  const unsigned lds_base = (unsigned)(uintptr_t)smem;
+  auto issue = [&](int st, int buf) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int c = tid + 256 * i, row = c >> 5, col = (c & 31) * 8;
-      const int half = col >> 7, cc = col & 127;
-      st16(base + half * HALF + img_off(row, cc), ra[i]);            // A halves at 0, 1
-      st16(base + (2 + half) * HALF + img_off(row, cc), rb[i]);      // B halves at 2, 3
+    for (int k = 0; k < 8; ++k) {
+      const int opnd = (w * 8 + k) >> 5;
+      const uint16_t* g = src[k] + st * (opnd == 0 ? astep : bstep);
+      glds16(g, lds_base + 2u * (unsigned)(buf * STAGE + dst[k]));
     }
   };
 
-  f32x16 acc[4][4];
+  f32x16 acc[4][2];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  if (nstage > 0) {
-    gload(0);
-    swrite(0);
-  }
-  __syncthreads();
+  if (nstage > 0) issue(0, 0);
   for (int st = 0; st < nstage; ++st) {
     const int buf = st & 1;
-    if (st + 1 < nstage) gload(st + 1);
-    const uint16_t* Ai = smem + buf * 4 * HALF + wp * HALF;
-    const uint16_t* Bi = smem + buf * 4 * HALF + (2 + wq) * HALF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed for every wave; nobody still reads buf ^ 1
+    if (st + 1 < nstage) issue(st + 1, buf ^ 1);
+    const uint16_t* Ai = smem + buf * STAGE + wp * HALF;
+    const uint16_t* Bi = smem + buf * STAGE + (2 + (wq >> 1)) * HALF;
+    const int bcol = (wq & 1) * 64;
 #pragma unroll
     for (int k16 = 0; k16 < BKM / 16; ++k16) {
       const int row = k16 * 16 + 8 * hh + tq;
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int col = 32 * i + 16 * g1 + 4 * tp;
         af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
-        bfr[i] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = bcol + 32 * j + 16 * g1 + 4 * tp;
+        bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
     }
-    if (st + 1 < nstage) swrite(buf ^ 1);
-    __syncthreads();
+  }
+  if (S == 1) {
+    // single slice: add the tile straight into the bf16 gradient
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int q = q0 + wq * 64 + 32 * j + r, qc = min(q, Q - 1);
+        float old[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {  // all loads first (clamped, unconditional), then the stores
+          const int p = min(p0 + wp * 128 + 32 * i + acc_row(e, hh), P - 1);
+          old[e] = accumulate ? bf2f(out[(int64_t)p * Q + qc]) : 0.f;
+        }
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const int p = p0 + wp * 128 + 32 * i + acc_row(e, hh);
+          if (p < P && q < Q) out[(int64_t)p * Q + q] = f2bf_bits(acc[i][j][e] + old[e]);
+        }
+      }
+    }
+    return;
   }
   // fp32 partial tile -> slab[s][P][Q]
-  float* out = part + (int64_t)s * P * Q;
+  float* dstp = part + (int64_t)s * P * Q;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = q0 + wq * 128 + 32 * j + r;
+    for (int j = 0; j < 2; ++j) {
+      const int q = q0 + wq * 64 + 32 * j + r;
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int p = p0 + wp * 128 + 32 * i + acc_row(e, hh);
-        if (p < P && q < Q) out[(int64_t)p * Q + q] = acc[i][j][e];
+        if (p < P && q < Q) dstp[(int64_t)p * Q + q] = acc[i][j][e];
       }
     }
   }
@@ -169,15 +208,26 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 namespace pllm {
 
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
+  // pick the slice count that fills whole rounds of 256 workgroups (one per CU) best,
+  // keeping >= 8 stages per slice; ties go to fewer slices (less slab traffic)
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-  int s = (256 + ntiles - 1) / ntiles;               // about one workgroup per CU
-  const int max_s = (M + 8 * BKM - 1) / (8 * BKM);    // keep >= 8 stages per slice
-  if (s > max_s) s = max_s;
-  if (s < 1) s = 1;
-  int sl = (M + s - 1) / s;
-  sl = (sl + BKM - 1) / BKM * BKM;
-  *S = (M + sl - 1) / sl;
-  *slice = sl;
+  const int kst = M / BKM;
+  int best = 1;
+  double best_eff = 0.0;
+  for (int s = 1; s <= 64; ++s) {
+    if (s > 1 && kst / s < 8) break;
+    const int n = ntiles * s;
+    const int rounds = (n + 255) / 256;
+    // a round of 256 costs (stages per slice); efficiency = useful / issued work
+    const double eff = (double)n / (256.0 * rounds);
+    if (eff > best_eff + 0.02) {
+      best_eff = eff;
+      best = s;
+    }
+  }
+  int st_per = (kst + best - 1) / best;
+  *slice = st_per * BKM;
+  *S = (kst + st_per - 1) / st_per;
 }
 
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
@@ -185,8 +235,9 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-  hipLaunchKernelGGL(wgrad_kernel, dim3(ntiles * S), dim3(256), 0, st, (const uint16_t*)dy, lda, (const uint16_t*)x,
-                     ldb, M, P, Q, S, slice, part);
+  hipLaunchKernelGGL(wgrad_kernel, dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda, (const uint16_t*)x,
+                     ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate);
+  if (S == 1) return;
   const int64_t PQ = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((PQ / 8 + 255) / 256)), dim3(256), 0, st, part, S, PQ,
                      (uint16_t*)out, (int)accumulate);

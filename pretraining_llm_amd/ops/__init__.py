@@ -117,9 +117,10 @@ class _LinearFn(torch.autograd.Function):
 import os as _os
 
 # weight-gradient GEMM engine: "hip" = hand-written split-K MFMA kernel (csrc/gemm_wgrad.hip),
-# "blas" = hipBLASLt/rocBLAS through torch (beta=1 addmm into the flat gradient; default:
-# measured 650-985 TFLOP/s vs 460-640 for the hand-written kernel at M=65536, bench/gemm_bench.py)
-WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "blas")
+# default: 824-1114 TFLOP/s at M=65536 vs 432-1003 for hipBLASLt's token-major "NT" kernels
+# (bench/gemm_bench.py, profiles/r1_wgrad_v2_gemm_bench.jsonl); "blas" = hipBLASLt/rocBLAS
+# through torch (beta=1 addmm into the flat gradient)
+WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
 
 
 def _weight_grad(dy2, x2, tgt):
