@@ -393,6 +393,63 @@ std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V
   return {dwte, dwpe};
 }
 
+// ---------------------------------------------------------------- batched transpose
+// Builds the descriptor table for dst[i] = src[i]^T (bf16 2-D, dims % 8 == 0, 16-B aligned);
+// returns it as a device int64 tensor [n, 6] whose last row-count column is the tile total.
+Tensor transpose_plan(const std::vector<Tensor>& src, const std::vector<Tensor>& dst) {
+  TORCH_CHECK(src.size() == dst.size() && !src.empty(), "transpose_plan: matching non-empty lists");
+  const int64_t n = (int64_t)src.size();
+  Tensor desc = at::empty({n, 6}, at::TensorOptions().dtype(at::kLong));
+  int64_t* d = desc.data_ptr<int64_t>();
+  int64_t tiles = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const Tensor &s = src[i], &t = dst[i];
+    check_bf16(s, "src");
+    check_bf16(t, "dst");
+    check_contig(s, "src");
+    check_contig(t, "dst");
+    TORCH_CHECK(s.dim() == 2 && t.dim() == 2 && t.size(0) == s.size(1) && t.size(1) == s.size(0),
+                "transpose_plan: dst must be [cols, rows] of src");
+    TORCH_CHECK(s.size(0) % 8 == 0 && s.size(1) % 8 == 0, "transpose_plan: dims must be multiples of 8");
+    check_aligned16(s, "src");
+    check_aligned16(t, "dst");
+    const int R = (int)s.size(0), C = (int)s.size(1);
+    d[i * 6 + 0] = (int64_t)(uintptr_t)s.data_ptr();
+    d[i * 6 + 1] = (int64_t)(uintptr_t)t.data_ptr();
+    d[i * 6 + 2] = R;
+    d[i * 6 + 3] = C;
+    d[i * 6 + 4] = tiles;
+    d[i * 6 + 5] = (C + 63) / 64;
+    tiles += pllm::transpose_tiles(R, C);
+  }
+  TORCH_CHECK(tiles < (1ll << 31), "transpose_plan: too many tiles");
+  return desc.to(src[0].device());
+}
+
+// total_tiles = sum over matrices of ceil(rows/64) * ceil(cols/64) (tiles past the table's
+// last matrix are guarded in the kernel: they load and store nothing)
+void transpose_run(const Tensor& desc, int64_t total_tiles) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == at::kLong && desc.dim() == 2 && desc.size(1) == 6 &&
+                  desc.is_contiguous(), "transpose_run: desc from transpose_plan");
+  pllm::transpose_batch(desc.data_ptr<int64_t>(), (int)desc.size(0), (int)total_tiles, cur_stream());
+}
+
+// ---------------------------------------------------------------- sampling
+// logits [B, V] (fp32 or bf16, unit column stride) -> int64 [B, 1] token ids
+Tensor sample(const Tensor& logits, double temperature, int64_t seed) {
+  check_gpu(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "sample: logits [B, V] with unit column stride");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16,
+              "sample: logits must be float32 or bfloat16");
+  const int64_t B = logits.size(0), V = logits.size(1);
+  TORCH_CHECK(V > 0 && V < (1ll << 31), "sample: vocabulary size");
+  Tensor out = at::empty({B, 1}, logits.options().dtype(at::kLong));
+  if (B > 0)
+    pllm::sample_tokens(logits.data_ptr(), logits.scalar_type() == at::kBFloat16, logits.stride(0), (int)B, (int)V,
+                        (float)temperature, (uint64_t)seed, out.data_ptr<int64_t>(), cur_stream());
+  return out;
+}
+
 // ---------------------------------------------------------------- attention
 void check_head_view(const Tensor& t, const char* name, int64_t D) {
   check_bf16(t, name);
@@ -496,6 +553,9 @@ TORCH_LIBRARY(pllm, m) {
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!)? dwte_acc=None, Tensor(b!)? dwpe_acc=None) -> Tensor[]");
+  m.def("transpose_plan(Tensor[] src, Tensor[] dst) -> Tensor");
+  m.def("transpose_run(Tensor desc, int total_tiles) -> ()");
+  m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale) -> ()");
 }
@@ -517,6 +577,9 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("sumsq", sumsq);
   m.impl("embedding_fwd", embedding_fwd);
   m.impl("embedding_bwd", embedding_bwd);
+  m.impl("transpose_plan", transpose_plan);
+  m.impl("transpose_run", transpose_run);
+  m.impl("sample", sample);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_bwd", attn_bwd);
 }

@@ -80,6 +80,14 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool accumulate, hipStream_t st);
 
+// transpose.hip: desc int64 [n][6] = (src, dst, rows, cols, first tile, tiles per row band)
+int transpose_tiles(int R, int C);
+void transpose_batch(const int64_t* desc, int n, int total_tiles, hipStream_t st);
+
+// sampling.hip: Gumbel-max draw of one token per row of logits [B, V] (temperature <= 0: argmax)
+void sample_tokens(const void* logits, bool bf16_in, int64_t ld, int B, int V, float temperature, uint64_t seed,
+                   int64_t* out, hipStream_t st);
+
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor

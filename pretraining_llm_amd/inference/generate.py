@@ -56,14 +56,23 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
 
 def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
                 generator: Optional[torch.Generator] = None) -> torch.Tensor:
-    """logits [B, V] (fp32) -> next token ids [B, 1]; temperature 0 = greedy."""
-    if temperature == 0.0:
-        return logits.argmax(-1, keepdim=True)
-    logits = logits / temperature
-    if top_k is not None and top_k < logits.shape[-1]:
+    """logits [B, V] (fp32) -> next token ids [B, 1]; temperature 0 = greedy.
+
+    On the GPU the draw is one fused Gumbel-max kernel (csrc/sampling.hip: an exact sample
+    of softmax(logits / T) in a single pass, seeded from ``generator``); on the CPU it is the
+    reference's softmax + multinomial (transformer.py:111-112)."""
+    if top_k is not None and top_k < logits.shape[-1] and temperature != 0.0:
         v, _ = torch.topk(logits, top_k)
         logits = logits.masked_fill(logits < v[:, [-1]], float("-inf"))
-    probs = torch.softmax(logits, dim=-1)
+    if ops._hip(logits):
+        seed = 0
+        if temperature != 0.0:
+            gdev = generator.device if generator is not None else "cpu"
+            seed = int(torch.randint(0, 2 ** 62, (1,), generator=generator, device=gdev).item())
+        return ops._ops().sample(logits, float(temperature), seed)
+    if temperature == 0.0:
+        return logits.argmax(-1, keepdim=True)
+    probs = torch.softmax(logits / temperature, dim=-1)
     return torch.multinomial(probs, num_samples=1, generator=generator)
 
 

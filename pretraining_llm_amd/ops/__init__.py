@@ -95,7 +95,7 @@ class _LinearFn(torch.autograd.Function):
         x, weight = ctx.saved_tensors
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = dy @ weight
+            dx = _dgrad(dy, weight)
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
@@ -121,6 +121,17 @@ import os as _os
 # (bench/gemm_bench.py, profiles/r1_wgrad_v2_gemm_bench.jsonl); "blas" = hipBLASLt/rocBLAS
 # through torch (beta=1 addmm into the flat gradient)
 WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
+
+
+def _dgrad(dy, weight):
+    """dx = dy @ weight.  When the optimizer keeps a transposed shadow of the weight
+    (FlatAdamW ``transposed_shadow``), the product runs as dy @ (W^T)^T: hipBLASLt's
+    kernels for that operand layout are 10-15% faster at these shapes than for
+    dy @ W (bench/gemm_fwd_bench.py: dgrad_nt vs dgrad_nn)."""
+    wt = getattr(weight, "_pllm_wT", None)
+    if wt is not None and getattr(weight, "_pllm_wT_ver", None) == weight._version:
+        return dy @ wt.t()
+    return dy @ weight
 
 
 def _weight_grad(dy2, x2, tgt):
@@ -500,7 +511,7 @@ class _LMHeadCEFn(torch.autograd.Function):
         h, weight, dlogits = ctx.saved_tensors
         g = dloss.to(torch.float32)
         gh = g.to(h.dtype)
-        dh = (dlogits @ weight).mul_(gh) if ctx.needs_input_grad[0] else None
+        dh = _dgrad(dlogits, weight).mul_(gh) if ctx.needs_input_grad[0] else None
         dw = db = None
         if ctx.needs_input_grad[1]:
             hs = h * gh  # fold the upstream scalar into the small operand, not the [N, V] gradient

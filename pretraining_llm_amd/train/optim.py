@@ -43,7 +43,7 @@ def _round_up(n: int, a: int) -> int:
 class FlatAdamW:
     def __init__(self, model: nn.Module, lr: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, decay_filter=None, grad_dtype: Optional[torch.dtype] = None,
-                 max_grad_norm: float = 0.0):
+                 max_grad_norm: float = 0.0, transposed_shadow: Optional[bool] = None):
         self.model = model
         self.lr = lr
         self.betas = betas
@@ -107,6 +107,40 @@ class FlatAdamW:
         self.last_grad_norm: Optional[torch.Tensor] = None
         # torch.optim-like surface for LR schedulers / logging
         self.param_groups = [{"lr": lr, "betas": betas, "eps": eps, "weight_decay": weight_decay}]
+        # transposed bf16 shadows of the 2-D weights, rewritten after every step: the backward
+        # data-gradient GEMMs read W^T contiguously (ops._dgrad), the layout hipBLASLt serves
+        # faster.  One extra bf16 copy of the matrices (~250 MB for GPT-2 small).
+        if transposed_shadow is None:
+            transposed_shadow = self.use_hip
+        self.shadowed = [p for p in params if transposed_shadow and p.dim() == 2]
+        sh_off, o = [], 0
+        for p in self.shadowed:
+            sh_off.append(o)
+            o += _round_up(p.numel(), ALIGN)
+        self.flat_shadow = torch.empty(o, dtype=pdtype, device=dev) if self.shadowed else None
+        for p, so in zip(self.shadowed, sh_off):
+            p._pllm_wT = self.flat_shadow[so:so + p.numel()].view(p.shape[1], p.shape[0])
+        # one batched-transpose launch refreshes every shadow (csrc/transpose.hip) when all
+        # dims are multiples of 8; otherwise per-matrix torch copies
+        self._tp_desc, self._tp_tiles = None, 0
+        if self.shadowed and self.use_hip and all(p.shape[0] % 8 == 0 and p.shape[1] % 8 == 0
+                                                  for p in self.shadowed):
+            self._tp_desc = _lib.require().transpose_plan([p.data for p in self.shadowed],
+                                                          [p._pllm_wT for p in self.shadowed])
+            self._tp_tiles = sum(((p.shape[0] + 63) // 64) * ((p.shape[1] + 63) // 64) for p in self.shadowed)
+        self.refresh_shadows()
+
+    @torch.no_grad()
+    def refresh_shadows(self):
+        if not self.shadowed:
+            return
+        if self._tp_desc is not None:
+            _lib.require().transpose_run(self._tp_desc, self._tp_tiles)
+        else:
+            for p in self.shadowed:
+                p._pllm_wT.copy_(p.t())
+        for p in self.shadowed:
+            p._pllm_wT_ver = p._version
 
     # ------------------------------------------------------------------
     def grad_view(self, i: int) -> torch.Tensor:
@@ -163,6 +197,7 @@ class FlatAdamW:
             _lib.require().adamw_(self.flat_param, self.master, self.exp_avg, self.exp_avg_sq, self.flat_grad,
                                   self.lr, b1, b2, self.eps, self.weight_decay, self.step_count, grad_scale, clip,
                                   self.wd_mask, self.hyper if graph else None)
+            self.refresh_shadows()
             return
         if graph:
             raise RuntimeError("graph-captured optimizer steps need the HIP AdamW kernel (bf16 params on GPU)")
@@ -177,6 +212,7 @@ class FlatAdamW:
             self.master.mul_(torch.where(self.wd_elem_mask, 1.0 - self.lr * self.weight_decay, 1.0))
             _ops_mod.ref.adamw_(self.flat_param, g32, self.exp_avg, self.exp_avg_sq, self.lr, b1, b2, self.eps,
                                 0.0, self.step_count, master=self.master)
+        self.refresh_shadows()
 
     # ------------------------------------------------------------------
     def state_dict(self) -> dict:
@@ -222,10 +258,13 @@ class FlatAdamW:
             self.param_groups[0]["lr"] = sd["param_groups"][0].get("lr", self.lr)
             self._sync_lr()
         self.flat_param.copy_(self.master.to(self.flat_param.dtype))
+        self.refresh_shadows()
 
+    @torch.no_grad()
     def sync_master_from_params(self):
         """Call after loading model weights directly into the params."""
         self.master.copy_(self.flat_param.float())
+        self.refresh_shadows()
 
 
 def no_decay_1d(name: str, p: torch.Tensor) -> bool:

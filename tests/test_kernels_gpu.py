@@ -455,3 +455,66 @@ def test_attention_block_bwd_partial_keys():
     # keys of block 1 are only seen by the second query half
     assert _rel(g1[1], kf.grad[:, T:]) < 2e-2
     assert _rel(g1[2], vf.grad[:, T:]) < 2e-2
+
+
+def test_fused_sampling_distribution():
+    """Gumbel-max kernel: greedy == argmax, masked logits never drawn, frequencies match softmax(l/T)."""
+    torch.manual_seed(22)
+    V = 8
+    base = torch.tensor([2.0, 1.0, 0.5, 0.0, -1.0, float("-inf"), 1.5, -0.5], device=DEV)
+    rows = 40000
+    logits = base.repeat(rows, 1)
+    ids = _ops().sample(logits, 0.7, 1234).view(-1)
+    assert ids.dtype == torch.int64 and int(ids.max()) < V
+    assert not bool((ids == 5).any())
+    freq = torch.bincount(ids, minlength=V).float() / rows
+    p = torch.softmax(base / 0.7, 0)
+    assert (freq - p).abs().max().item() < 0.01, (freq, p)
+    # different seeds -> different draws; same seed -> same draws
+    assert torch.equal(ids, _ops().sample(logits, 0.7, 1234).view(-1))
+    assert not torch.equal(ids, _ops().sample(logits, 0.7, 99).view(-1))
+    big = torch.randn(3, 50304, device=DEV)
+    assert torch.equal(_ops().sample(big, 0.0, 0).view(-1), big.argmax(-1))
+    assert torch.equal(_ops().sample(big.bfloat16(), 0.0, 0).view(-1), big.bfloat16().argmax(-1))
+
+
+def test_transposed_weight_shadows_track_steps():
+    """FlatAdamW's W^T shadows (used by the backward data-gradient GEMMs) stay equal to the
+    weights through optimizer steps, and training with them matches training without."""
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    cfg = get_preset("gpt2-tiny").replace(context_length=128, vocab_size=1024)
+    xs = [torch.randint(0, 1024, (2, 128), device=DEV) for _ in range(3)]
+    losses = {}
+    for shadow in (True, False):
+        torch.manual_seed(23)
+        m = GPT(cfg).to(DEV, torch.bfloat16)
+        opt = FlatAdamW(m, lr=1e-3, transposed_shadow=shadow)
+        assert bool(opt.shadowed) == shadow
+        out = []
+        for x in xs:
+            _, loss = m(x, x.roll(-1, 1), return_logits=False)
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+            out.append(loss.item())
+        for p in opt.shadowed:
+            assert torch.equal(p._pllm_wT, p.t())
+        losses[shadow] = (out, opt.flat_param.float().clone())
+    assert max(abs(a - b) for a, b in zip(losses[True][0], losses[False][0])) < 1e-2
+    assert _rel(losses[True][1], losses[False][1]) < 1e-2
+
+
+def test_batched_transpose_kernel():
+    torch.manual_seed(24)
+    shapes = [(72, 200), (1024, 56), (64, 64), (8, 8), (2304, 768)]
+    src = [torch.randn(s, device=DEV).bfloat16() for s in shapes]
+    dst = [torch.empty(s[1], s[0], device=DEV, dtype=torch.bfloat16) for s in shapes]
+    desc = _ops().transpose_plan(src, dst)
+    tiles = sum(((r + 63) // 64) * ((c + 63) // 64) for r, c in shapes)
+    _ops().transpose_run(desc, tiles)
+    for s, d in zip(src, dst):
+        assert torch.equal(d, s.t())
+    with pytest.raises(RuntimeError):
+        _ops().transpose_plan([torch.randn(12, 20, device=DEV).bfloat16()],
+                              [torch.empty(20, 12, device=DEV, dtype=torch.bfloat16)])
