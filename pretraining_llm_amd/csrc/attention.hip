@@ -11,8 +11,9 @@
 //    16-byte chunks (Img<D>): conflict-free both for ds_read_b128 row reads
 //    (MFMA operands that sum over D) and for ds_read_b64_tr_b16 transposed reads
 //    (operands that sum over rows), so one image serves both (guide §5.5 T2/T10).
-//  * forward: one workgroup = 4 waves = 128 query rows, K/V tiles of 64 keys
-//    double-buffered in LDS through registers (issue-early / write-late, T14).
+//  * forward: one workgroup = 4 waves, each owning 2 (D <= 64) or 1 (D = 128)
+//    blocks of 32 query rows, K/V tiles of 64 keys double-buffered in LDS through
+//    registers (issue-early / write-late, T14).
 //    S^T = K.Q^T is computed with the QUERY on the MFMA lane, so the softmax row
 //    statistics (m, l) are per-lane scalars and the P^T accumulator is directly
 //    the B operand of O^T += V^T.P^T (no LDS round trip for P).
@@ -27,6 +28,8 @@
 //    diagonal are skipped.  dQ per key block is summed over its keys on chip and written to a
 //    per-key-block fp32 slab; a second kernel sums the slabs in a fixed order
 //    (deterministic; the first version's fp32 atomics were its floor).
+#include <type_traits>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -86,9 +89,18 @@ struct Img {
 // ============================================================================
 // forward
 // ============================================================================
+// One workgroup = 4 waves.  A wave owns QB blocks of 32 query rows (QB = 2 for
+// D <= 64, 1 for D = 128: register budget), so every K fragment read from LDS and
+// every V transposed read feeds QB MFMAs instead of one, and the softmax of one
+// block overlaps the other block's MFMAs.  With QB = 2 wave w takes blocks w and
+// 7 - w of the workgroup's eight, which gives every wave the same share of the
+// causal diagonal.  A block whose keys in a tile are all masked (or whose rows lie
+// past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
 template <int D>
 struct FwdCfg {
-  static constexpr int BM = 128, BN = 64;
+  static constexpr int NW = 4;
+  static constexpr int QB = D <= 64 ? 2 : 1;
+  static constexpr int BM = NW * 32 * QB, BN = 64;
   static constexpr int CPR = D / 8;   // 16 B chunks per row
   static constexpr int LPT = BN * CPR / 256;
   static constexpr int TILE = BN * D;  // elements per K (or V) tile
@@ -99,7 +111,7 @@ template <int D>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   using C = FwdCfg<D>;
   using I = Img<D>;
-  constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, LPT = C::LPT, TILE = C::TILE;
+  constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, LPT = C::LPT, TILE = C::TILE, QB = C::QB, NW = C::NW;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
 
@@ -110,21 +122,31 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   const int bh = id % BH;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int q0 = qb * BM, qw0 = q0 + w * 32, qi = qw0 + r;
+  const int q0 = qb * BM;
   const int off = a.S - a.T;
   const uint16_t* qp = a.q + b * a.q_sb + (int64_t)h * a.q_sh;
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
-  bf16x8 qf[NKS];
+  // first query row of each of this wave's blocks, and the end of its (causal) key range
+  int qw[QB], qend[QB];
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks)
-    qf[ks] = qi < a.T ? as_frag(ld16(qp + (int64_t)qi * a.q_st + 16 * ks + 8 * hh)) : zero_frag();
+  for (int j = 0; j < QB; ++j) {
+    qw[j] = q0 + 32 * (j == 0 ? w : 2 * NW - 1 - w);
+    qend[j] = qw[j] >= a.T ? 0 : (a.causal ? min(a.S, qw[j] + 32 + off) : a.S);
+  }
+  bf16x8 qf[QB][NKS];
+#pragma unroll
+  for (int j = 0; j < QB; ++j) {
+    const int qi = qw[j] + r;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      qf[j][ks] = qi < a.T ? as_frag(ld16(qp + (int64_t)qi * a.q_st + 16 * ks + 8 * hh)) : zero_frag();
+  }
 
   int kv_end = a.S;
   if (a.causal) kv_end = min(a.S, q0 + BM + off);
   const int ntiles = (kv_end + BN - 1) / BN;
-  const int wave_kv_end = a.causal ? min(a.S, qw0 + 32 + off) : a.S;
 
   u32x4 kr[LPT], vr[LPT];
   auto gload = [&](int t) {
@@ -152,10 +174,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   };
 
-  f32x16 o[NDB];
+  f32x16 o[QB][NDB];
+  float m[QB], l[QB];  // m: running max of RAW scores (scale applied in the exponent)
 #pragma unroll
-  for (int db = 0; db < NDB; ++db) o[db] = zero16();
-  float m = -INFINITY, l = 0.f;  // m: running max of RAW scores (scale applied in the exponent)
+  for (int j = 0; j < QB; ++j) {
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) o[j][db] = zero16();
+    m[j] = -INFINITY;
+    l[j] = 0.f;
+  }
   const float c2 = a.scale_log2;
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
 
@@ -168,64 +195,76 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     const int buf = t & 1;
     if (t + 1 < ntiles) gload(t + 1);
     const int kv0 = t * BN;
-    if (kv0 < wave_kv_end) {
+    // which of this wave's blocks see keys of this tile: a compile-time mask per code
+    // path, so no MFMA is predicated (an if-converted MFMA keeps both results live)
+    const int mask = (kv0 < qend[0] ? 1 : 0) | (QB > 1 && kv0 < qend[QB - 1] ? 2 : 0);
+    auto tile = [&](auto mask_c) {
+      constexpr int MASK = decltype(mask_c)::value;
       const uint16_t* Kb = smem + buf * TILE;
       const uint16_t* Vb = smem + 2 * TILE + buf * TILE;
-      f32x16 s[2];
+      f32x16 s[QB][2];
+#pragma unroll
+      for (int j = 0; j < QB; ++j) s[j][0] = s[j][1] = zero16();
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        s[kb] = zero16();
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
           const bf16x8 kf = as_frag(ld16(Kb + I::off(kb * 32 + r, 16 * ks + 8 * hh)));
-          s[kb] = mfma32(kf, qf[ks], s[kb]);
+#pragma unroll
+          for (int j = 0; j < QB; ++j)
+            if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
         }
       }
-      const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw0 + off);
-      float mx = -INFINITY;
-      if (need_mask) {
+      bf16x8 pf[QB][4];
 #pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
+      for (int j = 0; j < QB; ++j) {
+        if (!((MASK >> j) & 1)) continue;
+        const int qi = qw[j] + r;
+        const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off);
+        if (need_mask) {
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const int key = kv0 + kb * 32 + acc_row(i, hh);
-            if (key >= a.S || (a.causal && key > qi + off)) s[kb][i] = -INFINITY;
-            mx = fmaxf(mx, s[kb][i]);
+          for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int key = kv0 + kb * 32 + acc_row(i, hh);
+              if (key >= a.S || (a.causal && key > qi + off)) s[j][kb][i] = -INFINITY;
+            }
           }
         }
-      } else {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-          for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kb][i]);
-        }
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mnew = fmaxf(m, mx);
-      const float mc = mnew == -INFINITY ? 0.f : mnew * c2;
-      const float alpha = exp2f(m * c2 - mc);  // m = -inf -> 0
-      float ls = 0.f;
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
+        // two independent max / sum chains per lane (ILP), then the lane pair (r, r+32)
+        float mx0 = -INFINITY, mx1 = -INFINITY;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          const float p = exp2f(__builtin_fmaf(s[kb][i], c2, -mc));
-          s[kb][i] = p;
-          ls += p;
+          mx0 = fmaxf(mx0, s[j][0][i]);
+          mx1 = fmaxf(mx1, s[j][1][i]);
         }
-      }
-      l = l * alpha + ls;
-      // rescale O only when some lane's running max moved (rare after the first tiles)
-      if (__any(mnew != m)) {
+        float mx = fmaxf(mx0, mx1);
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        const float mnew = fmaxf(m[j], mx);
+        const float mc = mnew == -INFINITY ? 0.f : mnew * c2;
+        const float alpha = fast_exp2(m[j] * c2 - mc);  // m = -inf -> 0
+        float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
-        for (int db = 0; db < NDB; ++db) o[db] *= alpha;
-      }
-      m = mnew;
-      bf16x8 pf[4];
+        for (int i = 0; i < 16; ++i) {
+          const float p0 = fast_exp2(__builtin_fmaf(s[j][0][i], c2, -mc));
+          const float p1 = fast_exp2(__builtin_fmaf(s[j][1][i], c2, -mc));
+          s[j][0][i] = p0;
+          s[j][1][i] = p1;
+          ls0 += p0;
+          ls1 += p1;
+        }
+        l[j] = l[j] * alpha + (ls0 + ls1);
+        // rescale O only when some lane's running max moved (rare after the first tiles)
+        if (__any(mnew != m[j])) {
 #pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        pf[2 * kb] = pack_frag(s[kb], 0);
-        pf[2 * kb + 1] = pack_frag(s[kb], 1);
+          for (int db = 0; db < NDB; ++db) o[j][db] *= alpha;
+        }
+        m[j] = mnew;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          pf[j][2 * kb] = pack_frag(s[j][kb], 0);
+          pf[j][2 * kb + 1] = pack_frag(s[j][kb], 1);
+        }
       }
 #pragma unroll
       for (int kst = 0; kst < 4; ++kst) {
@@ -233,29 +272,39 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
         for (int db = 0; db < NDB; ++db) {
           const int row = kst * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
           const bf16x8 va = cat_tr(ds_tr(Vb + I::off(row, col)), ds_tr(Vb + I::off(row + 8, col)));
-          o[db] = mfma32(va, pf[kst], o[db]);
+#pragma unroll
+          for (int j = 0; j < QB; ++j)
+            if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
         }
       }
-    }
+    };
+    if (mask == 3) tile(std::integral_constant<int, 3>{});
+    else if (mask == 1) tile(std::integral_constant<int, 1>{});
+    else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
     if (t + 1 < ntiles) swrite(buf ^ 1);
     __syncthreads();
   }
 
-  const float lt = l + __shfl_xor(l, 32, 64);
-  if (qi < a.T) {
-    const float inv = lt > 0.f ? 1.f / lt : 0.f;
-    uint16_t* op = a.o + b * a.o_sb + (int64_t)qi * a.o_st + (int64_t)h * a.o_sh;
 #pragma unroll
-    for (int db = 0; db < NDB; ++db) {
+  for (int j = 0; j < QB; ++j) {
+    const int qi = qw[j] + r;
+    const float lt = l[j] + __shfl_xor(l[j], 32, 64);
+    if (qi < a.T) {
+      const float inv = lt > 0.f ? 1.f / lt : 0.f;
+      uint16_t* op = a.o + b * a.o_sb + (int64_t)qi * a.o_st + (int64_t)h * a.o_sh;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u32x2 v2;
-        v2[0] = pack_bf16x2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv);
-        v2[1] = pack_bf16x2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hh) = v2;
+      for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          u32x2 v2;
+          v2[0] = pack_bf16x2(o[j][db][4 * g] * inv, o[j][db][4 * g + 1] * inv);
+          v2[1] = pack_bf16x2(o[j][db][4 * g + 2] * inv, o[j][db][4 * g + 3] * inv);
+          *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hh) = v2;
+        }
       }
+      if (hh == 0 && a.lse)
+        a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m[j] * c2 + log2f(lt)) * 0.69314718055994531f;
     }
-    if (hh == 0 && a.lse) a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m * c2 + log2f(lt)) * 0.69314718055994531f;
   }
 }
 
@@ -317,7 +366,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kern
   constexpr int QLPT = C::QLPT, KLPT = C::KLPT;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
-  __shared__ float rowc[2 * BQ];          // -lse/scale, -delta
+  __shared__ __attribute__((aligned(16))) float rowc[2 * BQ];  // -lse/scale, -delta
   uint16_t* Kl = smem;
   uint16_t* Ql = smem + BK * D;
   uint16_t* Ol = Ql + BQ * D;             // dO tile
@@ -427,11 +476,17 @@ __global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kern
         continue;
       }
       // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
+      // accumulator rows 4g..4g+3 are 4 consecutive queries: one 16-B LDS read each
       f32x16 s, dp;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        s[i] = rowc[32 * j + acc_row(i, hh)];
-        dp[i] = rowc[BQ + 32 * j + acc_row(i, hh)];
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
+        const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s[4 * g + e] = rs[e];
+          dp[4 * g + e] = rd[e];
+        }
       }
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
@@ -442,7 +497,7 @@ __global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kern
       }
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        float p = exp2f(c2 * s[i]);
+        float p = fast_exp2(c2 * s[i]);
         if (need_mask) {
           const int q = qj0 + acc_row(i, hh);
           if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
@@ -566,7 +621,7 @@ int attn_bwd_key_block(int D) { return D <= 64 ? BwdCfg<64>::BK : BwdCfg<128>::B
 
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
-  const int nqb = (a.T + 127) / 128;
+  const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
   hipLaunchKernelGGL(attn_fwd_kernel<D>, dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
 }
 

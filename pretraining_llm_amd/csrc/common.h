@@ -32,6 +32,11 @@ PLLM_DEV uint16_t f2bf_bits(float f) {
 PLLM_DEV uint32_t pack_bf16x2(float lo, float hi) {
   return (uint32_t)f2bf_bits(lo) | ((uint32_t)f2bf_bits(hi) << 16);
 }
+// Bare v_exp_f32 (2^x).  exp2f() lowers to a denormal-safe sequence (range test,
+// bias, v_exp, rescale: ~6 VALU) because f32 denormals are on by default; every
+// caller here feeds softmax-style sums where a flushed 2^-126 tail is harmless,
+// so the hot loops keep one transcendental per element.
+PLLM_DEV float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 PLLM_DEV float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 PLLM_DEV float hi_bf(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 

@@ -61,9 +61,9 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
     float f[8];
     unpack8(v[k], f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s += exp2f(__builtin_fmaf(f[j], LOG2E, -mc));
+    for (int j = 0; j < 8; ++j) s += fast_exp2(__builtin_fmaf(f[j], LOG2E, -mc));
   }
-  if (tj < V) s += exp2f(__builtin_fmaf(tv, LOG2E, -mc));
+  if (tj < V) s += fast_exp2(__builtin_fmaf(tv, LOG2E, -mc));
   s = block_sum<CE_WAVES>(s, scratch);
 #pragma unroll
   for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
@@ -82,13 +82,13 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
       float f[8];
       unpack8(v[k], f);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = exp2f(__builtin_fmaf(f[j], LOG2E, -mc)) * scale;
+      for (int j = 0; j < 8; ++j) f[j] = fast_exp2(__builtin_fmaf(f[j], LOG2E, -mc)) * scale;
       if (valid && (int)(t >> 3) == c) f[t & 7] -= in;
       st16(dx + c * 8, pack8(f));
     }
   }
   if (tj < V) {
-    float o = exp2f(__builtin_fmaf(tv, LOG2E, -mc)) * scale;
+    float o = fast_exp2(__builtin_fmaf(tv, LOG2E, -mc)) * scale;
     if (valid && tj == t) o -= in;
     dx[tj] = f2bf_bits(o);
   }
