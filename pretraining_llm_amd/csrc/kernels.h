@@ -77,6 +77,7 @@ void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, v
 
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
+void wgrad_set_mfma(int mf);
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool accumulate, hipStream_t st);
 
