@@ -489,6 +489,49 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   return {o, lse};
 }
 
+// single-query decode attention: q [B, 1, H, D], k/v [B, S, Hkv, D] views of a KV cache
+// (any batch/row strides).  ``seqlen``: optional int32 device scalar overriding S (the
+// number of valid cache rows) so a captured decode step replays at every position.
+Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, double scale, const c10::optional<Tensor>& seqlen) {
+  const int64_t D = q.size(3);
+  check_head_view(q, "q", D);
+  check_head_view(k, "k", D);
+  check_head_view(v, "v", D);
+  const int64_t B = q.size(0), H = q.size(2), S = k.size(1), Hkv = k.size(2);
+  TORCH_CHECK(q.size(1) == 1, "attn_decode: one query per sequence");
+  TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == S && v.size(2) == Hkv && k.size(3) == D && v.size(3) == D,
+              "attn_decode: k/v shape");
+  TORCH_CHECK(H % Hkv == 0 && pllm::attn_decode_supported((int)D, (int)(H / Hkv)),
+              "attn_decode: head dim 32/64/128 and group size 1/2/4/8 supported");
+  Tensor o = at::empty({B, 1, H, D}, q.options());
+  DecodeArgs a{};
+  a.q = (const uint16_t*)q.data_ptr();
+  a.k = (const uint16_t*)k.data_ptr();
+  a.v = (const uint16_t*)v.data_ptr();
+  a.o = (uint16_t*)o.data_ptr();
+  a.B = B; a.H = H; a.Hkv = Hkv; a.S = S; a.D = D;
+  a.q_sb = q.stride(0); a.q_sh = q.stride(2);
+  a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
+  a.v_sb = v.stride(0); a.v_st = v.stride(1); a.v_sh = v.stride(2);
+  a.o_sb = o.stride(0); a.o_sh = o.stride(2);
+  a.scale_log2 = (float)(scale * 1.4426950408889634);
+  if (seqlen.has_value()) {
+    TORCH_CHECK(seqlen->is_cuda() && seqlen->scalar_type() == at::kInt && seqlen->numel() == 1,
+                "attn_decode: seqlen must be a 1-element int32 device tensor");
+    a.seqlen = seqlen->data_ptr<int>();
+  }
+  a.splits = pllm::attn_decode_splits((int)B, (int)Hkv, (int)S);
+  Tensor part_o, part_lse;
+  if (a.splits > 1) {
+    part_o = at::empty({B, H, a.splits, D}, q.options().dtype(at::kFloat));
+    part_lse = at::empty({B, H, a.splits}, q.options().dtype(at::kFloat));
+    a.part_o = part_o.data_ptr<float>();
+    a.part_lse = part_lse.data_ptr<float>();
+  }
+  if (B > 0 && S > 0) pllm::attn_decode(a, cur_stream());
+  return o;
+}
+
 // dq/dk/dv are written into caller-provided views (e.g. slices of a packed dQKV buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
               Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale) {
@@ -558,6 +601,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("transpose_run(Tensor desc, int total_tiles) -> ()");
   m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
+  m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, Tensor? seqlen=None) -> Tensor");
   m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale) -> ()");
 }
 
@@ -582,5 +626,6 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("transpose_run", transpose_run);
   m.impl("sample", sample);
   m.impl("attn_fwd", attn_fwd);
+  m.impl("attn_decode", attn_decode);
   m.impl("attn_bwd", attn_bwd);
 }

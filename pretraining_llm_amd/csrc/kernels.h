@@ -16,6 +16,17 @@ struct AttnFwdArgs {
   int causal;
 };
 
+// q [B, H, D] (one query per sequence), k/v rows of a [B, S_max, Hkv, D]-strided cache
+struct DecodeArgs {
+  const uint16_t *q, *k, *v;
+  uint16_t* o;
+  float *part_o, *part_lse;  // [B, H, splits, D] / [B, H, splits] when splits > 1
+  const int* seqlen;         // optional device key count (graph capture); else S
+  int B, H, Hkv, S, D, splits;
+  int64_t q_sb, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_sh;
+  float scale_log2;
+};
+
 struct AttnBwdArgs {
   const uint16_t *q, *k, *v, *o, *dO;
   const float* lse;
@@ -92,6 +103,10 @@ void sample_tokens(const void* logits, bool bf16_in, int64_t ld, int B, int V, f
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
+// attn_decode.hip: split-KV single-query attention over a KV cache
+bool attn_decode_supported(int D, int group);
+int attn_decode_splits(int B, int Hkv, int S_max);
+void attn_decode(const DecodeArgs& a, hipStream_t st);
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st);
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st);
 

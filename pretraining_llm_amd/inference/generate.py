@@ -54,6 +54,55 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
     return torch.nn.functional.linear(h, model.head_weight, model.head_bias).float()
 
 
+@torch.no_grad()
+def forward_decode(model, tok: torch.Tensor, cache: KVCache, pos_t: torch.Tensor, len_t: torch.Tensor) -> torch.Tensor:
+    """One decode step for tokens ``tok`` [B, 1] at the device position ``pos_t`` (int64 [1]);
+    ``len_t`` = pos_t + 1 as int32.  Every op is position-agnostic on the host (indexing by
+    device tensors, decode kernel reading the key count from ``len_t``), so the whole step
+    is hipGraph-capturable.  Returns fp32 logits [B, V]."""
+    cfg = model.config
+    x = model.token_embed.weight.index_select(0, tok.view(-1)).view(tok.shape[0], 1, -1)
+    if model.position_embed is not None:
+        x = x + model.position_embed.weight.index_select(0, pos_t).view(1, 1, -1)
+    rope = model.rope_tables(tok.device, cache.max_len) if cfg.pos == "rope" else None
+    res = None
+    for i, blk in enumerate(model.attn_blocks):
+        x, res = blk.forward_decode(x, res, cache, i, pos_t, len_t, rope)
+    h, _ = model.layer_norm(x, res)
+    return torch.nn.functional.linear(h[:, -1, :], model.head_weight, model.head_bias).float()
+
+
+class DecodeGraph:
+    """A decode step captured once as a hipGraph and replayed per token.
+
+    A GPT-2-small step is ~130 small kernels (12 x {norm, 3 GEMMs, decode attention,
+    activation, ...}); at serving batch sizes each is a few microseconds, so eager decode
+    is launch-bound.  Replaying one graph removes the per-kernel host overhead.  Inputs
+    live in static buffers (token ids, device position); outputs in a static logits buffer."""
+
+    def __init__(self, model, cache: KVCache, batch: int, device, warmup: int = 2):
+        self.model, self.cache = model, cache
+        self.tok = torch.zeros(batch, 1, dtype=torch.long, device=device)
+        self.pos_t = torch.zeros(1, dtype=torch.long, device=device)
+        self.len_t = torch.ones(1, dtype=torch.int32, device=device)
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):  # warm up (allocator pools, lazy library init) off-graph
+            for _ in range(warmup):
+                forward_decode(model, self.tok, cache, self.pos_t, self.len_t)
+        torch.cuda.current_stream(device).wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.logits = forward_decode(model, self.tok, cache, self.pos_t, self.len_t)
+
+    def __call__(self, tok: torch.Tensor, pos: int) -> torch.Tensor:
+        self.tok.copy_(tok)
+        self.pos_t.fill_(pos)
+        self.len_t.fill_(pos + 1)
+        self.graph.replay()
+        return self.logits
+
+
 def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
                 generator: Optional[torch.Generator] = None) -> torch.Tensor:
     """logits [B, V] (fp32) -> next token ids [B, 1]; temperature 0 = greedy.
@@ -78,7 +127,9 @@ def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[
 
 @torch.no_grad()
 def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0, top_k: Optional[int] = None,
-             use_cache: bool = True, generator: Optional[torch.Generator] = None) -> torch.Tensor:
+             use_cache: bool = True, generator: Optional[torch.Generator] = None,
+             cuda_graph: bool = False) -> torch.Tensor:
+    """``cuda_graph``: replay each single-token step from one captured hipGraph (GPU only)."""
     was_training = model.training
     model.eval()
     cfg = model.config
@@ -97,6 +148,10 @@ def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float =
         dtype = model.token_embed.weight.dtype
         cache = KVCache(cfg.n_blocks, B, max(max_len, 1), cfg.n_kv_head, cfg.head_dim, dtype, idx.device)
         window = idx[:, -ctx_len:] if learned else idx
+        graph = None
+        if cuda_graph and idx.is_cuda and max_new_tokens > 1:
+            # captured before the prefill: its warm-up steps write cache row 0, which the prefill overwrites
+            graph = DecodeGraph(model, cache, B, idx.device)
         logits = forward_cached(model, window, cache, 0)
         pos = window.shape[1]
         for step in range(max_new_tokens):
@@ -109,6 +164,9 @@ def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float =
                 window = idx[:, -ctx_len:]
                 logits = forward_cached(model, window, cache, 0)
                 pos = window.shape[1]
+            elif graph is not None:
+                logits = graph(nxt, pos)
+                pos += 1
             else:
                 logits = forward_cached(model, nxt, cache, pos)
                 pos += 1

@@ -84,6 +84,28 @@ class Attention(nn.Module):
             y = ops.linear(y, self.proj.weight, self.proj.bias)
         return y
 
+    def forward_decode(self, x, cache, layer_idx, pos_t, len_t, rope=None):
+        """One-token step with the position on the DEVICE (``pos_t`` int64 [1], ``len_t`` =
+        pos+1 as int32 [1]): no host scalar reaches a kernel argument, so the step can be
+        captured once in a hipGraph and replayed at every position (inference/generate.py)."""
+        B = x.shape[0]
+        H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
+        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+        q = qkv[..., : H * D].view(B, 1, H, D)
+        k = qkv[..., H * D:(H + Hkv) * D].view(B, 1, Hkv, D)
+        v = qkv[..., (H + Hkv) * D:].view(B, 1, Hkv, D)
+        if rope is not None:
+            cos, sin = rope[0].index_select(0, pos_t), rope[1].index_select(0, pos_t)
+            q = ops.apply_rope(q, cos, sin, 0)
+            k = ops.apply_rope(k, cos, sin, 0)
+        cache.k[layer_idx].index_copy_(1, pos_t, k)
+        cache.v[layer_idx].index_copy_(1, pos_t, v)
+        y = ops.attention_decode(q.contiguous(), cache.k[layer_idx], cache.v[layer_idx], seqlen=len_t)
+        y = y.reshape(B, 1, H * D)
+        if self.proj is not None:
+            y = ops.linear(y, self.proj.weight, self.proj.bias)
+        return y
+
 
 class MLP(nn.Module):
     def __init__(self, cfg: ModelConfig):
@@ -151,6 +173,12 @@ class Block(nn.Module):
     def forward_cached(self, x, residual, cache, layer_idx, pos, rope=None):
         h, res = self.ln1(x, residual)
         a = self.attn.forward_cached(h, cache, layer_idx, pos, rope)
+        h2, res2 = self.ln2(a, res)
+        return self.mlp(h2), res2
+
+    def forward_decode(self, x, residual, cache, layer_idx, pos_t, len_t, rope=None):
+        h, res = self.ln1(x, residual)
+        a = self.attn.forward_decode(h, cache, layer_idx, pos_t, len_t, rope)
         h2, res2 = self.ln2(a, res)
         return self.mlp(h2), res2
 
@@ -276,7 +304,8 @@ class GPT(nn.Module):
     # ------------------------------------------------------------------
     @torch.no_grad()
     def generate(self, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0,
-                 top_k: Optional[int] = None, use_cache: bool = True, generator=None) -> torch.Tensor:
+                 top_k: Optional[int] = None, use_cache: bool = True, generator=None,
+                 cuda_graph: bool = False) -> torch.Tensor:
         from ..inference.generate import generate
         return generate(self, idx, max_new_tokens, temperature=temperature, top_k=top_k,
-                        use_cache=use_cache, generator=generator)
+                        use_cache=use_cache, generator=generator, cuda_graph=cuda_graph)

@@ -343,11 +343,29 @@ def attention(q, k, v, causal: bool = True, scale: Optional[float] = None, retur
     of the key sequence."""
     D = q.shape[-1]
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _hip(q) and q.shape[1] == 1 and not return_lse and q.shape[2] // k.shape[2] in (1, 2, 4, 8):
+        # one query per sequence (KV-cache decode): split-KV streaming kernel (csrc/attn_decode.hip)
+        return _ops().attn_decode(q, k, v, scale)
     if _hip(q):
         o, lse = _ops().attn_fwd(q, k, v, causal, scale)
     else:
         o, lse = ref.attention(q, k, v, causal=causal, scale=scale)
     return (o, lse) if return_lse else o
+
+
+def attention_decode(q, k, v, seqlen: Optional[torch.Tensor] = None, scale: Optional[float] = None):
+    """Single-query attention q [B,1,H,D] over cached k/v [B,S,Hkv,D]; ``seqlen`` (int32 [1]
+    device tensor) optionally limits the keys to the first ``seqlen`` rows, read on the
+    device so a captured decode step (hipGraph) replays at every position."""
+    D = q.shape[-1]
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _hip(q):
+        return _ops().attn_decode(q, k, v, scale, seqlen)
+    if seqlen is not None:
+        n = int(seqlen.item())
+        k, v = k[:, :n], v[:, :n]
+    o, _ = ref.attention(q, k, v, causal=False, scale=scale)
+    return o
 
 
 def attention_block_bwd(do, q, k, v, o, lse, causal: bool = True, scale: Optional[float] = None):

@@ -38,7 +38,7 @@ def load_model(model_path: str, device: str):
 
 
 def generate_text(model_path: str, input_text: str, max_new_tokens: int = 100, device: str = 'cuda',
-                  temperature: float = 1.0, top_k=None, seed=None) -> str:
+                  temperature: float = 1.0, top_k=None, seed=None, cuda_graph: bool = True) -> str:
     if device.startswith("cuda") and not torch.cuda.is_available():
         device = "cpu"
     from pretraining_llm_amd.data.tokenizer import get_tokenizer
@@ -51,7 +51,7 @@ def generate_text(model_path: str, input_text: str, max_new_tokens: int = 100, d
         gen = torch.Generator(device=device).manual_seed(int(seed))
     with torch.no_grad():
         tokens = model.generate(context, max_new_tokens=max_new_tokens, temperature=temperature, top_k=top_k,
-                                generator=gen)[0].tolist()
+                                generator=gen, cuda_graph=cuda_graph and device.startswith("cuda"))[0].tolist()
     return enc.decode(tokens)
 
 
@@ -64,9 +64,10 @@ def main() -> None:
     parser.add_argument('--temperature', type=float, default=1.0)
     parser.add_argument('--top_k', type=int, default=None)
     parser.add_argument('--seed', type=int, default=None)
+    parser.add_argument('--no_cuda_graph', action='store_true', help='eager decode steps instead of one hipGraph replay')
     args = parser.parse_args()
     generated = generate_text(args.model_path, args.input_text, args.max_new_tokens, args.device,
-                              args.temperature, args.top_k, args.seed)
+                              args.temperature, args.top_k, args.seed, cuda_graph=not args.no_cuda_graph)
     print(f"Generated text:\n{generated}")
 
 

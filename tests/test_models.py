@@ -132,6 +132,25 @@ def test_kv_cache_generation_matches_recompute(preset):
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny"])
+def test_device_position_decode_step_matches_cached(preset):
+    """forward_decode (position as a device tensor -- the hipGraph-capturable step) gives the
+    same logits as the host-position KV-cache step."""
+    from pretraining_llm_amd.inference.generate import KVCache, forward_cached, forward_decode
+    torch.manual_seed(6)
+    cfg = get_preset(preset).replace(vocab_size=256, context_length=32)
+    m = GPT(cfg).eval()
+    idx = torch.randint(0, 256, (2, 7))
+    mk = lambda: KVCache(cfg.n_blocks, 2, 32, cfg.n_kv_head, cfg.head_dim, torch.float32, "cpu")  # noqa: E731
+    c1, c2 = mk(), mk()
+    forward_cached(m, idx[:, :6], c1, 0)
+    forward_cached(m, idx[:, :6], c2, 0)
+    a = forward_cached(m, idx[:, 6:], c1, 6)
+    b = forward_decode(m, idx[:, 6:], c2, torch.tensor([6]), torch.tensor([7], dtype=torch.int32))
+    assert torch.allclose(a, b, atol=1e-5, rtol=1e-4)
+    assert torch.equal(c1.k[1][:, :7], c2.k[1][:, :7])
+
+
 def test_generation_context_crop_beyond_context_length():
     torch.manual_seed(4)
     cfg = _tiny().replace(context_length=16)
