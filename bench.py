@@ -43,6 +43,8 @@ def parse(argv=None):
     ap.add_argument("--act-ckpt", type=int, default=None, help="force activation checkpointing on (1) / off (0)")
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
+                    help="1 = ZeRO-1: reduce-scatter grads, shard fp32 master/moments, all-gather bf16 weights")
     ap.add_argument("--grad-clip", type=float, default=1.0)
     ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
     ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
@@ -84,9 +86,15 @@ def main(argv=None):
     if args.act_ckpt is not None:
         mcfg = mcfg.replace(activation_checkpointing=bool(args.act_ckpt))
     model = GPT(mcfg).to(device=dev, dtype=torch.bfloat16)
-    opt = FlatAdamW(model, lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
-                    max_grad_norm=args.grad_clip)
-    engine = DataParallelEngine(opt, bucket_mb=args.bucket_mb)
+    okw = dict(lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
+               max_grad_norm=args.grad_clip)
+    if args.zero:
+        from pretraining_llm_amd.parallel.zero import ShardedFlatAdamW, ZeroDataParallelEngine
+        opt = ShardedFlatAdamW(model, bucket_mb=args.bucket_mb, **okw)
+        engine = ZeroDataParallelEngine(opt)
+    else:
+        opt = FlatAdamW(model, **okw)
+        engine = DataParallelEngine(opt, bucket_mb=args.bucket_mb)
 
     B, T = args.batch, args.seq
     n_tok = max(4_000_000, 4 * B * (T + 1))
@@ -152,7 +160,7 @@ def main(argv=None):
             "dtype": "bf16",
             "data": "synthetic (native token loader over a generated uint16 shard), random-init weights",
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
-                       "parallelism": f"dp{world}", "micro_batch_per_gpu": B, "backend": args.backend,
+                       "parallelism": f"dp{world}" + ("-zero1" if args.zero else ""), "micro_batch_per_gpu": B, "backend": args.backend,
                        "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph)},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),
             "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),

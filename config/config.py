@@ -83,6 +83,10 @@ default_config = {
     'bucket_mb': 64.0,                # DP all-reduce bucket size (xGMI-sized, see parallel/dp.py)
     'first_bucket_mb': 4.0,
     'activation_checkpointing': None,
+    'zero_stage': 0,                  # 1 = shard fp32 master + AdamW moments over DP ranks (parallel/zero.py)
+    'profile_dir': None,              # torch.profiler (ROCm activity) chrome traces + kernel table per rank
+    'profile_steps': '3:6',           # [start:end) optimizer steps to profile
+    'deterministic': False,           # torch.use_deterministic_algorithms + fixed-order kernels only
 }
 
 # Named BASELINE.json configurations (override default_config)

@@ -5,3 +5,5 @@ from .tensor import (ColumnParallelLinear, RowParallelLinear, TensorParallelAtte
                      reduce_scatter_to_sequence, scatter_to_sequence, seq_to_head_all_to_all,
                      ulysses_attention)
 from .context import ring_attention, zigzag_positions, zigzag_shard, zigzag_unshard  # noqa: F401
+# ZeRO-1 (parallel/zero.py: ShardedFlatAdamW, ZeroDataParallelEngine) is imported from its module
+# directly: it builds on train.optim, which the trainer (train/) imports from here.

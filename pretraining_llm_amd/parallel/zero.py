@@ -1,0 +1,286 @@
+"""ZeRO-1: optimizer-state sharding on top of the flat parameter/gradient buffers.
+
+Reference: ``torch.optim.AdamW`` state fully replicated on every DDP rank
+(scripts/train_transformer.py:122-126; SURVEY.md §2.5 "FSDP / ZeRO: No").
+
+With 288 GB of HBM per MI355X, replicated fp32 master weights + moments (12 B/param) fit
+comfortably up to several billion parameters, so this is an option, not the default:
+it pays off when the optimizer state would crowd out activations (multi-B models at long
+sequence lengths) and it cuts the per-rank AdamW pass to 1/world.
+
+Layout (MI355X-first, built for RCCL over point-to-point xGMI):
+* the flat gradient buffer is cut into fixed-size buckets from its END (backward produces
+  the last layers' gradients first) -- a small first bucket, then ``bucket_mb`` ones --
+  every bucket a multiple of ``world * 64`` elements, so each splits into ``world`` equal,
+  64-element-aligned parts and rank r owns part r of EVERY bucket.  Every rank therefore
+  owns 1/world of every bucket (balanced ring traffic on every xGMI link) and the
+  ownership is independent of parameter boundaries;
+* backward: a bucket is reduce-scattered (RCCL, async, strictly in bucket order) as soon
+  as all parameters overlapping it have their gradients -- the same readiness machinery
+  as the all-reduce engine (``p._pllm_grad_ready`` from in-place kernels, post-accumulate
+  hooks otherwise).  A reduce-scatter moves half the bytes of an all-reduce;
+* step: per bucket, the fused AdamW kernel updates the owned part (fp32 master/moments
+  exist only for owned parts: 12 B/param / world) and writes the bf16 weights, then an
+  async all-gather of that bucket's bf16 weights is issued, so bucket b's all-gather
+  runs under bucket b+1's AdamW; the compute stream waits on all of them (no host sync);
+* gradient clipping: sum of squares of the owned reduced gradients, one scalar
+  all-reduce, device-side clip coefficient;
+* ``state_dict``/``load_state_dict`` are COLLECTIVE: they gather/scatter the shards so the
+  checkpoint keeps FlatAdamW's (torch.optim.AdamW-shaped) single-file format.
+"""
+from __future__ import annotations
+
+import contextlib
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import ops as _ops_mod
+from ..ops import _lib
+from ..train.optim import ALIGN, FlatAdamW, _round_up
+
+
+def _world_rank(group):
+    if dist.is_initialized():
+        return dist.get_world_size(group), dist.get_rank(group)
+    return 1, 0
+
+
+class ShardedFlatAdamW(FlatAdamW):
+    """FlatAdamW whose fp32 master weights and moments are sharded over a process group."""
+
+    collective_state = True  # state_dict / load_state_dict must be called on every rank
+
+    def __init__(self, model, lr: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.01,
+                 decay_filter=None, max_grad_norm: float = 0.0, process_group=None, bucket_mb: float = 64.0,
+                 first_bucket_mb: float = 4.0, transposed_shadow: Optional[bool] = None):
+        self.pg = process_group
+        self.world, self.rank = _world_rank(process_group)
+        unit = self.world * ALIGN
+        super().__init__(model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decay_filter=decay_filter,
+                         max_grad_norm=max_grad_norm, transposed_shadow=transposed_shadow, pad_multiple=unit)
+        esz = self.flat_grad.element_size()
+        # buckets from the end of the buffer, each a multiple of world*ALIGN elements
+        buckets = []
+        end = self.total
+        cap = max(unit, _round_up(int(first_bucket_mb * 2 ** 20) // esz, unit))
+        while end > 0:
+            start = max(0, end - cap)
+            buckets.append((start, end))
+            end = start
+            cap = max(unit, _round_up(int(bucket_mb * 2 ** 20) // esz, unit))
+        self.buckets = buckets                       # launch order (last layers first)
+        self.own = []                                # (flat_start, flat_end, shard_offset) per bucket
+        so = 0
+        for bs, be in buckets:
+            part = (be - bs) // self.world
+            self.own.append((bs + self.rank * part, bs + (self.rank + 1) * part, so))
+            so += part
+        self.shard_numel = so
+        # replace the replicated fp32 state by the owned slices
+        full_master = self.master
+        self.master = torch.empty(so, dtype=torch.float32, device=full_master.device)
+        for fs, fe, o in self.own:
+            self.master[o:o + fe - fs].copy_(full_master[fs:fe])
+        del full_master
+        self.exp_avg = torch.zeros(so, dtype=torch.float32, device=self.master.device)
+        self.exp_avg_sq = torch.zeros(so, dtype=torch.float32, device=self.master.device)
+        # reduced (summed) owned gradient parts land here
+        self.grad_shard = torch.zeros(so, dtype=self.grad_dtype, device=self.master.device)
+        self._inplace_ag = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
+
+    # ------------------------------------------------------------------
+    def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
+        if self.use_hip and _ops_mod.get_backend() == "auto":
+            ss = _lib.require().sumsq(self.grad_shard)
+        else:
+            ss = self.grad_shard.float().pow(2).sum()
+        ss = ss.reshape(1).float()
+        if self.world > 1:
+            dist.all_reduce(ss, op=dist.ReduceOp.SUM, group=self.pg)
+        return ss[0].sqrt() * grad_scale
+
+    def _update_part(self, fs, fe, o, grad_scale, clip):
+        n = fe - fs
+        b1, b2 = self.betas
+        p, mst = self.flat_param[fs:fe], self.master[o:o + n]
+        m, v, g = self.exp_avg[o:o + n], self.exp_avg_sq[o:o + n], self.grad_shard[o:o + n]
+        if self.use_hip and _ops_mod.get_backend() == "auto":
+            wm = None if self.wd_mask is None else self.wd_mask[fs // ALIGN:fe // ALIGN]
+            _lib.require().adamw_(p, mst, m, v, g, self.lr, b1, b2, self.eps, self.weight_decay, self.step_count,
+                                  grad_scale, clip, wm, None)
+            return
+        g32 = g.float() * grad_scale
+        if clip is not None:
+            g32 = g32 * clip
+        wd = self.weight_decay
+        if not self.all_decay:
+            mst.mul_(torch.where(self.wd_elem_mask[fs:fe], 1.0 - self.lr * wd, 1.0))
+            wd = 0.0
+        _ops_mod.ref.adamw_(p, g32, m, v, self.lr, b1, b2, self.eps, wd, self.step_count, master=mst)
+
+    def step(self, grad_scale: float = 1.0, graph: bool = False):
+        if graph:
+            raise RuntimeError("ShardedFlatAdamW: graph-captured steps are not supported (collectives in the step)")
+        self._sync_lr()
+        self.step_count += 1
+        clip = None
+        if self.max_grad_norm and self.max_grad_norm > 0:
+            norm = self.grad_norm(grad_scale)
+            self.last_grad_norm = norm
+            clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).to(torch.float32).reshape(1)
+        handles = []
+        for (bs, be), (fs, fe, o) in zip(self.buckets, self.own):
+            self._update_part(fs, fe, o, grad_scale, clip)
+            if self.world > 1:
+                src = self.flat_param[fs:fe] if self._inplace_ag else self.flat_param[fs:fe].clone()
+                handles.append(dist.all_gather_into_tensor(self.flat_param[bs:be], src, group=self.pg,
+                                                           async_op=True))
+        for h in handles:
+            h.wait()
+        self.refresh_shadows()
+
+    # ------------------------------------------------------------------
+    def _gather_full(self, shard: torch.Tensor) -> torch.Tensor:
+        full = torch.zeros(self.total, dtype=shard.dtype, device=shard.device)
+        for (bs, be), (fs, fe, o) in zip(self.buckets, self.own):
+            n = fe - fs
+            if self.world > 1:
+                dist.all_gather_into_tensor(full[bs:be], shard[o:o + n].contiguous(), group=self.pg)
+            else:
+                full[bs:be].copy_(shard[o:o + n])
+        return full
+
+    @contextlib.contextmanager
+    def _full_state(self):
+        saved = (self.master, self.exp_avg, self.exp_avg_sq)
+        self.master, self.exp_avg, self.exp_avg_sq = (self._gather_full(t) for t in saved)
+        try:
+            yield
+        finally:
+            full = (self.master, self.exp_avg, self.exp_avg_sq)
+            self.master, self.exp_avg, self.exp_avg_sq = saved
+            for dst, src in zip(saved, full):
+                for fs, fe, o in self.own:
+                    dst[o:o + fe - fs].copy_(src[fs:fe])
+
+    def state_dict(self) -> dict:
+        """COLLECTIVE: every rank must call it; returns the full (unsharded) state on every rank."""
+        with self._full_state():
+            return super().state_dict()
+
+    @torch.no_grad()
+    def load_state_dict(self, sd: dict):
+        """COLLECTIVE: every rank loads the same full state and keeps its own shard."""
+        with self._full_state():
+            super().load_state_dict(sd)
+
+    @torch.no_grad()
+    def sync_master_from_params(self):
+        for fs, fe, o in self.own:
+            self.master[o:o + fe - fs].copy_(self.flat_param[fs:fe].float())
+        self.refresh_shadows()
+
+
+class ZeroDataParallelEngine:
+    """Gradient reduce-scatter engine for ``ShardedFlatAdamW`` (same surface as
+    ``DataParallelEngine``: ``no_sync()``, ``finish_grad_sync() -> grad scale``)."""
+
+    def __init__(self, optimizer: ShardedFlatAdamW, broadcast_params: bool = True, overlap: bool = True):
+        self.opt = optimizer
+        self.pg = optimizer.pg
+        self.world = optimizer.world
+        self.enabled = True
+        self._handles = []
+        self._hooks = []
+        opt = optimizer
+        params = opt.params
+        # parameters overlapping each bucket
+        self.bucket_params: List[List[int]] = []
+        self.param_buckets: List[List[int]] = [[] for _ in params]
+        for b, (bs, be) in enumerate(opt.buckets):
+            ids = [i for i, p in enumerate(params) if opt.offsets[i] < be and opt.offsets[i] + p.numel() > bs]
+            self.bucket_params.append(ids)
+            for i in ids:
+                self.param_buckets[i].append(b)
+        self._expected: Optional[List[int]] = None
+        self._events = [0] * len(params)
+        self._reset_counters()
+        if broadcast_params and self.world > 1:
+            src = dist.get_global_rank(self.pg, 0) if self.pg is not None else 0
+            dist.broadcast(opt.flat_param, src=src, group=self.pg)
+            opt.sync_master_from_params()
+        if self.world > 1 and overlap:
+            for i, p in enumerate(params):
+                h = self._make_hook(i)
+                self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, h=h: h()))
+                p._pllm_grad_ready = h
+
+    def _reset_counters(self):
+        if self._expected is None:
+            self._pending = [len(ids) for ids in self.bucket_params]
+        else:
+            self._pending = [sum(1 for i in ids if self._expected[i] > 0) for ids in self.bucket_params]
+        self._events = [0] * len(self._events)
+        self._next_launch = 0
+        self._handles = []
+
+    def _make_hook(self, i):
+        def hook():
+            if not self.enabled:
+                return
+            self._events[i] += 1
+            if self._expected is None or self._events[i] != self._expected[i]:
+                return
+            for b in self.param_buckets[i]:
+                self._pending[b] -= 1
+            self._launch_ready()
+        return hook
+
+    def _launch(self, b):
+        opt = self.opt
+        bs, be = opt.buckets[b]
+        fs, fe, o = opt.own[b]
+        out = opt.grad_shard[o:o + fe - fs]
+        self._handles.append(dist.reduce_scatter_tensor(out, opt.flat_grad[bs:be], op=dist.ReduceOp.SUM,
+                                                        group=self.pg, async_op=True))
+
+    def _launch_ready(self):
+        while self._next_launch < len(self.opt.buckets) and self._pending[self._next_launch] <= 0:
+            self._launch(self._next_launch)
+            self._next_launch += 1
+
+    @contextlib.contextmanager
+    def no_sync(self):
+        old = self.enabled
+        self.enabled = False
+        try:
+            yield
+        finally:
+            self.enabled = old
+
+    def finish_grad_sync(self):
+        opt = self.opt
+        if self.world > 1:
+            while self._next_launch < len(opt.buckets):
+                self._launch(self._next_launch)
+                self._next_launch += 1
+            for h in self._handles:
+                h.wait()
+            if self._expected is None and self.enabled and any(self._events):
+                self._expected = list(self._events)
+        else:
+            for fs, fe, o in opt.own:
+                opt.grad_shard[o:o + fe - fs].copy_(opt.flat_grad[fs:fe])
+        self._reset_counters()
+        return 1.0 / self.world
+
+    def bucket_sizes_mb(self):
+        esz = self.opt.flat_grad.element_size()
+        return [(be - bs) * esz / 2 ** 20 for bs, be in self.opt.buckets]
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []

@@ -43,7 +43,7 @@ def _round_up(n: int, a: int) -> int:
 class FlatAdamW:
     def __init__(self, model: nn.Module, lr: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, decay_filter=None, grad_dtype: Optional[torch.dtype] = None,
-                 max_grad_norm: float = 0.0, transposed_shadow: Optional[bool] = None):
+                 max_grad_norm: float = 0.0, transposed_shadow: Optional[bool] = None, pad_multiple: int = ALIGN):
         self.model = model
         self.lr = lr
         self.betas = betas
@@ -74,7 +74,7 @@ class FlatAdamW:
         for i, p in enumerate(params):
             self.offsets[i] = off
             off += _round_up(p.numel(), ALIGN)
-        total = off
+        total = _round_up(off, pad_multiple)  # ZeRO pads to world * ALIGN (parallel/zero.py)
         self.decay = decay
         self.total = total
         dev = params[0].device

@@ -75,6 +75,10 @@ class Trainer:
         self.device = self.di.device
         seed = int(self.cfg.get("seed", 1337))
         torch.manual_seed(seed)  # identical init on every rank (then broadcast for certainty)
+        if self.cfg.get("deterministic", False):
+            # every hand-written kernel already reduces in a fixed order (attention dQ slabs,
+            # split-K wgrad slabs, sorted embedding backward); this pins torch's own ops too
+            torch.use_deterministic_algorithms(True, warn_only=True)
         self.mcfg = model_config_from(self.cfg)
         self.seq_len = int(self.cfg.get("seq_len") or self.mcfg.context_length)
         dtype_name = self.cfg.get("dtype", "bfloat16")
@@ -84,11 +88,18 @@ class Trainer:
             self.dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}[dtype_name]
         self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
         decay_filter = None if self.cfg.get("weight_decay_all", True) else no_decay_1d
-        self.opt = FlatAdamW(self.model, lr=self.cfg["t_lr"], betas=tuple(self.cfg.get("betas", (0.9, 0.999))),
-                             eps=self.cfg.get("eps", 1e-8), weight_decay=self.cfg.get("weight_decay", 0.01),
-                             decay_filter=decay_filter, max_grad_norm=self.cfg.get("max_grad_norm", 0.0))
-        self.engine = DataParallelEngine(self.opt, bucket_mb=self.cfg.get("bucket_mb", 64.0),
-                                         first_bucket_mb=self.cfg.get("first_bucket_mb", 4.0))
+        okw = dict(lr=self.cfg["t_lr"], betas=tuple(self.cfg.get("betas", (0.9, 0.999))),
+                   eps=self.cfg.get("eps", 1e-8), weight_decay=self.cfg.get("weight_decay", 0.01),
+                   decay_filter=decay_filter, max_grad_norm=self.cfg.get("max_grad_norm", 0.0))
+        bkw = dict(bucket_mb=self.cfg.get("bucket_mb", 64.0), first_bucket_mb=self.cfg.get("first_bucket_mb", 4.0))
+        if int(self.cfg.get("zero_stage", 0)) >= 1:
+            # ZeRO-1: fp32 master + moments sharded over the DP ranks (parallel/zero.py)
+            from ..parallel.zero import ShardedFlatAdamW, ZeroDataParallelEngine
+            self.opt = ShardedFlatAdamW(self.model, **okw, **bkw)
+            self.engine = ZeroDataParallelEngine(self.opt)
+        else:
+            self.opt = FlatAdamW(self.model, **okw)
+            self.engine = DataParallelEngine(self.opt, **bkw)
         self.accum = int(self.cfg.get("grad_accum_steps", 1))
         self.step = 0
         self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
@@ -164,8 +175,11 @@ class Trainer:
         t0 = time.perf_counter()
         window_steps = 0
         last_val = float("nan")
+        prof = self._profiler()
         while self.step < total:
             step = self.step
+            if prof is not None:
+                prof.step()
             do_eval = self.val_loader is not None and eval_every > 0 and step % eval_every == 0 and (
                 step > 0 or cfg.get("eval_at_start", True))
             if do_eval:
@@ -199,10 +213,42 @@ class Trainer:
                 t0 = time.perf_counter()
             if ckpt_every and self.step % ckpt_every == 0 and self.step < total:
                 self.save(self._ckpt_path(periodic=True))
+        if prof is not None:
+            self._finish_profile(prof)
         out = cfg.get("t_out_path")
         if out:
             self.save(out)
         return self
+
+    # ------------------------------------------------------------------
+    def _profiler(self):
+        """torch.profiler over optimizer steps [start, end) of ``profile_steps`` with ROCm
+        (HIP) activity: per-rank chrome trace + a kernel-time table.
+        Kernel-level counters come from ``rocprofv3`` (scripts/gpu/prof.sh, profiles/)."""
+        d = self.cfg.get("profile_dir")
+        if not d:
+            return None
+        a, b = (int(x) for x in str(self.cfg.get("profile_steps", "3:6")).split(":"))
+        acts = [torch.profiler.ProfilerActivity.CPU]
+        if self.device.type == "cuda":
+            acts.append(torch.profiler.ProfilerActivity.CUDA)
+        os.makedirs(d, exist_ok=True)
+        prof = torch.profiler.profile(activities=acts, schedule=torch.profiler.schedule(
+            wait=max(0, a - 1), warmup=1 if a > 0 else 0, active=max(1, b - a), repeat=1), record_shapes=False)
+        prof.start()
+        return prof
+
+    def _finish_profile(self, prof):
+        prof.stop()
+        d = self.cfg["profile_dir"]
+        path = os.path.join(d, f"trace_rank{self.di.rank}.json")
+        prof.export_chrome_trace(path)
+        key = "self_cuda_time_total" if self.device.type == "cuda" else "self_cpu_time_total"
+        table = prof.key_averages().table(sort_by=key, row_limit=25)
+        with open(os.path.join(d, f"kernels_rank{self.di.rank}.txt"), "w") as f:
+            f.write(table)
+        if self.di.is_master:
+            self.log(f"profile written to {path}")
 
     # ------------------------------------------------------------------
     def _ckpt_path(self, periodic=False):
@@ -215,8 +261,11 @@ class Trainer:
     def save(self, path: str):
         data_state = {"train_batches": self.train_loader.batches_consumed,
                       "val_batches": self.val_loader.batches_consumed if self.val_loader else 0}
+        # a sharded optimizer consolidates its state collectively (every rank), rank 0 writes it
+        osd = self.opt.state_dict() if getattr(self.opt, "collective_state", False) else None
         if self.di.is_master:
-            save_checkpoint(path, self.model, self.opt, step=self.step, config=self.cfg, data_state=data_state)
+            save_checkpoint(path, self.model, self.opt if osd is None else None, step=self.step, config=self.cfg,
+                            data_state=data_state, optimizer_state=osd)
             self.log(f"saved checkpoint to {path} (step {self.step})")
         if dist.is_initialized():
             dist.barrier()

@@ -36,13 +36,15 @@ def rng_state() -> dict:
 
 
 def save_checkpoint(path: str, model, optimizer=None, step: Optional[int] = None, config: Optional[dict] = None,
-                    data_state: Optional[dict] = None, extra: Optional[dict] = None) -> str:
+                    data_state: Optional[dict] = None, extra: Optional[dict] = None,
+                    optimizer_state: Optional[dict] = None) -> str:
     m = unwrap(model)
     sd = {k: v.detach().cpu() if torch.is_tensor(v) else v for k, v in m.state_dict().items()}
     ckpt = {"model_state_dict": strip_wrapper_prefixes(sd)}
     if optimizer is not None:
-        osd = optimizer.state_dict()
-        ckpt["optimizer_state_dict"] = _to_cpu(osd)
+        optimizer_state = optimizer.state_dict()
+    if optimizer_state is not None:
+        ckpt["optimizer_state_dict"] = _to_cpu(optimizer_state)
     if step is not None:
         ckpt["step"] = int(step)
     if config is not None:

@@ -1,0 +1,13 @@
+#!/bin/bash
+# full GPU suite (incl. ZeRO-1 + decode tests) + smoke + headline bench + ZeRO-1 bench
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/t15.log 2>&1
+rc=$?; tail -3 gpurun_out/t15.log
+if [ $rc -ne 0 ]; then grep -E "^E |FAILED|Error" gpurun_out/t15.log | head -30; exit $rc; fi
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/s15.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/s15.log; exit 5; }
+timeout -k 10 300 python bench.py > gpurun_out/b15.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/b15.log; exit 4; }
+tail -1 gpurun_out/b15.log | cut -c1-250
+timeout -k 10 300 python bench.py --zero 1 > gpurun_out/b15z.log 2>&1 || { echo "zero bench failed"; tail -20 gpurun_out/b15z.log; exit 4; }
+tail -1 gpurun_out/b15z.log | cut -c1-250

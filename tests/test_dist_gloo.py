@@ -130,3 +130,19 @@ def test_dp_no_sync_accumulation():
     acc = _run("accum")["accum.pt"]["grad"]
     ref = _single_process_grad()
     assert torch.allclose(acc, ref, atol=2e-6, rtol=1e-4), (acc - ref).abs().max()
+
+
+def test_comm_bench_sweep_gloo():
+    """bench/comm_bench.py (RCCL bus-bandwidth sweep) runs end-to-end under torchrun (gloo, 2 ranks)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "bench", "comm_bench.py"),
+                        "--backend", "gloo", "--device", "cpu", "--sizes-mb", "0.1", "--iters", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=240, cwd="/tmp")
+    assert r.returncode == 0, r.stderr[-2000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert {x["op"] for x in recs} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
+    assert all(x["busbw_GBps"] > 0 and x["world"] == 2 for x in recs)

@@ -53,6 +53,51 @@ def test_resume_is_exact(tmp_path):
         assert torch.allclose(v.float(), final_a[k].float(), atol=1e-6), k
 
 
+def test_profiler_writes_trace(tmp_path):
+    from pretraining_llm_amd.train import Trainer
+    d = tmp_path / "prof"
+    Trainer(_cfg(tmp_path, t_train_steps=6, profile_dir=str(d), profile_steps="2:4", t_out_path=None),
+            log=lambda *_: None).train()
+    assert (d / "trace_rank0.json").stat().st_size > 0
+    assert "Self CPU" in (d / "kernels_rank0.txt").read_text()
+
+
+def _zero_worker(rank, world, port, tmp):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    import pathlib
+    from pretraining_llm_amd.train import Trainer
+    from pretraining_llm_amd.utils.dist import init_distributed
+    tmp = pathlib.Path(tmp)
+    di = init_distributed("gloo", "cpu")
+    kw = dict(zero_stage=1, t_train_steps=8, ckpt_interval=4, max_grad_norm=1.0, bucket_mb=0.1, first_bucket_mb=0.02)
+    a = Trainer(_cfg(tmp, **kw), dist_info=di, log=lambda *_: None)
+    a.train()
+    final_a = {k: v.clone() for k, v in a.model.state_dict().items()}
+    b = Trainer(_cfg(tmp, resume=str(tmp / "models" / "tiny.latest.pt"), t_out_path=str(tmp / "b.pt"), **kw),
+                dist_info=di, log=lambda *_: None)
+    assert b.step == 4
+    b.train()
+    err = max((v.float() - final_a[k].float()).abs().max().item() for k, v in b.model.state_dict().items())
+    torch.save({"err": err}, str(tmp / f"zero_r{rank}.pt"))
+    import torch.distributed as dist
+    dist.destroy_process_group()
+
+
+def test_zero1_trainer_checkpoint_resume_gloo(tmp_path):
+    """ZeRO-1 trainer on 2 gloo ranks: collective checkpoint consolidation + exact resume."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mp.spawn(_zero_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert torch.load(tmp_path / f"zero_r{r}.pt", weights_only=True)["err"] < 1e-6
+
+
 def test_generate_text_cli_loads_trainer_checkpoint(tmp_path):
     from pretraining_llm_amd.train import Trainer
     Trainer(_cfg(tmp_path, t_train_steps=2), log=lambda *_: None).train()
