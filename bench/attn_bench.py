@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--configs", default="64x12x1024x64,8x16x2048x128,8x16x4096x64")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="", help="fwd|bwd: run only our kernel (for profiling)")
+    ap.add_argument("--variants", default="", help="comma list of backward tiling variants to A/B (attn_bwd_set_variant)")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
@@ -50,6 +51,21 @@ def main():
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         ours_f = lambda: torch.ops.pllm.attn_fwd(q, k, v, True, scale)
         ours_b = lambda: torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, True, scale)
+        if args.variants:
+            outs, res = {}, {"cfg": cfg}
+            for vv in (int(x) for x in args.variants.split(",")):
+                torch.ops.pllm.attn_bwd_set_variant(vv)
+                ts = [1e6 * timeit(ours_b) for _ in range(args.rounds)]
+                outs[vv] = [t.float().clone() for t in (dq, dk, dv)]
+                res[f"bwd_v{vv}_us"] = ts
+                res[f"bwd_v{vv}_tflops"] = 2.5 * 2 * 2 * B * H * T * T * D / 2 / (min(ts) * 1e-6) / 1e12
+            v0 = min(outs)
+            for vv, o_ in outs.items():
+                res[f"v{vv}_max_rel_diff_vs_v{v0}"] = max(((a - b).norm() / b.norm()).item()
+                                                          for a, b in zip(o_, outs[v0]))
+            torch.ops.pllm.attn_bwd_set_variant(0)
+            print(json.dumps(res), flush=True)
+            continue
         if args.only:
             fn = ours_f if args.only == "fwd" else ours_b
             for _ in range(5):

@@ -342,12 +342,14 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //   D <= 64 : 8 waves, 256 keys, 128 queries per iteration -> every dQ task (32 q x 32 d)
 //             sums all 256 keys on chip; half the dQ slabs of a 128-key block.
 //   D = 128 : 4 waves, 128 keys, 32 queries (register budget: dK^T/dV^T alone are 128 regs).
-template <int D>
+//   V = 1 (D <= 64): 4 waves, 128 keys, 64 queries: 48 KiB of LDS, so TWO workgroups share a
+//             CU and one's barrier waits overlap the other's MFMA work (more dQ slabs).
+template <int D, int V = 0>
 struct BwdCfg {
-  static constexpr int NW = D <= 64 ? 8 : 4;
+  static constexpr int NW = (D <= 64 && V == 0) ? 8 : 4;
   static constexpr int NT = 64 * NW;
   static constexpr int BK = 32 * NW;
-  static constexpr int BQ = D <= 64 ? 128 : 32;
+  static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : 32;
   static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
   static constexpr int QLPT = (BQ * CPR + NT - 1) / NT;
@@ -357,9 +359,9 @@ struct BwdCfg {
 
 // D=128 keeps dK^T/dV^T (128 regs) + K/V fragments (64) + S/dP in registers: one wave per
 // SIMD with the full register file instead of spilling at the 2-waves/SIMD budget.
-template <int D>
-__global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
-  using C = BwdCfg<D>;
+template <int D, int V>
+__global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
+  using C = BwdCfg<D, V>;
   using I = Img<D>;
   using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
   constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
@@ -578,10 +580,10 @@ __global__ __launch_bounds__(BwdCfg<D>::NT, D == 128 ? 1 : 2) void attn_bwd_kern
 // dq (bf16, strided) = scale * sum over contributing key blocks of the fp32 slabs
 // [nkb][B,T,H,D]; under the causal mask row t only reads blocks kb <= (t+off)/BK
 // (the others were never written for it).
-template <int D>
+template <int D, int V>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   constexpr int CPR = D / 8;
-  constexpr int BK = BwdCfg<D>::BK;
+  constexpr int BK = BwdCfg<D, V>::BK;
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t row = gid / CPR;
   const int c = (int)(gid % CPR);
@@ -617,7 +619,15 @@ namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-int attn_bwd_key_block(int D) { return D <= 64 ? BwdCfg<64>::BK : BwdCfg<128>::BK; }
+// backward tiling variant for D <= 64 (BwdCfg): 0 = 8-wave 256-key workgroups, 1 = 4-wave
+// 128-key workgroups two per CU
+static int g_bwd_variant = 0;
+void attn_bwd_set_variant(int v) { g_bwd_variant = v == 1 ? 1 : 0; }
+
+int attn_bwd_key_block(int D) {
+  if (D <= 64) return g_bwd_variant == 1 ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
+  return BwdCfg<128>::BK;
+}
 
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
@@ -625,14 +635,14 @@ static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(attn_fwd_kernel<D>, dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
 }
 
-template <int D>
+template <int D, int V>
 static void attn_bwd_t(const AttnBwdArgs& a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
-  const int nkb = (a.S + BwdCfg<D>::BK - 1) / BwdCfg<D>::BK;
+  const int nkb = (a.S + BwdCfg<D, V>::BK - 1) / BwdCfg<D, V>::BK;
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
-  hipLaunchKernelGGL(attn_bwd_kernel<D>, dim3(nkb * a.B * a.Hkv), dim3(BwdCfg<D>::NT), 0, st, a);
-  hipLaunchKernelGGL(attn_dq_reduce_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((attn_bwd_kernel<D, V>), dim3(nkb * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st, a);
+  hipLaunchKernelGGL((attn_dq_reduce_kernel<D, V>), dim3(pre_grid), dim3(256), 0, st, a);
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
@@ -642,9 +652,9 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
-  if (a.D == 32) attn_bwd_t<32>(a, st);
-  else if (a.D == 64) attn_bwd_t<64>(a, st);
-  else attn_bwd_t<128>(a, st);
+  if (a.D == 32) g_bwd_variant == 1 ? attn_bwd_t<32, 1>(a, st) : attn_bwd_t<32, 0>(a, st);
+  else if (a.D == 64) g_bwd_variant == 1 ? attn_bwd_t<64, 1>(a, st) : attn_bwd_t<64, 0>(a, st);
+  else attn_bwd_t<128, 0>(a, st);
 }
 
 }  // namespace pllm

@@ -168,6 +168,60 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   return out;
 }
 
+// ---------------------------------------------------------------- NT GEMM + MLP epilogues
+// epi 0: [a b^T (+bias)];  epi 1: [gelu(h), h] with h = a b^T + bias;
+// epi 2: [(a b^T) * gelu'(aux)], adding its column sums into ``bias_grad_acc`` (bf16, in place)
+std::vector<Tensor> gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
+                            const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_grad_acc) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_nt: a [M,K], b [N,K]");
+  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
+              "gemm_nt: K-contiguous operands, row strides % 8");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "gemm_nt: K % 64 == 0 and N % 8 == 0");
+  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm_nt: epi 0..2");
+  check_aligned16(a, "a");
+  check_aligned16(b, "b");
+  GemmNTArgs g{};
+  g.A = (const uint16_t*)a.data_ptr();
+  g.B = (const uint16_t*)b.data_ptr();
+  g.M = (int)M; g.N = (int)N; g.K = (int)K;
+  g.lda = a.stride(0); g.ldb = b.stride(0); g.ldc = N;
+  Tensor c = at::empty({M, N}, a.options());
+  g.C = (uint16_t*)c.data_ptr();
+  std::vector<Tensor> outs{c};
+  if (bias && epi != 2) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm_nt: bias [N]");
+    TORCH_CHECK(((uintptr_t)bias->data_ptr() & 7) == 0, "gemm_nt: bias must be 8-byte aligned");
+    g.bias = (const uint16_t*)bias->data_ptr();
+  }
+  Tensor part;
+  if (epi == 1) {
+    Tensor h = at::empty({M, N}, a.options());
+    g.aux = (uint16_t*)h.data_ptr();
+    outs.push_back(h);
+  } else if (epi == 2) {
+    TORCH_CHECK(aux.has_value(), "gemm_nt epi 2 needs aux (pre-activation)");
+    check_bf16(*aux, "aux");
+    TORCH_CHECK(aux->numel() == M * N && aux->is_contiguous(), "gemm_nt: aux [M,N] contiguous");
+    g.aux = (uint16_t*)aux->data_ptr();
+    TORCH_CHECK(bias_grad_acc.has_value(), "gemm_nt epi 2 needs bias_grad_acc");
+    check_bf16(*bias_grad_acc, "bias_grad_acc");
+    TORCH_CHECK(bias_grad_acc->numel() == N && bias_grad_acc->is_contiguous(), "gemm_nt: bias_grad_acc [N]");
+    part = at::empty({pllm::gemm_nt_part_rows((int)M), N}, a.options().dtype(at::kFloat));
+    g.part = part.data_ptr<float>();
+  }
+  if (M > 0) {
+    pllm::gemm_nt(g, (int)epi, cur_stream());
+    if (epi == 2)
+      pllm::col_reduce(g.part, pllm::gemm_nt_part_rows((int)M), (int)N, bias_grad_acc->data_ptr(), true,
+                       cur_stream());
+  }
+  return outs;
+}
+
 // ---------------------------------------------------------------- activations
 Tensor act_fwd(const Tensor& x, int64_t op) {
   check_bf16(x, "x");
@@ -585,6 +639,9 @@ TORCH_LIBRARY(pllm, m) {
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
+  m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
+  m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_grad_acc=None) -> Tensor[]");
+  m.def("gemm_nt_set_pipe(int p) -> ()", [](int64_t p) { pllm::gemm_nt_set_pipe((int)p); });
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
   m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
@@ -627,5 +684,6 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("sample", sample);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_decode", attn_decode);
+  m.impl("gemm_nt", gemm_nt);
   m.impl("attn_bwd", attn_bwd);
 }

@@ -16,6 +16,17 @@ struct AttnFwdArgs {
   int causal;
 };
 
+// C[M, N] = A[M, K] . B[N, K]^T with fused MLP epilogues (gemm_nt.hip)
+struct GemmNTArgs {
+  const uint16_t *A, *B;
+  uint16_t* C;
+  uint16_t* aux;            // EPI 1: pre-activation out; EPI 2: pre-activation in
+  const uint16_t* bias;     // EPI 0/1 (optional)
+  float* part;              // EPI 2: [gemm_nt_part_rows(M), N] bias-gradient partials
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+};
+
 // q [B, H, D] (one query per sequence), k/v rows of a [B, S_max, Hkv, D]-strided cache
 struct DecodeArgs {
   const uint16_t *q, *k, *v;
@@ -100,9 +111,15 @@ void transpose_batch(const int64_t* desc, int n, int total_tiles, hipStream_t st
 void sample_tokens(const void* logits, bool bf16_in, int64_t ld, int B, int V, float temperature, uint64_t seed,
                    int64_t* out, hipStream_t st);
 
+// gemm_nt.hip
+int gemm_nt_part_rows(int M);
+void gemm_nt_set_pipe(int p);
+void gemm_nt(const GemmNTArgs& a, int epi, hipStream_t st);
+
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
+void attn_bwd_set_variant(int v);
 // attn_decode.hip: split-KV single-query attention over a KV cache
 bool attn_decode_supported(int D, int group);
 int attn_decode_splits(int B, int Hkv, int S_max);

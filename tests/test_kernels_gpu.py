@@ -302,6 +302,38 @@ def test_attention_decode_kernel(D, H, Hkv, B, S):
     assert torch.equal(o2, o) or _rel(o2, ref_o) < 1e-2
 
 
+@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(1000, 776, 128), (512, 3072, 768), (300, 256, 3072)])
+def test_gemm_nt_epilogues(pipe, M, N, K):
+    """NT GEMM (csrc/gemm_nt.hip) vs fp32 torch: plain + bias, GELU with pre-activation
+    output, dGELU with the bias-gradient column sums (ragged M and N edges included)."""
+    torch.manual_seed(M + N)
+    ops = _ops()
+    ops.gemm_nt_set_pipe(pipe)
+    try:
+        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
+        b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
+        bias = torch.randn(N, device=DEV, dtype=torch.bfloat16) * 0.1
+        ref = a.float() @ b.float().t()
+        (c0,) = ops.gemm_nt(a, b, None, 0)
+        assert _rel(c0, ref) < 5e-3
+        (c0b,) = ops.gemm_nt(a, b, bias, 0)
+        assert _rel(c0b, ref + bias.float()) < 5e-3
+        g, h = ops.gemm_nt(a, b, bias, 1)
+        href = ref + bias.float()
+        assert _rel(h, href) < 5e-3
+        assert _rel(g, F.gelu(h.float(), approximate="tanh")) < 5e-3
+        bg = torch.full((N,), 0.25, device=DEV, dtype=torch.bfloat16)   # accumulates into it
+        (dh,) = ops.gemm_nt(a, b, None, 2, h, bg)
+        hf = h.float().requires_grad_()
+        gl = F.gelu(hf, approximate="tanh")
+        (dref,) = torch.autograd.grad(gl, hf, ref)
+        assert _rel(dh, dref) < 1e-2
+        assert _rel(bg.float() - 0.25, dh.float().sum(0)) < 1e-2
+    finally:
+        ops.gemm_nt_set_pipe(0)
+
+
 @pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny"])
 def test_graphed_decode_matches_eager(preset):
     """generate(cuda_graph=True) (one hipGraph replay per token, device-side position and
