@@ -448,6 +448,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd
   constexpr int NTASK = NQB * NDB;
   const int tq_blk = w / NDB, tdb = w % NDB;
 
+  // static priority for the second-dispatched half of an 8-wave workgroup: it loses every
+  // VALU arbitration to its older SIMD partner otherwise (MI355X_MICROARCH.md, 'Two waves
+  // per SIMD' item 4)
+  if (C::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(1);
   if (total > 0) gload(0);
   for (int it = 0; it < total; ++it) {
     const int h = hk * G + it / per_head;
@@ -549,11 +553,13 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd
         acc = mfma32(A, Bf, acc);
       }
       const int64_t slab = (int64_t)a.B * a.T * a.H * D;
-      float* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
+      // bf16 slab: a partial over 256 keys rounded once (rel. 2^-9), summed in fp32 by the
+      // reduce -- half the slab bytes of fp32 on both the store and the reduce side
+      uint16_t* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = qt0 + acc_row(i, hh);
-        if (q < a.T) dq[(int64_t)q * a.H * D] = acc[i];
+        if (q < a.T) dq[(int64_t)q * a.H * D] = f2bf_bits(acc[i]);
       }
     }
   }
@@ -598,15 +604,12 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   if (a.causal) kmax = min(kmax, (t + a.S - a.T) / BK);
   const int64_t slab = nrows * D;
   float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const float* src = a.dq_acc + row * D + c * 8;
+  const uint16_t* src = a.dq_acc + row * D + c * 8;
   for (int kb = 0; kb <= kmax; ++kb) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(src + kb * slab);
-    const f32x4 x0 = p[0], x1 = p[1];
+    float x[8];
+    unpack8(ld16(src + kb * slab), x);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f[j] += x0[j];
-      f[4 + j] += x1[j];
-    }
+    for (int j = 0; j < 8; ++j) f[j] += x[j];
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] *= a.scale;

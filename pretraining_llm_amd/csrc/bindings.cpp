@@ -603,7 +603,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   // per-key-block dQ partial slabs (attention.hip: plain stores + ordered reduce, no atomics)
   const int64_t kbk = pllm::attn_bwd_key_block((int)D);
   const int64_t nkb = (S + kbk - 1) / kbk;
-  Tensor dq_acc = at::empty({nkb, B, T, H, D}, f32);
+  Tensor dq_acc = at::empty({nkb, B, T, H, D}, q.options());  // bf16 partial slabs
   AttnBwdArgs a{};
   a.q = (const uint16_t*)q.data_ptr();
   a.k = (const uint16_t*)k.data_ptr();
@@ -612,7 +612,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.dO = (const uint16_t*)dout.data_ptr();
   a.lse = lse.data_ptr<float>();
   a.delta = delta.data_ptr<float>();
-  a.dq_acc = dq_acc.data_ptr<float>();
+  a.dq_acc = (uint16_t*)dq_acc.data_ptr();
   a.dq = (uint16_t*)dq.data_ptr();
   a.dk = (uint16_t*)dk.data_ptr();
   a.dv = (uint16_t*)dv.data_ptr();

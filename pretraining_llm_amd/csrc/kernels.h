@@ -42,7 +42,7 @@ struct AttnBwdArgs {
   const uint16_t *q, *k, *v, *o, *dO;
   const float* lse;
   float* delta;   // [B, H, T] scratch
-  float* dq_acc;  // [B, T, H, D] fp32 scratch
+  uint16_t* dq_acc;  // [nkb][B, T, H, D] bf16 per-key-block dQ partial slabs
   uint16_t *dq, *dk, *dv;
   int B, H, Hkv, T, S, D;
   int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh, do_sb, do_st, do_sh;
