@@ -71,7 +71,7 @@ template <int MF>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part,
-                                                   uint16_t* __restrict__ out, int accumulate) {
+                                                   uint16_t* __restrict__ out, int accumulate, int g_prio) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
@@ -124,6 +124,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
+  if (g_prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // younger half: static priority (A/B: wgrad_set_mfma)
   if (nstage > 0) issue(0, 0);
   for (int st = 0; st < nstage; ++st) {
     const int buf = st & 1;
@@ -251,7 +252,13 @@ namespace pllm {
 // MFMA shape of the wgrad main loop (16 or 32); 32x32 measured 0-6% faster on the GPT-2 shapes
 // (profiles/r1_wgrad_mfma_ab.jsonl), so it is the default
 static int g_wgrad_mfma = 32;
-void wgrad_set_mfma(int mf) { g_wgrad_mfma = mf == 16 ? 16 : 32; }
+// +64 on the argument: static s_setprio(1) for waves 4-7 (A/B switch)
+static int g_wgrad_prio = 0;
+void wgrad_set_mfma(int mf) {
+  g_wgrad_prio = mf >= 64 ? 1 : 0;
+  mf = mf >= 64 ? mf - 64 : mf;
+  g_wgrad_mfma = mf == 16 ? 16 : 32;
+}
 
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   // pick the slice count that fills whole rounds of 256 workgroups (one per CU) best,
@@ -283,10 +290,10 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
   if (g_wgrad_mfma == 32)
     hipLaunchKernelGGL(wgrad_kernel<32>, dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,
-                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate);
+                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio);
   else
     hipLaunchKernelGGL(wgrad_kernel<16>, dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,
-                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate);
+                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio);
   if (S == 1) return;
   const int64_t PQ = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((PQ / 8 + 255) / 256)), dim3(256), 0, st, part, S, PQ,
