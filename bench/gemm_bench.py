@@ -28,6 +28,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--shapes", default="gpt2", choices=["gpt2", "llama"])
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
@@ -35,7 +36,8 @@ def main():
     enable_tuned_gemms(0)
     dev = torch.device("cuda")
     M = args.M
-    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (50304, 768)]
+    shapes = {"gpt2": [(2304, 768), (768, 768), (3072, 768), (768, 3072), (50304, 768)],
+              "llama": [(6144, 2048), (2048, 2048), (11008, 2048), (2048, 5504), (50304, 2048)]}[args.shapes]
     out = []
     for P, Q in shapes:
         torch.manual_seed(0)
@@ -48,17 +50,17 @@ def main():
         rel = ((r.float() - ref).norm() / ref.norm()).item()
         flops = 2.0 * M * P * Q
         res = {"P": P, "Q": Q, "M": M, "rel_err": rel}
-        for mf in (32, 96):  # 32x32 MFMA main loop without / with (+64) static priority for waves 4-7
+        for mf in (32, 160):  # cost-model split plan / (+128) the older fill-efficiency plan
             torch.ops.pllm.wgrad_set_mfma(mf)
             r = torch.ops.pllm.wgrad(dy[:4096], x[:4096])
             res[f"rel_err{mf}"] = ((r.float() - ref).norm() / ref.norm()).item()
         for _ in range(args.rounds):
-            for mf in (32, 96):
+            for mf in (32, 160):
                 torch.ops.pllm.wgrad_set_mfma(mf)
                 res.setdefault(f"hip{mf}_us", []).append(1e6 * timeit(lambda: torch.ops.pllm.wgrad(dy, x, tgt)))
             res.setdefault("blas_us", []).append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
         torch.ops.pllm.wgrad_set_mfma(32)
-        for k in ("hip32", "hip96", "blas"):
+        for k in ("hip32", "hip160", "blas"):
             res[f"{k}_tflops"] = flops / (min(res[f"{k}_us"]) * 1e-6) / 1e12
         print(json.dumps(res), flush=True)
         out.append(res)

@@ -344,12 +344,14 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //   D = 128 : 4 waves, 128 keys, 32 queries (register budget: dK^T/dV^T alone are 128 regs).
 //   V = 1 (D <= 64): 4 waves, 128 keys, 64 queries: 48 KiB of LDS, so TWO workgroups share a
 //             CU and one's barrier waits overlap the other's MFMA work (more dQ slabs).
+//   V = 1 (D = 128): 8 waves, 256 keys, 32 queries (two waves per SIMD at <= 256 VGPRs).
 template <int D, int V = 0>
 struct BwdCfg {
-  static constexpr int NW = (D <= 64 && V == 0) ? 8 : 4;
+  static constexpr int NW = D <= 64 ? (V == 0 ? 8 : 4) : (V == 0 ? 4 : 8);
   static constexpr int NT = 64 * NW;
   static constexpr int BK = 32 * NW;
   static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : 32;
+  static constexpr int MIN_WAVES = (D == 128 && NW == 4) ? 1 : 2;
   static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
   static constexpr int QLPT = (BQ * CPR + NT - 1) / NT;
@@ -360,7 +362,7 @@ struct BwdCfg {
 // D=128 keeps dK^T/dV^T (128 regs) + K/V fragments (64) + S/dP in registers: one wave per
 // SIMD with the full register file instead of spilling at the 2-waves/SIMD budget.
 template <int D, int V>
-__global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd_kernel(AttnBwdArgs a) {
+__global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D, V>;
   using I = Img<D>;
   using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
@@ -387,11 +389,14 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
-  // this lane's key row of K and V as B-operand fragments (k = head dim)
-  bf16x8 kf[NKS], vf[NKS];
+  // this lane's key row of K and V as B-operand fragments (k = head dim).  The 8-wave D=128
+  // variant reads its K fragments from the LDS K image instead (32 fewer VGPRs: no spills at
+  // two waves per SIMD).
+  constexpr bool KF_LDS = (D == 128 && V == 1);
+  bf16x8 kf[KF_LDS ? 1 : NKS], vf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
-    kf[ks] = key < a.S ? as_frag(ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh)) : zero_frag();
+    if constexpr (!KF_LDS) kf[ks] = key < a.S ? as_frag(ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh)) : zero_frag();
     vf[ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
   }
   // whole K block into LDS for the dQ product
@@ -497,7 +502,8 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), D == 128 ? 1 : 2) void attn_bwd
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         const bf16x8 qa = as_frag(ld16(Ql + I::off(32 * j + r, 16 * ks + 8 * hh)));
-        s = mfma32(qa, kf[ks], s);
+        if constexpr (KF_LDS) s = mfma32(qa, as_frag(ld16(Kl + I::off(kl, 16 * ks + 8 * hh))), s);
+        else s = mfma32(qa, kf[ks], s);
         const bf16x8 oa = as_frag(ld16(Ol + I::off(32 * j + r, 16 * ks + 8 * hh)));
         dp = mfma32(oa, vf[ks], dp);
       }
@@ -624,12 +630,13 @@ bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
 // backward tiling variant for D <= 64 (BwdCfg): 0 = 8-wave 256-key workgroups, 1 = 4-wave
 // 128-key workgroups two per CU
+// bit 0: variant for D <= 64, bit 1: variant for D = 128 (BwdCfg)
 static int g_bwd_variant = 0;
-void attn_bwd_set_variant(int v) { g_bwd_variant = v == 1 ? 1 : 0; }
+void attn_bwd_set_variant(int v) { g_bwd_variant = v & 3; }
 
 int attn_bwd_key_block(int D) {
-  if (D <= 64) return g_bwd_variant == 1 ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
-  return BwdCfg<128>::BK;
+  if (D <= 64) return (g_bwd_variant & 1) ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
+  return (g_bwd_variant & 2) ? BwdCfg<128, 1>::BK : BwdCfg<128, 0>::BK;
 }
 
 template <int D>
@@ -655,9 +662,9 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
-  if (a.D == 32) g_bwd_variant == 1 ? attn_bwd_t<32, 1>(a, st) : attn_bwd_t<32, 0>(a, st);
-  else if (a.D == 64) g_bwd_variant == 1 ? attn_bwd_t<64, 1>(a, st) : attn_bwd_t<64, 0>(a, st);
-  else attn_bwd_t<128, 0>(a, st);
+  if (a.D == 32) (g_bwd_variant & 1) ? attn_bwd_t<32, 1>(a, st) : attn_bwd_t<32, 0>(a, st);
+  else if (a.D == 64) (g_bwd_variant & 1) ? attn_bwd_t<64, 1>(a, st) : attn_bwd_t<64, 0>(a, st);
+  else (g_bwd_variant & 2) ? attn_bwd_t<128, 1>(a, st) : attn_bwd_t<128, 0>(a, st);
 }
 
 }  // namespace pllm

@@ -254,27 +254,42 @@ namespace pllm {
 static int g_wgrad_mfma = 32;
 // +64 on the argument: static s_setprio(1) for waves 4-7 (A/B switch)
 static int g_wgrad_prio = 0;
+static int g_wgrad_plan_fill = 0;  // A/B (+128): the older fill-efficiency-only split plan
 void wgrad_set_mfma(int mf) {
+  g_wgrad_plan_fill = (mf & 128) ? 1 : 0;
+  mf &= 127;
   g_wgrad_prio = mf >= 64 ? 1 : 0;
   mf = mf >= 64 ? mf - 64 : mf;
   g_wgrad_mfma = mf == 16 ? 16 : 32;
 }
 
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
-  // pick the slice count that fills whole rounds of 256 workgroups (one per CU) best,
-  // keeping >= 8 stages per slice; ties go to fewer slices (less slab traffic)
+  // Split-K slice count from a cost model: rounds of 256 workgroups (one per CU) x stages per
+  // slice x ~2.0 us per 256x256x64 stage, plus -- for S > 1 -- the fp32 slab traffic (S slabs
+  // written by the main kernel and read back by the reduce) at ~4 TB/s.  The slab term is what
+  // keeps S small when P x Q is large (llama MLP: 11008 x 2048 at 16K tokens -> S = 2, not 11).
+  // >= 8 stages per slice; near-ties (< 2 %) go to fewer slices.
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
   const int kst = M / BKM;
   int best = 1;
-  double best_eff = 0.0;
+  double best_t = 1e30, best_eff = 0.0;
   for (int s = 1; s <= 64; ++s) {
     if (s > 1 && kst / s < 8) break;
     const int n = ntiles * s;
     const int rounds = (n + 255) / 256;
-    // a round of 256 costs (stages per slice); efficiency = useful / issued work
-    const double eff = (double)n / (256.0 * rounds);
-    if (eff > best_eff + 0.02) {
-      best_eff = eff;
+    if (g_wgrad_plan_fill) {
+      const double eff = (double)n / (256.0 * rounds);
+      if (eff > best_eff + 0.02) {
+        best_eff = eff;
+        best = s;
+      }
+      continue;
+    }
+    const int st_per = (kst + s - 1) / s;
+    double t = rounds * (double)st_per * 2.0e-6;
+    if (s > 1) t += (double)P * Q * 4.0 * (2 * s + 1) / 4.0e12;
+    if (t < best_t * 0.98) {
+      best_t = t;
       best = s;
     }
   }

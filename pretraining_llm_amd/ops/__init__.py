@@ -121,6 +121,10 @@ import os as _os
 # (bench/gemm_bench.py, profiles/r1_wgrad_v2_gemm_bench.jsonl); "blas" = hipBLASLt/rocBLAS
 # through torch (beta=1 addmm into the flat gradient)
 WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
+# (tokens M, P, Q) weight-gradient shapes where hipBLASLt measured faster than the hand-written
+# kernel on MI355X (bench/gemm_bench.py --shapes llama --M 16384, profiles/r1_wgrad_plan_ab.jsonl):
+# llama-1.3B at 8 x 2048 tokens -- QKV, MLP down projection and LM head
+WGRAD_BLAS_SHAPES = {(16384, 6144, 2048), (16384, 2048, 5504), (16384, 50304, 2048)}
 
 
 def _dgrad(dy, weight):
@@ -137,7 +141,8 @@ def _dgrad(dy, weight):
 def _weight_grad(dy2, x2, tgt):
     """dW = dy2^T @ x2, added into ``tgt`` when given (returns None) else returned."""
     use_hip = (WGRAD_ENGINE == "hip" and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
-               and dy2.shape[0] % 64 == 0)
+               and dy2.shape[0] % 64 == 0
+               and (dy2.shape[0], dy2.shape[1], x2.shape[1]) not in WGRAD_BLAS_SHAPES)
     if use_hip:
         dy2, x2 = dy2.contiguous(), x2.contiguous()
         if tgt is not None:
