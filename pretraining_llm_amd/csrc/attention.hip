@@ -344,13 +344,15 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //   D = 128 : 4 waves, 128 keys, 32 queries (register budget: dK^T/dV^T alone are 128 regs).
 //   V = 1 (D <= 64): 4 waves, 128 keys, 64 queries: 48 KiB of LDS, so TWO workgroups share a
 //             CU and one's barrier waits overlap the other's MFMA work (more dQ slabs).
-//   V = 1 (D = 128): 8 waves, 256 keys, 32 queries (two waves per SIMD at <= 256 VGPRs).
+//   V = 1, 2 (D = 128): 4 waves, 128 keys, 64 / 128 queries per iteration (1/2, 1/4 of the
+//             barriers per query of V = 0; every wave runs 2 / 4 dQ tasks).  V = 1 measured
+//             1349 -> 1083 us at B=8 H=16 T=2048 (profiles/r1_attn_bwd_d128_bq_ab.jsonl).
 template <int D, int V = 0>
 struct BwdCfg {
-  static constexpr int NW = D <= 64 ? (V == 0 ? 8 : 4) : (V == 0 ? 4 : 8);
+  static constexpr int NW = D <= 64 ? (V == 0 ? 8 : 4) : 4;
   static constexpr int NT = 64 * NW;
   static constexpr int BK = 32 * NW;
-  static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : 32;
+  static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : (32 << V);
   static constexpr int MIN_WAVES = (D == 128 && NW == 4) ? 1 : 2;
   static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
@@ -392,7 +394,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   // this lane's key row of K and V as B-operand fragments (k = head dim).  The 8-wave D=128
   // variant reads its K fragments from the LDS K image instead (32 fewer VGPRs: no spills at
   // two waves per SIMD).
-  constexpr bool KF_LDS = (D == 128 && V == 1);
+  constexpr bool KF_LDS = false;  // true: K fragments from the LDS image (32 fewer VGPRs)
   bf16x8 kf[KF_LDS ? 1 : NKS], vf[NKS];
 #pragma unroll
   for (int ks = 0; ks < NKS; ++ks) {
@@ -451,7 +453,6 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
 
   // dQ task of this wave in each iteration: (query sub-block, d-block)
   constexpr int NTASK = NQB * NDB;
-  const int tq_blk = w / NDB, tdb = w % NDB;
 
   // static priority for the second-dispatched half of an 8-wave workgroup: it loses every
   // VALU arbitration to its older SIMD partner otherwise (MI355X_MICROARCH.md, 'Two waves
@@ -542,8 +543,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     }
     __syncthreads();
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
-    // d-block) task per wave, summed over all BK keys on chip, stored into the key block's slab.
-    if (w < NTASK) {
+    // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
+    // the key block's slab.
+    for (int task = w; task < NTASK; task += C::NW) {
+      const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
       // causal: key steps entirely after the task's last query contribute zeros -> skip
       int ks_end = BK / 16;
@@ -630,13 +633,13 @@ bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
 // backward tiling variant for D <= 64 (BwdCfg): 0 = 8-wave 256-key workgroups, 1 = 4-wave
 // 128-key workgroups two per CU
-// bit 0: variant for D <= 64, bit 1: variant for D = 128 (BwdCfg)
-static int g_bwd_variant = 0;
-void attn_bwd_set_variant(int v) { g_bwd_variant = v & 3; }
+// v & 1: variant for D <= 64 (default 0); (v >> 1) & 3: variant for D = 128 (default 1) (BwdCfg)
+static int g_bwd_variant = 1 << 1;
+void attn_bwd_set_variant(int v) { g_bwd_variant = v & 7; }
 
 int attn_bwd_key_block(int D) {
   if (D <= 64) return (g_bwd_variant & 1) ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
-  return (g_bwd_variant & 2) ? BwdCfg<128, 1>::BK : BwdCfg<128, 0>::BK;
+  return BwdCfg<128>::BK;  // 128 keys in every D = 128 variant
 }
 
 template <int D>
@@ -664,7 +667,12 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
   if (a.D == 32) (g_bwd_variant & 1) ? attn_bwd_t<32, 1>(a, st) : attn_bwd_t<32, 0>(a, st);
   else if (a.D == 64) (g_bwd_variant & 1) ? attn_bwd_t<64, 1>(a, st) : attn_bwd_t<64, 0>(a, st);
-  else (g_bwd_variant & 2) ? attn_bwd_t<128, 1>(a, st) : attn_bwd_t<128, 0>(a, st);
+  else {
+    const int v = (g_bwd_variant >> 1) & 3;
+    if (v == 0) attn_bwd_t<128, 0>(a, st);
+    else if (v == 1) attn_bwd_t<128, 1>(a, st);
+    else attn_bwd_t<128, 2>(a, st);
+  }
 }
 
 }  // namespace pllm
