@@ -87,6 +87,7 @@ default_config = {
     'profile_dir': None,              # torch.profiler (ROCm activity) chrome traces + kernel table per rank
     'profile_steps': '3:6',           # [start:end) optimizer steps to profile
     'deterministic': False,           # torch.use_deterministic_algorithms + fixed-order kernels only
+    'debug_sync': False,              # AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1 (set before HIP init)
 }
 
 # Named BASELINE.json configurations (override default_config)

@@ -8,7 +8,14 @@ include only ``hip_runtime.h`` so they compile in seconds), ``bindings.cpp``
 that ship with the installed PyTorch-ROCm.  Objects are cached under
 ``csrc/build`` and rebuilt when a source or header changes.
 
-Usage: ``python -m pretraining_llm_amd.build [--force] [-j N]``
+Usage: ``python -m pretraining_llm_amd.build [--force] [-j N] [--debug]``
+
+``--debug`` rebuilds everything with ``-DPLLM_DEBUG``: the kernels then report contract
+violations they otherwise tolerate silently (out-of-range token ids / targets) with a device
+printf naming the kernel and the offending value (no trap: a faulting kernel can take the
+whole node down).  Combine with ``debug_sync=True`` in the trainer config
+(AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1) to attribute a failure to one launch.
+Rebuild with ``--force`` to return to the release objects.
 """
 from __future__ import annotations
 
@@ -73,7 +80,11 @@ def build_host(force: bool = False) -> str:
     return HOST_OUT
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool = False) -> str:
+    global COMMON_FLAGS
+    if debug:
+        force = True
+        COMMON_FLAGS = COMMON_FLAGS + ["-DPLLM_DEBUG=1"]
     build_host(force)
     os.makedirs(BUILD, exist_ok=True)
     hipcc = _hipcc()
@@ -113,8 +124,9 @@ def main(argv=None):
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=int(os.environ.get("MAX_JOBS", "8")))
     ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--debug", action="store_true", help="device-side contract diagnostics (-DPLLM_DEBUG)")
     args = ap.parse_args(argv)
-    out = build(force=args.force, jobs=args.jobs, verbose=args.verbose)
+    out = build(force=args.force, jobs=args.jobs, verbose=args.verbose, debug=args.debug)
     print(out)
 
 

@@ -110,3 +110,16 @@ PLLM_DEV int xcd_remap(int orig, int nwg) {
 }
 
 #define PLLM_CHECK_LAUNCH() (void)hipGetLastError()
+
+// Debug builds (python -m pretraining_llm_amd.build --debug): report a violated device-side
+// contract with printf and carry on (the kernels stay defensive; no trap, which would fault).
+#ifdef PLLM_DEBUG
+#define PLLM_DCHECK(cond, what, val)                                                              \
+  do {                                                                                            \
+    if (!(cond)) printf("[pllm debug] %s: %s violated (value %lld)\n", __func__, what, (long long)(val)); \
+  } while (0)
+#else
+#define PLLM_DCHECK(cond, what, val) \
+  do {                               \
+  } while (0)
+#endif

@@ -69,6 +69,7 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
   for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
   const int64_t t = targets[row];
   const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
+  if (threadIdx.x == 0) PLLM_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
   if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - bf2f(x[t])) : 0.f;
   if (!WRITE_GRAD) return;
   __syncthreads();  // every lane has read its logits before in-place overwrite (x may alias dlogits)

@@ -48,6 +48,11 @@ def build_config(argv=None) -> dict:
 
 def main(argv=None):
     cfg = build_config(argv)
+    if cfg.get("debug_sync"):
+        # serialize every kernel launch so a fault is attributed to the launch that caused it;
+        # must be in the environment before the HIP runtime initialises (torch import below)
+        os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+        os.environ.setdefault("HIP_LAUNCH_BLOCKING", "1")
     from pretraining_llm_amd.train import Trainer
     from pretraining_llm_amd.utils.dist import destroy
     trainer = Trainer(cfg)
