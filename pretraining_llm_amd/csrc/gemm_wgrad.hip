@@ -67,19 +67,30 @@ constexpr int NT = 512;             // 8 waves
 constexpr int HALF = BKM * 128;     // elements of one [64][128] image
 constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 2,3 (64 KiB)
 
-template <int MF>
+// RING 0: 64-token stages in two slots (vmcnt(0) + barrier per stage, one stage of prefetch);
+// RING 1/2: 32-token stages in a 4/5-slot ring with 3/4 stages in flight across raw barriers
+// (counted vmcnt): more load latency covered per stage of MFMA work.  Measured 4-15 % SLOWER
+// than RING 0 on every GPT-2 / llama shape (profiles/r1_wgrad_ring_ab.jsonl): the extra
+// barriers cost more than the latency they hide, so RING 0 is the default.
+template <int MF, int RING>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part,
                                                    uint16_t* __restrict__ out, int accumulate, int g_prio) {
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
+  constexpr int BK_ = RING == 0 ? BKM : 32;
+  constexpr int SLOTS = RING == 0 ? 2 : (RING == 1 ? 4 : 5);
+  constexpr int AHEAD = SLOTS - 1;
+  constexpr int HALF_ = BK_ * 128, STAGE_ = 4 * HALF_;
+  constexpr int QUADS = BK_ / 4;  // row-quads per image
+  constexpr int PPW = BK_ / 8;    // 1-KiB pieces per wave and stage
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[SLOTS * STAGE_];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int s = lid / ntiles, t = lid % ntiles;
   const int p0 = (t / tiles_q) * BT, q0 = (t % tiles_q) * BT;
   const int m_begin = s * slice;
-  const int nstage = (min(M, m_begin + slice) - m_begin) / BKM;
+  const int nstage = (min(M, m_begin + slice) - m_begin) / BK_;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wp = w >> 2, wq = w & 3;  // wave's 128x64 sub-tile
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
@@ -88,25 +99,26 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   // Lane l of a piece fills image row 4*quad + l/16, chunk position l%16, which holds
   // logical chunk (l%16) ^ swz(row).  Columns past P/Q are clamped to a valid chunk:
   // they only feed output rows/columns that are never stored.
-  const uint16_t* src[8];
-  int dst[8];
+  const uint16_t* src[PPW];
+  int dst[PPW];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int pc = w * 8 + k, opnd = pc >> 5, half = (pc >> 4) & 1, quad = pc & 15;
+  for (int k = 0; k < PPW; ++k) {
+    const int pc = w * PPW + k, opnd = pc / (2 * QUADS), half = (pc / QUADS) & 1, quad = pc % QUADS;
     const int row = 4 * quad + (lane >> 4);
     const int col = half * 128 + (((lane & 15) ^ swz(row)) << 3);
     if (opnd == 0) src[k] = A + (int64_t)(m_begin + row) * lda + min(p0 + col, P - 8);
     else src[k] = B + (int64_t)(m_begin + row) * ldb + min(q0 + col, Q - 8);
-    dst[k] = (opnd * 2 + half) * HALF + quad * 512;
+    dst[k] = (opnd * 2 + half) * HALF_ + quad * 512;
   }
-  const int64_t astep = (int64_t)BKM * lda, bstep = (int64_t)BKM * ldb;
+  const int64_t astep = (int64_t)BK_ * lda, bstep = (int64_t)BK_ * ldb;
   const unsigned lds_base = (unsigned)(uintptr_t)smem;
-  auto issue = [&](int st, int buf) {
+  auto issue = [&](int st) {
+    const int slot = st % SLOTS;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int opnd = (w * 8 + k) >> 5;
+    for (int k = 0; k < PPW; ++k) {
+      const int opnd = (w * PPW + k) / (2 * QUADS);
       const uint16_t* g = src[k] + st * (opnd == 0 ? astep : bstep);
-      glds16(g, lds_base + 2u * (unsigned)(buf * STAGE + dst[k]));
+      glds16(g, lds_base + 2u * (unsigned)(slot * STAGE_ + dst[k]));
     }
   };
 
@@ -125,18 +137,32 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
   if (g_prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // younger half: static priority (A/B: wgrad_set_mfma)
-  if (nstage > 0) issue(0, 0);
+#pragma unroll
+  for (int s0 = 0; s0 < AHEAD; ++s0)
+    if (s0 < nstage) issue(s0);
   for (int st = 0; st < nstage; ++st) {
-    const int buf = st & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage st landed for every wave; nobody still reads buf ^ 1
-    if (st + 1 < nstage) issue(st + 1, buf ^ 1);
-    const uint16_t* Ai = smem + buf * STAGE + wp * HALF;
-    const uint16_t* Bi = smem + buf * STAGE + (2 + (wq >> 1)) * HALF;
+    const int slot = st % SLOTS;
+    if constexpr (RING == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // stage st landed for every wave; nobody still reads the other slot
+    } else {
+      // retire stage st, keep the stages issued after it in flight across the barrier
+      const int pending = min(AHEAD - 1, nstage - 1 - st);
+      if (pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // stage st landed for every wave; slot of st-1 is free
+      asm volatile("" ::: "memory");
+    }
+    if (st + AHEAD < nstage) issue(st + AHEAD);
+    const uint16_t* Ai = smem + slot * STAGE_ + wp * HALF_;
+    const uint16_t* Bi = smem + slot * STAGE_ + (2 + (wq >> 1)) * HALF_;
     const int bcol = (wq & 1) * 64;
     if constexpr (MF == 32) {
 #pragma unroll
-      for (int k16 = 0; k16 < BKM / 16; ++k16) {
+      for (int k16 = 0; k16 < BK_ / 16; ++k16) {
         const int row = k16 * 16 + 8 * hh + tq;
         bf16x8 af[4], bfr[2];
 #pragma unroll
@@ -158,7 +184,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       // 16x16x32 operand: lane l holds column l%16, reduction rows 8*(l/16) .. +7
       const int gq = lane >> 4;
 #pragma unroll
-      for (int k32 = 0; k32 < BKM / 32; ++k32) {
+      for (int k32 = 0; k32 < BK_ / 32; ++k32) {
         const int row = k32 * 32 + 8 * gq + tq;
         bf16x8 af[8], bfr[4];
 #pragma unroll
@@ -255,7 +281,10 @@ static int g_wgrad_mfma = 32;
 // +64 on the argument: static s_setprio(1) for waves 4-7 (A/B switch)
 static int g_wgrad_prio = 0;
 static int g_wgrad_plan_fill = 0;  // A/B (+128): the older fill-efficiency-only split plan
+static int g_wgrad_ring = 0;       // A/B (+256 / +512): staging ring 1 / 2 (wgrad_kernel RING)
 void wgrad_set_mfma(int mf) {
+  g_wgrad_ring = (mf & 512) ? 2 : ((mf & 256) ? 1 : 0);
+  mf &= 255;
   g_wgrad_plan_fill = (mf & 128) ? 1 : 0;
   mf &= 127;
   g_wgrad_prio = mf >= 64 ? 1 : 0;
@@ -303,12 +332,14 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-  if (g_wgrad_mfma == 32)
-    hipLaunchKernelGGL(wgrad_kernel<32>, dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,
-                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio);
-  else
-    hipLaunchKernelGGL(wgrad_kernel<16>, dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,
-                       (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio);
+#define PLLM_WGRAD_LAUNCH(MFV, RV)                                                                         \
+  hipLaunchKernelGGL((wgrad_kernel<MFV, RV>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,   \
+                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio)
+  if (g_wgrad_mfma == 16) PLLM_WGRAD_LAUNCH(16, 0);
+  else if (g_wgrad_ring == 1) PLLM_WGRAD_LAUNCH(32, 1);
+  else if (g_wgrad_ring == 2) PLLM_WGRAD_LAUNCH(32, 2);
+  else PLLM_WGRAD_LAUNCH(32, 0);
+#undef PLLM_WGRAD_LAUNCH
   if (S == 1) return;
   const int64_t PQ = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((PQ / 8 + 255) / 256)), dim3(256), 0, st, part, S, PQ,
