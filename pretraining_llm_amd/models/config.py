@@ -42,7 +42,9 @@ class ModelConfig:
     rope_theta: float = 10000.0
     init: str = "gpt2"                       # gpt2 | torch_default
     init_std: float = 0.02
-    activation_checkpointing: bool = False
+    # True / False, or "auto": checkpoint only when the estimated activation memory of a
+    # step would not fit comfortably in the GPU's free HBM (GPT.use_checkpointing)
+    activation_checkpointing: object = False
     dtype: str = "bfloat16"                  # compute/parameter dtype for training
 
     def __post_init__(self):

@@ -186,3 +186,13 @@ def test_gqa_llama_forward_backward():
     _, loss = m(x, x)
     loss.backward()
     assert all(p.grad is not None for p in m.parameters())
+
+
+def test_activation_checkpointing_auto_policy():
+    """'auto' checkpoints only when the activation estimate exceeds half the free HBM: never
+    on CPU tensors; the estimate is 2 B x (6C + 2F) per token and layer."""
+    cfg = get_preset("gpt2-medium").replace(vocab_size=256, context_length=64, activation_checkpointing="auto")
+    m = GPT(cfg)
+    assert m.activation_bytes(32768) == 2 * (6 * 1024 + 2 * 4096) * 32768 * 24
+    assert m.use_checkpointing(torch.zeros(2, 8, dtype=torch.long)) is False
+    assert GPT(_tiny().replace(activation_checkpointing=True)).use_checkpointing(torch.zeros(1, 4, dtype=torch.long))
