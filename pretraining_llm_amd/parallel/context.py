@@ -99,18 +99,30 @@ class _Ring:
         self.reqs = []
 
     def start(self, tensors: List[torch.Tensor]) -> List[torch.Tensor]:
-        recv = [torch.empty_like(t) for t in tensors]
+        # gloo moves CPU tensors only: device blocks travel through pinned host copies there
+        # (test / CPU-cluster path); on RCCL they go GPU to GPU over xGMI
+        self.host = dist.get_backend(self.group) == "gloo" and tensors[0].is_cuda
+        send = [t.contiguous() for t in tensors]
+        if self.host:
+            send = [t.cpu() for t in send]
+        recv = [torch.empty_like(t) for t in send]
         p2p = []
-        for t, rv in zip(tensors, recv):
-            p2p.append(dist.P2POp(dist.isend, t.contiguous(), self.nxt, self.group))
+        for t, rv in zip(send, recv):
+            p2p.append(dist.P2POp(dist.isend, t, self.nxt, self.group))
             p2p.append(dist.P2POp(dist.irecv, rv, self.prv, self.group))
         self.reqs = dist.batch_isend_irecv(p2p)
+        self.recv, self.dev = recv, tensors[0].device
         return recv
 
     def wait(self):
         for q in self.reqs:
             q.wait()
         self.reqs = []
+        if self.host:
+            # hand back device tensors in place of the host buffers start() returned
+            for i, t in enumerate(self.recv):
+                self.recv[i] = t.to(self.dev, non_blocking=False)
+        return self.recv
 
 
 def _split(x: torch.Tensor, n: int) -> List[torch.Tensor]:
