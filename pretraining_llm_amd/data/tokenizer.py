@@ -57,7 +57,13 @@ def get_tokenizer(name: str = "gpt2"):
     try:
         from transformers import GPT2TokenizerFast  # type: ignore
         tok = GPT2TokenizerFast.from_pretrained("gpt2", local_files_only=True)
-        return _HFWrap(tok)
+        wrap = _HFWrap(tok)
+        # a cache entry without the BPE vocab/merges loads but encodes everything to []:
+        # only accept a tokenizer that round-trips a probe string
+        probe = "Hello world"
+        ids = wrap.encode_ordinary(probe)
+        if ids and wrap.decode(ids) == probe:
+            return wrap
     except Exception:
         pass
     return ByteTokenizer()

@@ -106,6 +106,8 @@ def test_generate_text_cli_loads_trainer_checkpoint(tmp_path):
                           "--device", "cpu", "--seed", "0"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert out.stdout.startswith("Generated text:\n")
+    # the prompt survives the encode -> generate -> decode round trip (whatever tokenizer resolved)
+    assert out.stdout[len("Generated text:\n"):].startswith("hello")
 
 
 def test_reference_style_checkpoint_loads_in_generate(tmp_path):
