@@ -196,3 +196,16 @@ def test_activation_checkpointing_auto_policy():
     assert m.activation_bytes(32768) == 2 * (6 * 1024 + 2 * 4096) * 32768 * 24
     assert m.use_checkpointing(torch.zeros(2, 8, dtype=torch.long)) is False
     assert GPT(_tiny().replace(activation_checkpointing=True)).use_checkpointing(torch.zeros(1, 4, dtype=torch.long))
+
+
+@pytest.mark.parametrize("mod", ["attention", "mlp", "transformer_block", "transformer"])
+def test_reference_module_demos_run(mod):
+    """The src.models.* modules keep the reference's runnable shape demos."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", f"src.models.{mod}"], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "->" in r.stdout or "loss" in r.stdout
