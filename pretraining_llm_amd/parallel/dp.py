@@ -122,6 +122,8 @@ class DataParallelEngine:
         return hook
 
     def _launch(self, b):
+        from .. import ops
+        ops.sync_side_streams()  # side-stream weight gradients of this bucket must have landed
         bk = self.buckets[b]
         view = self.opt.flat_grad[bk["start"]:bk["end"]]
         self._handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
@@ -144,6 +146,8 @@ class DataParallelEngine:
     def finish_grad_sync(self):
         """Launch any bucket not yet launched (unused params, no-overlap mode) and wait for all.
         Returns the gradient scale the optimizer must apply (1/world)."""
+        from .. import ops
+        ops.sync_side_streams()
         if self.world > 1:
             while self._next_launch < len(self.buckets):
                 self._launch(self._next_launch)

@@ -239,6 +239,8 @@ class ZeroDataParallelEngine:
         return hook
 
     def _launch(self, b):
+        from .. import ops
+        ops.sync_side_streams()
         opt = self.opt
         bs, be = opt.buckets[b]
         fs, fe, o = opt.own[b]
@@ -261,6 +263,8 @@ class ZeroDataParallelEngine:
             self.enabled = old
 
     def finish_grad_sync(self):
+        from .. import ops
+        ops.sync_side_streams()
         opt = self.opt
         if self.world > 1:
             while self._next_launch < len(opt.buckets):
