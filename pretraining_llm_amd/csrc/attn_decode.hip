@@ -30,7 +30,6 @@ constexpr int NT = 256;
 template <int D, int G, int U>
 __global__ __launch_bounds__(NT) void attn_decode_kernel(DecodeArgs a) {
   constexpr int LPR = D / 8;          // lanes per key row
-  constexpr int KPW = 64 / LPR;       // key-slices per wave
   constexpr int NKS = NT / LPR;       // key-slices per workgroup
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
@@ -103,7 +102,7 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(DecodeArgs a) {
     }
   }
 
-  // merge the KPW key-slices of this wave (lane bits above log2(LPR))
+  // merge the 64 / LPR key-slices of this wave (lane bits above log2(LPR))
 #pragma unroll
   for (int o = LPR; o < 64; o <<= 1) {
 #pragma unroll
@@ -133,7 +132,6 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(DecodeArgs a) {
     }
   }
   __syncthreads();
-  (void)KPW;
   for (int i = t; i < G * D; i += NT) {
     const int g = i / D, d = i % D;
     float mx = -INFINITY;

@@ -111,7 +111,8 @@ class FlatAdamW:
         # data-gradient GEMMs read W^T contiguously (ops._dgrad), the layout hipBLASLt serves
         # faster.  One extra bf16 copy of the matrices (~250 MB for GPT-2 small).
         if transposed_shadow is None:
-            transposed_shadow = self.use_hip
+            import os as _os
+            transposed_shadow = self.use_hip and _os.environ.get("PLLM_WT_SHADOW", "1") == "1"
         self.shadowed = [p for p in params if transposed_shadow and p.dim() == 2]
         sh_off, o = [], 0
         for p in self.shadowed:
