@@ -168,6 +168,29 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   return out;
 }
 
+// ---------------------------------------------------------------- skinny GEMM (decode)
+// y[M, N] = x[M, K] w[N, K]^T (+ bias) for M <= 8 token rows
+Tensor gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias) {
+  check_bf16(x, "x");
+  check_bf16(w, "w");
+  TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv: x [M,K], w [N,K]");
+  const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
+  TORCH_CHECK(M <= pllm::gemv_max_rows(), "gemv: at most ", pllm::gemv_max_rows(), " rows");
+  TORCH_CHECK(K % 8 == 0 && x.stride(1) == 1 && w.stride(1) == 1 && x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
+              "gemv: K % 8 == 0, unit column stride, row strides % 8");
+  check_aligned16(x, "x");
+  check_aligned16(w, "w");
+  if (bias) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemv: bias [N]");
+  }
+  Tensor y = at::empty({M, N}, x.options());
+  if (M > 0 && N > 0)
+    pllm::gemv(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), opt_ptr(bias), y.data_ptr(), N, (int)M, (int)N,
+               (int)K, cur_stream());
+  return y;
+}
+
 // ---------------------------------------------------------------- NT GEMM + MLP epilogues
 // epi 0: [a b^T (+bias)];  epi 1: [gelu(h), h] with h = a b^T + bias;
 // epi 2: [(a b^T) * gelu'(aux)], adding its column sums into ``bias_grad_acc`` (bf16, in place)
@@ -641,6 +664,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_grad_acc=None) -> Tensor[]");
+  m.def("gemv(Tensor x, Tensor w, Tensor? bias) -> Tensor");
   m.def("gemm_nt_set_pipe(int p) -> ()", [](int64_t p) { pllm::gemm_nt_set_pipe((int)p); });
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
@@ -685,5 +709,6 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_decode", attn_decode);
   m.impl("gemm_nt", gemm_nt);
+  m.impl("gemv", gemv);
   m.impl("attn_bwd", attn_bwd);
 }

@@ -111,6 +111,11 @@ void transpose_batch(const int64_t* desc, int n, int total_tiles, hipStream_t st
 void sample_tokens(const void* logits, bool bf16_in, int64_t ld, int B, int V, float temperature, uint64_t seed,
                    int64_t* out, hipStream_t st);
 
+// gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ bias) for M <= gemv_max_rows() (decode projections)
+int gemv_max_rows();
+void gemv(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy, int M,
+          int N, int K, hipStream_t st);
+
 // gemm_nt.hip
 int gemm_nt_part_rows(int M);
 void gemm_nt_set_pipe(int p);

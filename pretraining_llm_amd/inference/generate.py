@@ -51,7 +51,7 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
         x, res = blk.forward_cached(x, res, cache, i, pos, rope)
     h, _ = model.layer_norm(x, res)
     h = h[:, -1, :]
-    return torch.nn.functional.linear(h, model.head_weight, model.head_bias).float()
+    return ops.linear(h, model.head_weight, model.head_bias).float()
 
 
 @torch.no_grad()
@@ -69,7 +69,7 @@ def forward_decode(model, tok: torch.Tensor, cache: KVCache, pos_t: torch.Tensor
     for i, blk in enumerate(model.attn_blocks):
         x, res = blk.forward_decode(x, res, cache, i, pos_t, len_t, rope)
     h, _ = model.layer_norm(x, res)
-    return torch.nn.functional.linear(h[:, -1, :], model.head_weight, model.head_bias).float()
+    return ops.linear(h[:, -1, :], model.head_weight, model.head_bias).float()
 
 
 class DecodeGraph:

@@ -195,6 +195,14 @@ def _weight_grad(dy2, x2, tgt):
 def linear(x, weight, bias=None, bias_grad_external: bool = False):
     if _hip(x) and torch.is_grad_enabled() and weight.requires_grad:
         return _LinearFn.apply(x, weight, bias, bias_grad_external and bias is not None)
+    if _hip(x) and not (torch.is_grad_enabled() and x.requires_grad):
+        # decode-sized inference projections (<= 8 token rows): weight-streaming skinny GEMM
+        # (csrc/gemv.hip) instead of the training-sized library tiles
+        K = x.shape[-1]
+        rows = x.numel() // K if K else 0
+        if 0 < rows <= 8 and K % 8 == 0 and weight.is_contiguous() and weight.data_ptr() % 16 == 0:
+            y = _ops().gemv(x.reshape(rows, K).contiguous(), weight, bias)
+            return y.view(*x.shape[:-1], weight.shape[0])
     return F.linear(x, weight, bias)
 
 

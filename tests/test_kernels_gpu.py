@@ -334,6 +334,24 @@ def test_gemm_nt_epilogues(pipe, M, N, K):
         ops.gemm_nt_set_pipe(0)
 
 
+@pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("N,K", [(777, 768), (2000, 512), (3072, 768), (768, 3072), (9000, 256), (50304, 768)])
+def test_gemv_skinny_gemm(M, N, K):
+    """Decode-sized projection kernel (csrc/gemv.hip) vs fp32 torch, with and without bias,
+    on a row-strided x view; ops.linear routes <= 8-row inference calls to it."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(M * 7 + N)
+    xb = torch.randn(M, 2 * K, device=DEV, dtype=torch.bfloat16)
+    x = xb[:, :K]
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    ref = x.float() @ w.float().t()
+    assert _rel(_ops().gemv(x, w, None), ref) < 5e-3
+    assert _rel(_ops().gemv(x, w, b), ref + b.float()) < 5e-3
+    with torch.no_grad():
+        assert _rel(ops.linear(x.reshape(1, M, K), w, b).reshape(M, N), ref + b.float()) < 5e-3
+
+
 @pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny"])
 def test_graphed_decode_matches_eager(preset):
     """generate(cuda_graph=True) (one hipGraph replay per token, device-side position and
