@@ -169,8 +169,13 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 }
 
 // ---------------------------------------------------------------- skinny GEMM (decode)
-// y[M, N] = x[M, K] w[N, K]^T (+ bias) for M <= 8 token rows
-Tensor gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias) {
+// y[M, N] = act(in[M, K] w[N, K]^T (+ bias)) for M <= 8 token rows; in = x, or (gamma given)
+// norm(x (+ res)) -- then also returns the residual stream s = x + res when res is given
+std::vector<Tensor> gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias,
+                         const std::optional<Tensor>& res, const std::optional<Tensor>& gamma,
+                         const std::optional<Tensor>& beta, double eps, int64_t rms, int64_t act,
+                         const std::optional<Tensor>& kc, const std::optional<Tensor>& vc,
+                         const std::optional<Tensor>& pos, int64_t q_cols) {
   check_bf16(x, "x");
   check_bf16(w, "w");
   TORCH_CHECK(x.dim() == 2 && w.dim() == 2 && x.size(1) == w.size(1), "gemv: x [M,K], w [N,K]");
@@ -178,17 +183,82 @@ Tensor gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias)
   TORCH_CHECK(M <= pllm::gemv_max_rows(), "gemv: at most ", pllm::gemv_max_rows(), " rows");
   TORCH_CHECK(K % 8 == 0 && x.stride(1) == 1 && w.stride(1) == 1 && x.stride(0) % 8 == 0 && w.stride(0) % 8 == 0,
               "gemv: K % 8 == 0, unit column stride, row strides % 8");
+  TORCH_CHECK(act >= 0 && act <= 2, "gemv: act 0 (none), 1 (gelu), 2 (relu)");
   check_aligned16(x, "x");
   check_aligned16(w, "w");
   if (bias) {
     check_bf16(*bias, "bias");
     TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemv: bias [N]");
   }
+  TORCH_CHECK(!res || gamma, "gemv: res requires the norm prologue (gamma)");
+  if (gamma) {
+    check_bf16(*gamma, "gamma");
+    TORCH_CHECK(gamma->numel() == K && gamma->is_contiguous(), "gemv: gamma [K]");
+    check_aligned16(*gamma, "gamma");
+    if (beta) {
+      check_bf16(*beta, "beta");
+      TORCH_CHECK(beta->numel() == K && beta->is_contiguous(), "gemv: beta [K]");
+      check_aligned16(*beta, "beta");
+    }
+  }
+  if (res) {
+    check_bf16(*res, "res");
+    TORCH_CHECK(res->dim() == 2 && res->size(0) == M && res->size(1) == K && res->stride(1) == 1 &&
+                    res->stride(0) % 8 == 0,
+                "gemv: res [M,K], unit column stride");
+    check_aligned16(*res, "res");
+  }
+  int64_t kv_cols = 0, kv_ldb = 0;
+  if (kc) {
+    TORCH_CHECK(vc && pos, "gemv: kc needs vc and pos");
+    check_bf16(*kc, "kc");
+    check_bf16(*vc, "vc");
+    TORCH_CHECK(kc->is_contiguous() && vc->is_contiguous() && kc->sizes() == vc->sizes() && kc->dim() >= 3 &&
+                    kc->size(0) == M,
+                "gemv: kc/vc contiguous [B = rows, S_max, ...] of equal shape");
+    kv_ldb = kc->stride(0);
+    kv_cols = kc->stride(1);
+    TORCH_CHECK(q_cols >= 0 && q_cols + 2 * kv_cols == N, "gemv: q_cols + 2 * kv_cols must equal N");
+    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->numel() == 1 && pos->device() == x.device(),
+                "gemv: pos int64 [1] on the device");
+    // the position itself stays on the device (hipGraph replay); the caller bounds it by S_max
+  }
   Tensor y = at::empty({M, N}, x.options());
-  if (M > 0 && N > 0)
-    pllm::gemv(x.data_ptr(), x.stride(0), w.data_ptr(), w.stride(0), opt_ptr(bias), y.data_ptr(), N, (int)M, (int)N,
-               (int)K, cur_stream());
-  return y;
+  Tensor s;
+  if (res) s = at::empty({M, K}, x.options());
+  if (M > 0 && N > 0) {
+    pllm::GemvArgs a{};
+    a.x = (const uint16_t*)x.data_ptr();
+    a.ldx = x.stride(0);
+    a.res = res ? (const uint16_t*)res->data_ptr() : nullptr;
+    a.ldr = res ? res->stride(0) : 0;
+    a.gamma = gamma ? (const uint16_t*)gamma->data_ptr() : nullptr;
+    a.beta = (gamma && beta) ? (const uint16_t*)beta->data_ptr() : nullptr;
+    a.s_out = res ? (uint16_t*)s.data_ptr() : nullptr;
+    a.lds = K;
+    a.eps = (float)eps;
+    a.rms = (int)rms;
+    a.w = (const uint16_t*)w.data_ptr();
+    a.ldw = w.stride(0);
+    a.bias = bias ? (const uint16_t*)bias->data_ptr() : nullptr;
+    a.y = (uint16_t*)y.data_ptr();
+    a.ldy = N;
+    a.N = (int)N;
+    a.K = (int)K;
+    a.Mr = (int)M;
+    a.act = (int)act;
+    a.kc = kc ? (uint16_t*)kc->data_ptr() : nullptr;
+    a.vc = kc ? (uint16_t*)vc->data_ptr() : nullptr;
+    a.pos = kc ? (const int64_t*)pos->data_ptr() : nullptr;
+    a.kv_ldb = kv_ldb;
+    a.q_cols = (int)q_cols;
+    a.kv_cols = (int)kv_cols;
+    a.kv_smax = kc ? (int)kc->size(1) : 0;
+    TORCH_CHECK(!a.kc || a.act == 0, "gemv: KV-cache append takes no activation");
+    pllm::gemv(a, cur_stream());
+  }
+  if (res) return {y, s};
+  return {y};
 }
 
 // ---------------------------------------------------------------- NT GEMM + MLP epilogues
@@ -664,7 +734,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
   m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_grad_acc=None) -> Tensor[]");
-  m.def("gemv(Tensor x, Tensor w, Tensor? bias) -> Tensor");
+  m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> Tensor[]");
   m.def("gemm_nt_set_pipe(int p) -> ()", [](int64_t p) { pllm::gemm_nt_set_pipe((int)p); });
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");

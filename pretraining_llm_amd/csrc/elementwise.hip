@@ -12,24 +12,6 @@
 
 namespace {
 
-constexpr float kGeluK = 0.7978845608028654f;  // sqrt(2/pi)
-constexpr float kGeluC = 0.044715f;
-
-PLLM_DEV float tanh_fast(float u) {
-  // tanh(u) = 1 - 2 / (exp(2u) + 1); saturates correctly for |u| large.  v_rcp_f32 instead
-  // of an IEEE division: the division's scale/fixup sequence made GELU VALU-bound
-  // (~25 VALU ops per element at 8 elements per 16-B access) instead of HBM-bound.
-  return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f);
-}
-PLLM_DEV float gelu_f(float x) {
-  const float t = tanh_fast(kGeluK * (x + kGeluC * x * x * x));
-  return 0.5f * x * (1.f + t);
-}
-PLLM_DEV float gelu_df(float x) {
-  const float x2 = x * x;
-  const float t = tanh_fast(kGeluK * (x + kGeluC * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK * (1.f + 3.f * kGeluC * x2);
-}
 PLLM_DEV float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 inline int ew_grid(size_t n_vec) {

@@ -52,16 +52,6 @@ PLLM_DEV void glds16(const void* src, unsigned lds_byte) {
                : "memory", "m0");
 }
 
-constexpr float kGeluK = 0.7978845608028654f;
-constexpr float kGeluC = 0.044715f;
-PLLM_DEV float tanh_fast(float u) { return 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * u) + 1.f); }
-PLLM_DEV float gelu_f(float x) { return 0.5f * x * (1.f + tanh_fast(kGeluK * (x + kGeluC * x * x * x))); }
-PLLM_DEV float gelu_df(float x) {
-  const float x2 = x * x;
-  const float t = tanh_fast(kGeluK * (x + kGeluC * x2 * x));
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * kGeluK * (1.f + 3.f * kGeluC * x2);
-}
-
 constexpr int BT = 256;  // output tile (M and N)
 constexpr int NT = 512;  // 8 waves
 constexpr int GM = 8;    // M-tiles per visiting group

@@ -83,17 +83,106 @@ __global__ __launch_bounds__(GV_THREADS) void gemv_kernel(const uint16_t* __rest
   }
 }
 
+PLLM_DEV float bf16_round(float v) { return bf2f(f2bf_bits(v)); }
+
+// block-wide sums of M per-thread values (all threads get the totals); `red` holds NW x M floats
+template <int M, int NW>
+PLLM_DEV void block_sum(float (&v)[M], float* red) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const float t = wave_sum(v[m]);
+    if (lane == 0) red[wave * M + m] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) t += red[i * M + m];
+    v[m] = t;
+  }
+  __syncthreads();
+}
+
 // Split-K form: workgroup = T threads over C columns; thread t owns K chunks t, t + T, ...
-template <int M, int C, int T>
-__global__ __launch_bounds__(T) void gemv_splitk_kernel(const uint16_t* __restrict__ x, int64_t ldx,
-                                                        const uint16_t* __restrict__ w, int64_t ldw,
-                                                        const uint16_t* __restrict__ bias, uint16_t* __restrict__ y,
-                                                        int64_t ldy, int N, int K, int Mr) {
+// NORM: the GEMM input is norm(x + res) (LayerNorm, or RMSNorm when a.rms), computed in the
+// workgroup itself -- each workgroup re-reads the <= 8 L2-resident input rows for the two
+// statistics passes, and workgroup 0 writes the new residual stream x + res -- so a decode
+// block runs no separate norm kernel.  Epilogue: + bias, then GELU (act 1) or ReLU (act 2).
+// With a.kc set (decode QKV projection) the K and V columns are also appended to the KV cache at
+// the device-side position *a.pos.  Roundings follow the unfused path: x + res, the normalised input and the pre-activation are
+// rounded to bf16 where the separate kernels would have stored them.
+template <int M, int C, int T, bool NORM>
+__global__ __launch_bounds__(T) void gemv_splitk_kernel(const pllm::GemvArgs a) {
   constexpr int NW = T / 64;
   __shared__ float part[NW][C * M];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n0 = blockIdx.x * C;
-  const int nch = K >> 3;
+  const int nch = a.K >> 3, Mr = a.Mr, N = a.N;
+  const uint16_t* __restrict__ x = a.x;
+  const uint16_t* __restrict__ res = a.res;
+  const uint16_t* __restrict__ w = a.w;
+  float mean[M], rstd[M];
+  if constexpr (NORM) {
+    // pass 1: mean (and the residual-stream write), pass 2: centred sum of squares
+    float sum[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) sum[m] = 0.f;
+    for (int ch = threadIdx.x; ch < nch; ch += T) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (m < Mr) {
+          float f[8];
+          unpack8(ld16(x + (int64_t)m * a.ldx + ch * 8), f);
+          if (res) {
+            float r[8];
+            unpack8(ld16(res + (int64_t)m * a.ldr + ch * 8), r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = bf16_round(f[e] + r[e]);
+            if (a.s_out && blockIdx.x == 0) st16(a.s_out + (int64_t)m * a.lds + ch * 8, pack8(f));
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) sum[m] += f[e];
+        }
+      }
+    }
+    const float invK = 1.f / (float)a.K;
+    if (!a.rms) {
+      block_sum<M, NW>(sum, &part[0][0]);
+#pragma unroll
+      for (int m = 0; m < M; ++m) mean[m] = sum[m] * invK;
+    } else {
+#pragma unroll
+      for (int m = 0; m < M; ++m) mean[m] = 0.f;
+    }
+    float sq[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) sq[m] = 0.f;
+    for (int ch = threadIdx.x; ch < nch; ch += T) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        if (m < Mr) {
+          float f[8];
+          unpack8(ld16(x + (int64_t)m * a.ldx + ch * 8), f);
+          if (res) {
+            float r[8];
+            unpack8(ld16(res + (int64_t)m * a.ldr + ch * 8), r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) f[e] = bf16_round(f[e] + r[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float d = f[e] - mean[m];
+            sq[m] += d * d;
+          }
+        }
+      }
+    }
+    block_sum<M, NW>(sq, &part[0][0]);
+#pragma unroll
+    for (int m = 0; m < M; ++m) rstd[m] = rsqrtf(sq[m] * invK + a.eps);
+  }
   float acc[C][M];
 #pragma unroll
   for (int c = 0; c < C; ++c)
@@ -102,12 +191,32 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const uint16_t* __restri
   for (int ch = threadIdx.x; ch < nch; ch += T) {
     u32x4 wr[C];
 #pragma unroll
-    for (int c = 0; c < C; ++c) wr[c] = ld16_nt(w + (int64_t)min(n0 + c, N - 1) * ldw + ch * 8);
+    for (int c = 0; c < C; ++c) wr[c] = ld16_nt(w + (int64_t)min(n0 + c, N - 1) * a.ldw + ch * 8);
+    float g[8], bt[8];
+    if constexpr (NORM) {
+      unpack8(ld16(a.gamma + ch * 8), g);
+      if (a.beta) {
+        unpack8(ld16(a.beta + ch * 8), bt);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bt[e] = 0.f;
+      }
+    }
     float xf[M][8];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       if (m < Mr) {
-        unpack8(ld16(x + (int64_t)m * ldx + ch * 8), xf[m]);
+        unpack8(ld16(x + (int64_t)m * a.ldx + ch * 8), xf[m]);
+        if constexpr (NORM) {
+          if (res) {
+            float r[8];
+            unpack8(ld16(res + (int64_t)m * a.ldr + ch * 8), r);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xf[m][e] = bf16_round(xf[m][e] + r[e]);
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) xf[m][e] = bf16_round((xf[m][e] - mean[m]) * rstd[m] * g[e] + bt[e]);
+        }
       } else {
 #pragma unroll
         for (int e = 0; e < 8; ++e) xf[m][e] = 0.f;
@@ -135,23 +244,30 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const uint16_t* __restri
   if (t < C * M) {
     const int c = t / M, m = t % M, n = n0 + c;
     if (n < N && m < Mr) {
-      float v = bias ? bf2f(bias[n]) : 0.f;
+      float v = a.bias ? bf2f(a.bias[n]) : 0.f;
 #pragma unroll
       for (int i = 0; i < NW; ++i) v += part[i][t];
-      y[(int64_t)m * ldy + n] = f2bf_bits(v);
+      if (a.act == 1) v = gelu_f(bf16_round(v));
+      else if (a.act == 2) v = fmaxf(v, 0.f);
+      const uint16_t o = f2bf_bits(v);
+      a.y[(int64_t)m * a.ldy + n] = o;
+      const int64_t p = a.kc ? *a.pos : -1;
+      if (a.kc && n >= a.q_cols && p >= 0 && p < a.kv_smax) {  // KV-cache append (no copy kernels)
+        const int j = n - a.q_cols;
+        const int64_t at = (int64_t)m * a.kv_ldb + p * a.kv_cols;
+        if (j < a.kv_cols) a.kc[at + j] = o;
+        else a.vc[at + j - a.kv_cols] = o;
+      }
     }
   }
 }
 
-template <int M>
-void launch_splitk(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy,
-                   int Mr, int N, int K, hipStream_t st) {
-  const int nch = K >> 3;
-  const int C = N <= 1024 ? 1 : N <= 2048 ? 2 : 4;  // >= 512 workgroups for N >= 512
-  const dim3 grid((N + C - 1) / C);
-#define LS(CC, TT)                                                                                             \
-  hipLaunchKernelGGL((gemv_splitk_kernel<M, CC, TT>), grid, dim3(TT), 0, st, (const uint16_t*)x, ldx,          \
-                     (const uint16_t*)w, ldw, (const uint16_t*)bias, (uint16_t*)y, ldy, N, K, Mr)
+template <int M, bool NORM>
+void launch_splitk(const pllm::GemvArgs& a, hipStream_t st) {
+  const int nch = a.K >> 3;
+  const int C = a.N <= 1024 ? 1 : a.N <= 2048 ? 2 : 4;  // >= 512 workgroups for N >= 512
+  const dim3 grid((a.N + C - 1) / C);
+#define LS(CC, TT) hipLaunchKernelGGL((gemv_splitk_kernel<M, CC, TT, NORM>), grid, dim3(TT), 0, st, a)
 #define LC(CC)                     \
   if (nch > 128) LS(CC, 256);      \
   else if (nch > 64) LS(CC, 128);  \
@@ -167,32 +283,37 @@ void launch_splitk(const void* x, int64_t ldx, const void* w, int64_t ldw, const
 #undef LS
 }
 
+template <bool NORM>
+void dispatch_splitk(const pllm::GemvArgs& a, hipStream_t st) {
+  if (a.Mr <= 1) launch_splitk<1, NORM>(a, st);
+  else if (a.Mr <= 2) launch_splitk<2, NORM>(a, st);
+  else if (a.Mr <= 4) launch_splitk<4, NORM>(a, st);
+  else launch_splitk<8, NORM>(a, st);
+}
+
 }  // namespace
 
 namespace pllm {
 
 int gemv_max_rows() { return 8; }
 
-void gemv(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy, int M,
-          int N, int K, hipStream_t st) {
-  if (N < 8192) {
-    if (M <= 1) launch_splitk<1>(x, ldx, w, ldw, bias, y, ldy, M, N, K, st);
-    else if (M <= 2) launch_splitk<2>(x, ldx, w, ldw, bias, y, ldy, M, N, K, st);
-    else if (M <= 4) launch_splitk<4>(x, ldx, w, ldw, bias, y, ldy, M, N, K, st);
-    else launch_splitk<8>(x, ldx, w, ldw, bias, y, ldy, M, N, K, st);
-    PLLM_CHECK_LAUNCH();
-    return;
-  }
-  const int cols_per_block = GV_COLS * (GV_THREADS / 64);
-  const dim3 grid((N + cols_per_block - 1) / cols_per_block);
+void gemv(const GemvArgs& a, hipStream_t st) {
+  if (a.gamma) {
+    dispatch_splitk<true>(a, st);
+  } else if (a.N < 8192 || a.act != 0 || a.kc) {
+    dispatch_splitk<false>(a, st);
+  } else {
+    const int cols_per_block = GV_COLS * (GV_THREADS / 64);
+    const dim3 grid((a.N + cols_per_block - 1) / cols_per_block);
 #define L(MM)                                                                                                  \
-  hipLaunchKernelGGL((gemv_kernel<MM>), grid, dim3(GV_THREADS), 0, st, (const uint16_t*)x, ldx,                 \
-                     (const uint16_t*)w, ldw, (const uint16_t*)bias, (uint16_t*)y, ldy, N, K, M)
-  if (M <= 1) L(1);
-  else if (M <= 2) L(2);
-  else if (M <= 4) L(4);
-  else L(8);
+  hipLaunchKernelGGL((gemv_kernel<MM>), grid, dim3(GV_THREADS), 0, st, a.x, a.ldx, a.w, a.ldw, a.bias, a.y,     \
+                     a.ldy, a.N, a.K, a.Mr)
+    if (a.Mr <= 1) L(1);
+    else if (a.Mr <= 2) L(2);
+    else if (a.Mr <= 4) L(4);
+    else L(8);
 #undef L
+  }
   PLLM_CHECK_LAUNCH();
 }
 

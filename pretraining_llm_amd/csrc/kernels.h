@@ -111,10 +111,36 @@ void transpose_batch(const int64_t* desc, int n, int total_tiles, hipStream_t st
 void sample_tokens(const void* logits, bool bf16_in, int64_t ld, int B, int V, float temperature, uint64_t seed,
                    int64_t* out, hipStream_t st);
 
-// gemv.hip: y[M, N] = x[M, K] W[N, K]^T (+ bias) for M <= gemv_max_rows() (decode projections)
+// gemv.hip: y[M, N] = act(in[M, K] W[N, K]^T + bias) for M <= gemv_max_rows() (decode projections),
+// in = x, or norm(x + res) with the residual stream x + res written to s_out when gamma is set
+struct GemvArgs {
+  const uint16_t* x;
+  int64_t ldx;
+  const uint16_t* res;    // nullable (NORM only)
+  int64_t ldr;
+  const uint16_t* gamma;  // nullable: no norm prologue
+  const uint16_t* beta;   // nullable: RMSNorm / no shift
+  uint16_t* s_out;        // nullable: x + res
+  int64_t lds;
+  float eps;
+  int rms;
+  const uint16_t* w;
+  int64_t ldw;
+  const uint16_t* bias;   // nullable
+  uint16_t* y;
+  int64_t ldy;
+  int N, K, Mr;
+  int act;  // 0 none, 1 GELU (tanh), 2 ReLU
+  // decode KV-cache append (nullable kc): output columns [q_cols, q_cols + kv_cols) of row m
+  // also go to kc[m, *pos, :], the next kv_cols to vc[m, *pos, :] (caches [B, S_max, kv_cols])
+  uint16_t* kc;
+  uint16_t* vc;
+  const int64_t* pos;
+  int64_t kv_ldb;
+  int q_cols, kv_cols, kv_smax;  // positions outside [0, kv_smax) are dropped, never written
+};
 int gemv_max_rows();
-void gemv(const void* x, int64_t ldx, const void* w, int64_t ldw, const void* bias, void* y, int64_t ldy, int M,
-          int N, int K, hipStream_t st);
+void gemv(const GemvArgs& a, hipStream_t st);
 
 // gemm_nt.hip
 int gemm_nt_part_rows(int M);

@@ -46,14 +46,28 @@ __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logi
   const uint64_t rkey = mix64(seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(row + 1)));
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int i = threadIdx.x; i < V; i += blockDim.x) {
-    float s = load_logit<T>(x, i);
-    if (!greedy) {
-      const uint64_t h = mix64(rkey + (uint64_t)i);
-      const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
-      s = s * inv_temp - __logf(-__logf(u));
+  // SU independent loads in flight per thread before any compare: a plain strided loop kept
+  // one load outstanding at a time (21.5 us for one 50,304-logit row,
+  // profiles/r1_decode_gemv_kernel_stats.md)
+  constexpr int SU = 16;
+  for (int i0 = threadIdx.x; i0 < V; i0 += blockDim.x * SU) {
+    float sv_[SU];
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int i = i0 + u * blockDim.x;
+      sv_[u] = i < V ? load_logit<T>(x, i) : NAN;
     }
-    if (s == s) better(best, bi, s, i);  // NaN logits are never drawn
+#pragma unroll
+    for (int u = 0; u < SU; ++u) {
+      const int i = i0 + u * blockDim.x;
+      float s = sv_[u];
+      if (!greedy) {
+        const uint64_t h = mix64(rkey + (uint64_t)i);
+        const float uu = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);  // (0, 1)
+        s = s * inv_temp - __logf(-__logf(uu));
+      }
+      if (s == s) better(best, bi, s, i);  // NaN logits (and the tail padding) are never drawn
+    }
   }
   // wave then block argmax
 #pragma unroll

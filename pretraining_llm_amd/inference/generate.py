@@ -49,9 +49,10 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
     res = None
     for i, blk in enumerate(model.attn_blocks):
         x, res = blk.forward_cached(x, res, cache, i, pos, rope)
-    h, _ = model.layer_norm(x, res)
-    h = h[:, -1, :]
-    return ops.linear(h, model.head_weight, model.head_bias).float()
+    # only the last position's logits are needed: norm + head on that row alone
+    logits, _ = model.layer_norm.linear(x[:, -1:], res[:, -1:] if res is not None else None,
+                                        model.head_weight, model.head_bias)
+    return logits[:, -1, :].float()
 
 
 @torch.no_grad()
@@ -68,8 +69,8 @@ def forward_decode(model, tok: torch.Tensor, cache: KVCache, pos_t: torch.Tensor
     res = None
     for i, blk in enumerate(model.attn_blocks):
         x, res = blk.forward_decode(x, res, cache, i, pos_t, len_t, rope)
-    h, _ = model.layer_norm(x, res)
-    return ops.linear(h[:, -1, :], model.head_weight, model.head_bias).float()
+    logits, _ = model.layer_norm.linear(x, res, model.head_weight, model.head_bias)
+    return logits[:, -1, :].float()
 
 
 class DecodeGraph:

@@ -46,6 +46,11 @@ class Norm(nn.Module):
             return ops.rms_norm(x, self.weight, self.eps, residual, x_bias=x_bias)
         return ops.layer_norm(x, self.weight, self.bias, self.eps, residual, x_bias=x_bias)
 
+    def linear(self, x, residual, weight, bias=None, act=None, kv=None):
+        """Inference: (act(norm(x + residual) @ weight^T + bias), x + residual) -- one fused
+        skinny-GEMM launch for decode-sized inputs (ops.norm_linear, csrc/gemv.hip)."""
+        return ops.norm_linear(x, residual, self.weight, self.bias, self.eps, self.rms, weight, bias, act, kv)
+
 
 class Attention(nn.Module):
     def __init__(self, cfg: ModelConfig, layer_idx: int = 0):
@@ -66,10 +71,11 @@ class Attention(nn.Module):
         return y
 
     # --- KV-cache decode -------------------------------------------------
-    def forward_cached(self, x, cache, layer_idx, pos, rope=None):
-        B, T, _ = x.shape
+    def forward_cached(self, x, cache, layer_idx, pos, rope=None, qkv=None):
+        if qkv is None:
+            qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+        B, T, _ = qkv.shape
         H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
-        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         q = qkv[..., : H * D].view(B, T, H, D)
         k = qkv[..., H * D:(H + Hkv) * D].view(B, T, Hkv, D)
         v = qkv[..., (H + Hkv) * D:].view(B, T, Hkv, D)
@@ -84,13 +90,16 @@ class Attention(nn.Module):
             y = ops.linear(y, self.proj.weight, self.proj.bias)
         return y
 
-    def forward_decode(self, x, cache, layer_idx, pos_t, len_t, rope=None):
+    def forward_decode(self, x, cache, layer_idx, pos_t, len_t, rope=None, qkv=None, kv_written=False):
         """One-token step with the position on the DEVICE (``pos_t`` int64 [1], ``len_t`` =
         pos+1 as int32 [1]): no host scalar reaches a kernel argument, so the step can be
-        captured once in a hipGraph and replayed at every position (inference/generate.py)."""
-        B = x.shape[0]
+        captured once in a hipGraph and replayed at every position (inference/generate.py).
+        ``qkv``: the already-projected input (the block fuses ln1 into the projection);
+        ``kv_written``: that projection already appended k/v to the cache (no RoPE only)."""
+        if qkv is None:
+            qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+        B = qkv.shape[0]
         H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
-        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         q = qkv[..., : H * D].view(B, 1, H, D)
         k = qkv[..., H * D:(H + Hkv) * D].view(B, 1, Hkv, D)
         v = qkv[..., (H + Hkv) * D:].view(B, 1, Hkv, D)
@@ -98,8 +107,9 @@ class Attention(nn.Module):
             cos, sin = rope[0].index_select(0, pos_t), rope[1].index_select(0, pos_t)
             q = ops.apply_rope(q, cos, sin, 0)
             k = ops.apply_rope(k, cos, sin, 0)
-        cache.k[layer_idx].index_copy_(1, pos_t, k)
-        cache.v[layer_idx].index_copy_(1, pos_t, v)
+        if not kv_written:
+            cache.k[layer_idx].index_copy_(1, pos_t, k)
+            cache.v[layer_idx].index_copy_(1, pos_t, v)
         y = ops.attention_decode(q.contiguous(), cache.k[layer_idx], cache.v[layer_idx], seqlen=len_t)
         y = y.reshape(B, 1, H * D)
         if self.proj is not None:
@@ -170,17 +180,32 @@ class Block(nn.Module):
             return self.mlp.proj.bias
         return None
 
+    # Inference steps: each norm runs as the prologue of the projection after it and the MLP
+    # activation as the epilogue of the up-projection (Norm.linear -> ops.norm_linear): at
+    # decode sizes a block is 4 skinny-GEMM launches + attention; prefill falls back to the
+    # unfused kernels.
+    def _mlp_infer(self, a, res):
+        kind = self.mlp.kind
+        act = None if kind == "swiglu" else ("gelu" if kind == "gelu" else "relu")
+        h, res2 = self.ln2.linear(a, res, self.mlp.hidden.weight, self.mlp.hidden.bias, act=act)
+        if kind == "swiglu":
+            h = ops.swiglu(h)
+        return ops.linear(h, self.mlp.proj.weight, self.mlp.proj.bias), res2
+
     def forward_cached(self, x, residual, cache, layer_idx, pos, rope=None):
-        h, res = self.ln1(x, residual)
-        a = self.attn.forward_cached(h, cache, layer_idx, pos, rope)
-        h2, res2 = self.ln2(a, res)
-        return self.mlp(h2), res2
+        qkv, res = self.ln1.linear(x, residual, self.attn.qkv.weight, self.attn.qkv.bias)
+        a = self.attn.forward_cached(None, cache, layer_idx, pos, rope, qkv=qkv)
+        return self._mlp_infer(a, res)
 
     def forward_decode(self, x, residual, cache, layer_idx, pos_t, len_t, rope=None):
-        h, res = self.ln1(x, residual)
-        a = self.attn.forward_decode(h, cache, layer_idx, pos_t, len_t, rope)
-        h2, res2 = self.ln2(a, res)
-        return self.mlp(h2), res2
+        # without RoPE the QKV projection's epilogue also appends k/v to the cache
+        kv = None
+        if rope is None:
+            kv = (cache.k[layer_idx], cache.v[layer_idx], pos_t, self.attn.n_head * self.attn.head_dim)
+        qkv, res = self.ln1.linear(x, residual, self.attn.qkv.weight, self.attn.qkv.bias, kv=kv)
+        a = self.attn.forward_decode(None, cache, layer_idx, pos_t, len_t, rope, qkv=qkv,
+                                     kv_written=kv is not None)
+        return self._mlp_infer(a, res)
 
     def forward_embedding(self, x, residual=None, rope=None):
         h, res = self.ln1(x, residual)

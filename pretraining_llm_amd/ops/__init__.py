@@ -201,9 +201,63 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
         K = x.shape[-1]
         rows = x.numel() // K if K else 0
         if 0 < rows <= 8 and K % 8 == 0 and weight.is_contiguous() and weight.data_ptr() % 16 == 0:
-            y = _ops().gemv(x.reshape(rows, K).contiguous(), weight, bias)
+            y = _ops().gemv(x.reshape(rows, K).contiguous(), weight, bias)[0]
             return y.view(*x.shape[:-1], weight.shape[0])
     return F.linear(x, weight, bias)
+
+
+_ACT_IDS = {None: 0, "gelu": 1, "relu": 2}
+
+
+def _gemv_ok(x, weight):
+    K = x.shape[-1]
+    rows = x.numel() // K if K else 0
+    return (_hip(x) and not torch.is_grad_enabled() and 0 < rows <= 8 and K % 8 == 0
+            and weight.is_contiguous() and weight.data_ptr() % 16 == 0)
+
+
+def norm_linear(x, residual, norm_weight, norm_bias, eps: float, rms: bool, weight, bias=None,
+                act: Optional[str] = None, kv=None):
+    """Inference-only ``(act(norm(x + residual) @ weight^T + bias), x + residual)``.
+
+    For decode-sized inputs (<= 8 token rows) on the HIP path this is ONE launch of the
+    skinny-GEMM kernel with the norm as its prologue and the activation as its epilogue
+    (csrc/gemv.hip): a decode block then runs no separate norm or activation kernels.
+    Otherwise it is the unfused norm -> linear -> activation sequence.
+
+    ``kv = (k_cache, v_cache, pos_t, q_cols)`` (decode QKV projection, caches [B, S_max, Hkv, D],
+    ``pos_t`` int64 [1] on the device): output columns q_cols.. are also appended to the caches
+    at position ``pos_t`` -- by the kernel's epilogue on the fused path."""
+    if _gemv_ok(x, weight) and norm_weight.dtype == x.dtype:
+        K = x.shape[-1]
+        rows = x.numel() // K
+        x2 = x.reshape(rows, K).contiguous()
+        r2 = residual.reshape(rows, K).contiguous() if residual is not None else None
+        kc = vc = pos = None
+        q_cols = 0
+        if kv is not None:
+            kc, vc, pos, q_cols = kv
+        out = _ops().gemv(x2, weight, bias, r2, norm_weight, None if rms else norm_bias, eps, int(rms),
+                          _ACT_IDS[act], kc, vc, pos, q_cols)
+        y = out[0].view(*x.shape[:-1], weight.shape[0])
+        s = out[1].view(x.shape) if residual is not None else x
+        return y, s
+    if rms:
+        h, s = rms_norm(x, norm_weight, eps, residual)
+    else:
+        h, s = layer_norm(x, norm_weight, norm_bias, eps, residual)
+    y = linear(h, weight, bias)
+    if act == "gelu":
+        y = gelu(y)
+    elif act == "relu":
+        y = relu(y)
+    if kv is not None:
+        kc, vc, pos, q_cols = kv
+        B, kvc = kc.shape[0], kc[0, 0].numel()
+        y2 = y.reshape(B, -1)
+        kc.index_copy_(1, pos, y2[:, q_cols:q_cols + kvc].reshape(B, 1, *kc.shape[2:]))
+        vc.index_copy_(1, pos, y2[:, q_cols + kvc:].reshape(B, 1, *vc.shape[2:]))
+    return y, s
 
 
 # ---------------------------------------------------------------------------

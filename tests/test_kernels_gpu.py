@@ -346,10 +346,86 @@ def test_gemv_skinny_gemm(M, N, K):
     w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
     b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
     ref = x.float() @ w.float().t()
-    assert _rel(_ops().gemv(x, w, None), ref) < 5e-3
-    assert _rel(_ops().gemv(x, w, b), ref + b.float()) < 5e-3
+    assert _rel(_ops().gemv(x, w, None)[0], ref) < 5e-3
+    assert _rel(_ops().gemv(x, w, b)[0], ref + b.float()) < 5e-3
     with torch.no_grad():
         assert _rel(ops.linear(x.reshape(1, M, K), w, b).reshape(M, N), ref + b.float()) < 5e-3
+
+
+@pytest.mark.parametrize("M", [1, 3, 8])
+@pytest.mark.parametrize("rms", [0, 1])
+@pytest.mark.parametrize("with_res", [False, True])
+@pytest.mark.parametrize("act", [0, 1, 2])
+@pytest.mark.parametrize("N,K", [(2304, 768), (9000, 512)])
+def test_gemv_norm_prologue_act_epilogue(M, rms, with_res, act, N, K):
+    """Decode fusion (csrc/gemv.hip): act(norm(x + res) W^T + b) and the residual stream x + res
+    from one launch vs fp32 torch (LayerNorm / RMSNorm, GELU-tanh / ReLU)."""
+    torch.manual_seed(M + 10 * rms + 100 * act + N)
+    x = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) * 2 + 0.5
+    r = torch.randn(M, K, device=DEV, dtype=torch.bfloat16) if with_res else None
+    g = (1 + 0.1 * torch.randn(K, device=DEV)).bfloat16()
+    be = None if rms else (0.1 * torch.randn(K, device=DEV)).bfloat16()
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
+    b = torch.randn(N, device=DEV, dtype=torch.bfloat16)
+    out = _ops().gemv(x, w, b, r, g, be, 1e-5, rms, act)
+    s = x.float() + r.float() if with_res else x.float()
+    if with_res:
+        assert len(out) == 2 and _rel(out[1], s) < 5e-3
+    if rms:
+        h = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + 1e-5) * g.float()
+    else:
+        h = torch.nn.functional.layer_norm(s, (K,), g.float(), be.float(), 1e-5)
+    ref = h @ w.float().t() + b.float()
+    if act == 1:
+        ref = torch.nn.functional.gelu(ref, approximate="tanh")
+    elif act == 2:
+        ref = torch.relu(ref)
+    assert _rel(out[0], ref) < 1e-2
+
+
+def test_gemv_kv_cache_append():
+    """QKV decode projection appends its K/V columns to the caches at the device position;
+    other cache rows stay untouched and an out-of-range position writes nothing."""
+    torch.manual_seed(3)
+    B, S, Hkv, D, H, K = 3, 16, 2, 64, 4, 256
+    N = (H + 2 * Hkv) * D
+    x = torch.randn(B, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
+    g = torch.ones(K, device=DEV, dtype=torch.bfloat16)
+    kc = torch.zeros(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    pos = torch.tensor([5], device=DEV)
+    y = _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, pos, H * D)[0]
+    assert torch.equal(kc[:, 5].reshape(B, -1), y[:, H * D:(H + Hkv) * D])
+    assert torch.equal(vc[:, 5].reshape(B, -1), y[:, (H + Hkv) * D:])
+    kc[:, 5] = 0
+    vc[:, 5] = 0
+    assert not kc.any() and not vc.any()
+    _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, torch.tensor([S], device=DEV), H * D)
+    torch.cuda.synchronize()
+    assert not kc.any() and not vc.any()
+
+
+@pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny", "ref-small"])
+def test_fused_decode_step_matches_full_forward(preset):
+    """KV-cache decode step (fused norm->projection->activation skinny GEMMs) == the last-position
+    logits of a full, uncached training-path forward."""
+    from pretraining_llm_amd.inference.generate import KVCache, forward_cached, forward_decode
+    from pretraining_llm_amd.models import GPT, get_preset
+    torch.manual_seed(5)
+    cfg = get_preset(preset).replace(vocab_size=512, context_length=64)
+    if preset == "ref-small":  # reference architecture (ReLU, no W_o, biased untied head), tiny dims
+        cfg = cfg.replace(n_embed=128, n_head=4, n_kv_head=4, n_blocks=2, ffn_hidden=512)
+    m = GPT(cfg).to(DEV, torch.bfloat16).eval()
+    idx = torch.randint(0, 512, (2, 20), device=DEV)
+    with torch.no_grad():
+        full, _ = m(idx)
+        cache = KVCache(cfg.n_blocks, 2, 64, cfg.n_kv_head, cfg.head_dim, torch.bfloat16, idx.device)
+        pre = forward_cached(m, idx[:, :-1], cache, 0)
+        pos_t = torch.tensor([19], device=DEV)
+        dec = forward_decode(m, idx[:, -1:], cache, pos_t, (pos_t + 1).int())
+    assert _rel(pre, full[:, -2].float()) < 3e-2
+    assert _rel(dec, full[:, -1].float()) < 3e-2
 
 
 @pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny"])
@@ -385,6 +461,29 @@ def test_model_hip_matches_reference_path():
     assert abs(l1.item() - l2.item()) < 2e-2
     for n, p in m.named_parameters():
         assert _rel(g1[n], p.grad) < 6e-2, n
+
+
+def test_gemv_kv_cache_append():
+    """QKV decode projection appends its K/V columns to the caches at the device position;
+    other cache rows stay untouched and an out-of-range position writes nothing."""
+    torch.manual_seed(3)
+    B, S, Hkv, D, H, K = 3, 16, 2, 64, 4, 256
+    N = (H + 2 * Hkv) * D
+    x = torch.randn(B, K, device=DEV, dtype=torch.bfloat16)
+    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
+    g = torch.ones(K, device=DEV, dtype=torch.bfloat16)
+    kc = torch.zeros(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    vc = torch.zeros_like(kc)
+    pos = torch.tensor([5], device=DEV)
+    y = _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, pos, H * D)[0]
+    assert torch.equal(kc[:, 5].reshape(B, -1), y[:, H * D:(H + Hkv) * D])
+    assert torch.equal(vc[:, 5].reshape(B, -1), y[:, (H + Hkv) * D:])
+    kc[:, 5] = 0
+    vc[:, 5] = 0
+    assert not kc.any() and not vc.any()
+    _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, torch.tensor([S], device=DEV), H * D)
+    torch.cuda.synchronize()
+    assert not kc.any() and not vc.any()
 
 
 @pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny", "ref-small"])
