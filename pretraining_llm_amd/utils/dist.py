@@ -37,8 +37,14 @@ def init_distributed(backend: str = "auto", device: str = "auto", timeout_s: int
     world = int(os.environ.get("WORLD_SIZE", 1))
     if device == "auto":
         device = "cuda" if torch.cuda.is_available() else "cpu"
+    # Rehearsal switches for a multi-rank launch on a ONE-GPU box (functional only, never a
+    # measurement): PLLM_DIST_BACKEND=gloo overrides the backend, PLLM_DIST_ONE_DEVICE=1 puts
+    # every local rank on device 0 (RCCL itself refuses two ranks on one GPU).
+    one_device = os.environ.get("PLLM_DIST_ONE_DEVICE", "0") == "1"
+    backend = os.environ.get("PLLM_DIST_BACKEND", backend)
     if device.startswith("cuda"):
-        dev = torch.device("cuda", local_rank if env_dist else (torch.device(device).index or 0))
+        idx = 0 if one_device else local_rank if env_dist else (torch.device(device).index or 0)
+        dev = torch.device("cuda", idx)
         torch.cuda.set_device(dev)
     else:
         dev = torch.device("cpu")
