@@ -107,8 +107,8 @@ PLLM_DEV void block_sum(float (&v)[M], float* red) {
 
 // Split-K form: workgroup = T threads over C columns; thread t owns K chunks t, t + T, ...
 // NORM: the GEMM input is norm(x + res) (LayerNorm, or RMSNorm when a.rms), computed in the
-// workgroup itself -- each workgroup re-reads the <= 8 L2-resident input rows for the two
-// statistics passes, and workgroup 0 writes the new residual stream x + res -- so a decode
+// workgroup itself -- each workgroup re-reads the <= 8 L2-resident input rows for one
+// statistics pass, and workgroup 0 writes the new residual stream x + res -- so a decode
 // block runs no separate norm kernel.  Epilogue: + bias, then GELU (act 1) or ReLU (act 2).
 // With a.kc set (decode QKV projection) the K and V columns are also appended to the KV cache at
 // the device-side position *a.pos.  Roundings follow the unfused path: x + res, the normalised input and the pre-activation are
@@ -124,11 +124,21 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const pllm::GemvArgs a) 
   const uint16_t* __restrict__ res = a.res;
   const uint16_t* __restrict__ w = a.w;
   float mean[M], rstd[M];
-  if constexpr (NORM) {
-    // pass 1: mean (and the residual-stream write), pass 2: centred sum of squares
-    float sum[M];
+  // the first weight chunks are requested before the norm statistics so their HBM latency
+  // overlaps the statistics pass and its block reduction
+  u32x4 wpre[C];
+  if (threadIdx.x < nch) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) sum[m] = 0.f;
+    for (int c = 0; c < C; ++c) wpre[c] = ld16_nt(w + (int64_t)min(n0 + c, N - 1) * a.ldw + threadIdx.x * 8);
+  }
+  if constexpr (NORM) {
+    // one statistics pass (sums of s and s^2 in fp32; var = E[s^2] - E[s]^2 -- a shift by the
+    // row's first element cost a dependent load round trip, +1 us per launch); workgroup 0 also
+    // writes the residual stream s = x + res
+    __shared__ float red[NW * 2 * M];
+    float st[2 * M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) st[m] = st[M + m] = 0.f;
     for (int ch = threadIdx.x; ch < nch; ch += T) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
@@ -143,45 +153,20 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const pllm::GemvArgs a) 
             if (a.s_out && blockIdx.x == 0) st16(a.s_out + (int64_t)m * a.lds + ch * 8, pack8(f));
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) sum[m] += f[e];
-        }
-      }
-    }
-    const float invK = 1.f / (float)a.K;
-    if (!a.rms) {
-      block_sum<M, NW>(sum, &part[0][0]);
-#pragma unroll
-      for (int m = 0; m < M; ++m) mean[m] = sum[m] * invK;
-    } else {
-#pragma unroll
-      for (int m = 0; m < M; ++m) mean[m] = 0.f;
-    }
-    float sq[M];
-#pragma unroll
-    for (int m = 0; m < M; ++m) sq[m] = 0.f;
-    for (int ch = threadIdx.x; ch < nch; ch += T) {
-#pragma unroll
-      for (int m = 0; m < M; ++m) {
-        if (m < Mr) {
-          float f[8];
-          unpack8(ld16(x + (int64_t)m * a.ldx + ch * 8), f);
-          if (res) {
-            float r[8];
-            unpack8(ld16(res + (int64_t)m * a.ldr + ch * 8), r);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) f[e] = bf16_round(f[e] + r[e]);
-          }
-#pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const float d = f[e] - mean[m];
-            sq[m] += d * d;
+            st[m] += f[e];
+            st[M + m] += f[e] * f[e];
           }
         }
       }
     }
-    block_sum<M, NW>(sq, &part[0][0]);
+    block_sum<2 * M, NW>(st, red);
+    const float invK = 1.f / (float)a.K;
 #pragma unroll
-    for (int m = 0; m < M; ++m) rstd[m] = rsqrtf(sq[m] * invK + a.eps);
+    for (int m = 0; m < M; ++m) {
+      mean[m] = a.rms ? 0.f : st[m] * invK;
+      rstd[m] = rsqrtf(fmaxf(st[M + m] * invK - mean[m] * mean[m], 0.f) + a.eps);
+    }
   }
   float acc[C][M];
 #pragma unroll
@@ -190,8 +175,13 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const pllm::GemvArgs a) 
     for (int m = 0; m < M; ++m) acc[c][m] = 0.f;
   for (int ch = threadIdx.x; ch < nch; ch += T) {
     u32x4 wr[C];
+    if (ch == (int)threadIdx.x) {
 #pragma unroll
-    for (int c = 0; c < C; ++c) wr[c] = ld16_nt(w + (int64_t)min(n0 + c, N - 1) * a.ldw + ch * 8);
+      for (int c = 0; c < C; ++c) wr[c] = wpre[c];
+    } else {
+#pragma unroll
+      for (int c = 0; c < C; ++c) wr[c] = ld16_nt(w + (int64_t)min(n0 + c, N - 1) * a.ldw + ch * 8);
+    }
     float g[8], bt[8];
     if constexpr (NORM) {
       unpack8(ld16(a.gamma + ch * 8), g);
