@@ -45,8 +45,9 @@ def parse(argv=None):
     ap.add_argument("--batch", type=int, default=int(os.environ.get("PLLM_BENCH_BATCH", "64")),
                     help="micro-batch (sequences) per GPU")
     ap.add_argument("--seq", type=int, default=None, help="sequence length (default: the model's context length)")
-    ap.add_argument("--act-ckpt", default=None, choices=["0", "1", "auto"],
-                    help="activation checkpointing on (1) / off (0) / by HBM budget (auto); default: the preset's")
+    ap.add_argument("--act-ckpt", default=None,
+                    help="activation checkpointing on (1) / off (0) / a fraction of the blocks (e.g. 0.5) / "
+                         "by HBM budget (auto); default: the preset's")
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
     ap.add_argument("--bucket-mb", type=float, default=64.0)
     ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
@@ -90,7 +91,8 @@ def main(argv=None):
     if args.seq != mcfg.context_length:
         mcfg = mcfg.replace(context_length=max(args.seq, mcfg.context_length))
     if args.act_ckpt is not None:
-        mcfg = mcfg.replace(activation_checkpointing="auto" if args.act_ckpt == "auto" else args.act_ckpt == "1")
+        ac = args.act_ckpt
+        mcfg = mcfg.replace(activation_checkpointing=ac if ac == "auto" else ac == "1" if ac in ("0", "1") else float(ac))
     model = GPT(mcfg).to(device=dev, dtype=torch.bfloat16)
     okw = dict(lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
                max_grad_norm=args.grad_clip)
@@ -170,7 +172,8 @@ def main(argv=None):
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
                        "parallelism": f"dp{world}" + ("-zero1" if args.zero else ""), "micro_batch_per_gpu": B, "backend": args.backend,
                        "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph),
-                       "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev)))},
+                       "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev))),
+                       "checkpointed_blocks": int(model.checkpointed_blocks(torch.empty(B, T, device=dev)))},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),
             "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),
             "final_loss": round(final_loss, 4),

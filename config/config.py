@@ -103,5 +103,5 @@ PRESET_RUNS = {
                        warmup_frac=0.02),
     'gpt2-medium-4k': dict(model_preset='gpt2-medium', t_batch_size=8, t_lr=3e-4, weight_decay=0.1,
                            weight_decay_all=False, betas=(0.9, 0.95), max_grad_norm=1.0,
-                           activation_checkpointing=True),
+                           activation_checkpointing='auto'),
 }

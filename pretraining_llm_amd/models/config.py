@@ -42,8 +42,8 @@ class ModelConfig:
     rope_theta: float = 10000.0
     init: str = "gpt2"                       # gpt2 | torch_default
     init_std: float = 0.02
-    # True / False, or "auto": checkpoint only when the estimated activation memory of a
-    # step would not fit comfortably in the GPU's free HBM (GPT.use_checkpointing)
+    # True / False, a float fraction of the blocks, or "auto": checkpoint only as many blocks as
+    # it takes for a step's activations to fit comfortably in the free HBM (GPT.checkpointed_blocks)
     activation_checkpointing: object = False
     dtype: str = "bfloat16"                  # compute/parameter dtype for training
 
@@ -162,8 +162,9 @@ PRESETS = {
     # BASELINE configs 2/3: headline
     "gpt2-small": lambda: _gpt2(vocab_size=50304, context_length=1024, n_embed=768, n_head=12, n_blocks=12),
     # BASELINE config 5: long context
+    # (activation checkpointing sized to the HBM: only as many blocks as needed, GPT.checkpointed_blocks)
     "gpt2-medium": lambda: _gpt2(vocab_size=50304, context_length=4096, n_embed=1024, n_head=16, n_blocks=24,
-                                 activation_checkpointing=True),
+                                 activation_checkpointing="auto"),
     # BASELINE config 4
     "llama-1.3b": lambda: _llama(vocab_size=50304, context_length=2048, n_embed=2048, n_head=16, n_blocks=24,
                                  ffn_hidden=5504),

@@ -283,20 +283,46 @@ class GPT(nn.Module):
         cfg = self.config
         return 2 * (6 * cfg.n_embed + 2 * cfg.ffn_hidden) * tokens * cfg.n_blocks
 
-    def use_checkpointing(self, idx) -> bool:
-        """``activation_checkpointing="auto"``: recompute each block in backward only when the
-        activations would take more than half of the GPU's currently free HBM.  On a 288 GB
+    def checkpointed_blocks(self, idx) -> int:
+        """How many of the first blocks recompute their forward in backward.
+
+        ``activation_checkpointing`` is True (all), False (none), a float fraction of the blocks,
+        or ``"auto"``: checkpoint only as many blocks as it takes for the kept activations to fit
+        in half of the GPU's currently free HBM.  A checkpointed block keeps just its two
+        [tokens, C] inputs (x, residual) instead of its ``activation_bytes`` share.  On a 288 GB
         MI355X that keeps GPT-2 medium at 8 x 4096 tokens (23 GB of activations) un-checkpointed
-        (300K vs 236K tokens/s) and switches it on around 64 x 4096."""
+        (308K vs 241K tokens/s, profiles/r1_bench_gpt2medium_s4096.jsonl) and checkpoints a
+        growing fraction of the blocks from about 64 x 4096 on, instead of all-or-nothing."""
         mode = self.config.activation_checkpointing
+        L = self.config.n_blocks
+        if isinstance(mode, bool) or mode is None:
+            return L if mode else 0
+        if isinstance(mode, float):
+            return min(L, max(0, math.ceil(mode * L)))
         if mode != "auto":
-            return bool(mode)
+            raise ValueError(f"activation_checkpointing={mode!r}: expected bool, float fraction or 'auto'")
         if not idx.is_cuda:
-            return False
+            return 0
         if getattr(self, "_ckpt_auto", None) is None or self._ckpt_auto[0] != idx.numel():
             free, _ = torch.cuda.mem_get_info(idx.device)
-            self._ckpt_auto = (idx.numel(), self.activation_bytes(idx.numel()) > 0.5 * free)
+            self._ckpt_auto = (idx.numel(), self.auto_checkpoint_blocks(idx.numel(), 0.5 * free))
         return self._ckpt_auto[1]
+
+    def auto_checkpoint_blocks(self, tokens: int, budget_bytes: float) -> int:
+        """Fewest checkpointed blocks whose kept activations fit ``budget_bytes`` (all if none do)."""
+        L = self.config.n_blocks
+        full = self.activation_bytes(tokens)
+        if full <= budget_bytes:
+            return 0
+        per_block = full / L
+        saved = per_block - 2 * 2 * self.config.n_embed * tokens  # a checkpointed block keeps x, res
+        if saved <= 0:
+            return L
+        return min(L, math.ceil((full - budget_bytes) / saved))
+
+    def use_checkpointing(self, idx) -> bool:
+        """True when at least one block is checkpointed (see ``checkpointed_blocks``)."""
+        return self.checkpointed_blocks(idx) > 0
 
     def num_params(self) -> int:
         return sum(p.numel() for p in self.parameters())
@@ -313,10 +339,10 @@ class GPT(nn.Module):
         x = self._embed(idx)
         rope = self.rope_tables(idx.device, idx.shape[1])
         res = None
-        ckpt = self.use_checkpointing(idx) and self.training and torch.is_grad_enabled()
+        n_ckpt = self.checkpointed_blocks(idx) if self.training and torch.is_grad_enabled() else 0
         x_bias = None  # bias of the layer that produced x (fused into the next norm's backward)
-        for blk in self.attn_blocks:
-            if ckpt:
+        for i, blk in enumerate(self.attn_blocks):
+            if i < n_ckpt:
                 x, res = checkpoint(blk, x, res, rope, x_bias, True, use_reentrant=False)
             else:
                 x, res = blk(x, res, rope, x_bias, True)

@@ -196,6 +196,32 @@ def test_activation_checkpointing_auto_policy():
     assert m.activation_bytes(32768) == 2 * (6 * 1024 + 2 * 4096) * 32768 * 24
     assert m.use_checkpointing(torch.zeros(2, 8, dtype=torch.long)) is False
     assert GPT(_tiny().replace(activation_checkpointing=True)).use_checkpointing(torch.zeros(1, 4, dtype=torch.long))
+    # partial: only as many blocks as it takes to fit the budget
+    full = m.activation_bytes(32768)
+    assert m.auto_checkpoint_blocks(32768, 2 * full) == 0
+    saved = full / 24 - 4 * 1024 * 32768
+    assert m.auto_checkpoint_blocks(32768, full - 5.5 * saved) == 6
+    assert m.auto_checkpoint_blocks(32768, 0) == 24
+    assert GPT(_tiny().replace(activation_checkpointing=0.5)).checkpointed_blocks(torch.zeros(1, 4)) == 1
+
+
+def test_partial_activation_checkpointing_same_grads():
+    """Checkpointing a fraction of the blocks leaves loss and gradients unchanged."""
+    cfg = _tiny().replace(n_blocks=3)
+    torch.manual_seed(0)
+    m1 = GPT(cfg)
+    m2 = GPT(cfg.replace(activation_checkpointing=0.5))
+    m2.load_state_dict(m1.state_dict())
+    assert m2.checkpointed_blocks(torch.zeros(1, 4)) == 2
+    x = torch.randint(0, cfg.vocab_size, (2, 16))
+    losses = []
+    for m in (m1, m2):
+        _, loss = m(x, x)
+        loss.backward()
+        losses.append(loss.item())
+    assert abs(losses[0] - losses[1]) < 1e-6
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        torch.testing.assert_close(p1.grad, p2.grad, rtol=1e-5, atol=1e-6, msg=n)
 
 
 @pytest.mark.parametrize("mod", ["attention", "mlp", "transformer_block", "transformer"])
