@@ -50,17 +50,17 @@ def main():
         rel = ((r.float() - ref).norm() / ref.norm()).item()
         flops = 2.0 * M * P * Q
         res = {"P": P, "Q": Q, "M": M, "rel_err": rel}
-        for mf in (32, 288, 544):  # staging: 64-token double buffer / (+256) 32-token 4-slot ring / (+512) 5-slot ring
+        for mf in (32, 1056):  # split-K slices summed by the separate reduce pass (default) / (+1024) in-kernel
             torch.ops.pllm.wgrad_set_mfma(mf)
             r = torch.ops.pllm.wgrad(dy[:4096], x[:4096])
             res[f"rel_err{mf}"] = ((r.float() - ref).norm() / ref.norm()).item()
         for _ in range(args.rounds):
-            for mf in (32, 288, 544):
+            for mf in (32, 1056):
                 torch.ops.pllm.wgrad_set_mfma(mf)
                 res.setdefault(f"hip{mf}_us", []).append(1e6 * timeit(lambda: torch.ops.pllm.wgrad(dy, x, tgt)))
             res.setdefault("blas_us", []).append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
         torch.ops.pllm.wgrad_set_mfma(32)
-        for k in ("hip32", "hip288", "hip544", "blas"):
+        for k in ("hip32", "hip1056", "blas"):
             res[f"{k}_tflops"] = flops / (min(res[f"{k}_us"]) * 1e-6) / 1e12
         print(json.dumps(res), flush=True)
         out.append(res)

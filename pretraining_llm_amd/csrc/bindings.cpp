@@ -159,10 +159,14 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   int S = 1, slice = 1;
   pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
   Tensor part = at::empty({S > 1 ? S : 0, P, Q}, dy.options().dtype(at::kFloat));
+  Tensor cnt;  // per-output-tile arrival counters for the in-kernel split-K reduction
+  if (S > 1 && pllm::wgrad_fused_reduce())
+    cnt = at::zeros({((P + 255) / 256) * ((Q + 255) / 256)}, dy.options().dtype(at::kInt));
   if (M > 0)
     pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
                 S > 1 ? part.data_ptr<float>() : nullptr,
-                out.data_ptr(), out_acc.has_value(), cur_stream());
+                out.data_ptr(), out_acc.has_value(), cnt.defined() ? cnt.data_ptr<int>() : nullptr,
+                cur_stream());
   else if (!out_acc)
     out.zero_();
   return out;

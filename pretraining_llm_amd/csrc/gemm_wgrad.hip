@@ -21,8 +21,12 @@
 //  * both MFMA fragments come from ds_read_b64_tr_b16 transposed reads (the reduction
 //    index is the image row);
 //  * one slice: the tile is added straight into the bf16 gradient; several: fp32
-//    partial tiles go to a [S][P][Q] slab and a reduce kernel sums the slices in a
-//    fixed order into the bf16 gradient (deterministic, accumulate fused).
+//    partial tiles go to a [S][P][Q] slab summed in a fixed slice order by wgrad_reduce_kernel
+//    (default), or the last workgroup of each tile to arrive
+//    (per-tile arrival counter, release/acquire fences) sums the slices in a fixed order
+//    into the bf16 gradient (deterministic, accumulate fused) -- no second launch, and the
+//    partials are re-read while still in the MALL.  That variant is an A/B switch
+//    (wgrad_set_mfma +1024) and measured slower than the default separate reduce pass.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include <type_traits>
 
@@ -76,7 +80,8 @@ template <int MF, int RING>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part,
-                                                   uint16_t* __restrict__ out, int accumulate, int g_prio) {
+                                                   uint16_t* __restrict__ out, int accumulate, int g_prio,
+                                                   int* __restrict__ tile_cnt) {
   constexpr int BK_ = RING == 0 ? BKM : 32;
   constexpr int SLOTS = RING == 0 ? 2 : (RING == 1 ? 4 : 5);
   constexpr int AHEAD = SLOTS - 1;
@@ -245,6 +250,41 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       }
     }
   }
+  if (!tile_cnt) return;  // separate wgrad_reduce_kernel pass
+  // The last of the S workgroups of this tile to finish sums the S partial tiles in slice order
+  // (bit-identical to wgrad_reduce_kernel) while they are still in the MALL, saving the reduce
+  // launch and its HBM re-read.  Release: this workgroup's partial stores before its count;
+  // acquire: every wave of the last workgroup fences before reading the other slices' partials.
+  int* is_last = reinterpret_cast<int*>(smem);  // the staging ring is idle after the barrier below
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) *is_last = atomicAdd(tile_cnt + t, 1) == S - 1;
+  __syncthreads();
+  if (!*is_last) return;
+  __threadfence();
+  const int64_t PQ = (int64_t)P * Q;
+  for (int c = tid; c < BT * (BT / 8); c += NT) {
+    const int p = p0 + c / (BT / 8), q = q0 + (c % (BT / 8)) * 8;
+    if (p >= P || q >= Q) continue;
+    const int64_t idx = (int64_t)p * Q + q;
+    float f[8];
+    if (accumulate) {
+      unpack8(ld16(out + idx), f);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) f[k] = 0.f;
+    }
+    for (int ss = 0; ss < S; ++ss) {
+      const f32x4* pp = reinterpret_cast<const f32x4*>(part + ss * PQ + idx);
+      const f32x4 a = pp[0], b = pp[1];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        f[k] += a[k];
+        f[4 + k] += b[k];
+      }
+    }
+    st16(out + idx, pack8(f));
+  }
 }
 
 // dW[p, q] (+)= sum_s slab[s][p][q]   (8 columns per thread, fixed slice order)
@@ -282,7 +322,15 @@ static int g_wgrad_mfma = 32;
 static int g_wgrad_prio = 0;
 static int g_wgrad_plan_fill = 0;  // A/B (+128): the older fill-efficiency-only split plan
 static int g_wgrad_ring = 0;       // A/B (+256 / +512): staging ring 1 / 2 (wgrad_kernel RING)
+// A/B (+1024): split-K slices summed in-kernel by the last workgroup of each tile instead of by
+// the separate wgrad_reduce_kernel.  Measured 1.0-3.2x SLOWER on every GPT-2 / llama shape
+// (profiles/r1_wgrad_fused_reduce_negative.jsonl): the sum of S slices of a tile lands on one
+// CU (9 of them for a 768x768 gradient) instead of spreading over the whole GPU, so the
+// separate pass stays the default.
+static int g_wgrad_split_reduce = 1;
 void wgrad_set_mfma(int mf) {
+  g_wgrad_split_reduce = (mf & 1024) ? 0 : 1;
+  mf &= 1023;
   g_wgrad_ring = (mf & 512) ? 2 : ((mf & 256) ? 1 : 0);
   mf &= 255;
   g_wgrad_plan_fill = (mf & 128) ? 1 : 0;
@@ -327,20 +375,24 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   *S = (kst + st_per - 1) / st_per;
 }
 
+int wgrad_fused_reduce() { return !g_wgrad_split_reduce; }
+
+// tile_cnt: ntiles zeroed ints when the slices are summed in-kernel (wgrad_fused_reduce()), else null
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool accumulate, hipStream_t st) {
+           bool accumulate, int* tile_cnt, hipStream_t st) {
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
 #define PLLM_WGRAD_LAUNCH(MFV, RV)                                                                         \
   hipLaunchKernelGGL((wgrad_kernel<MFV, RV>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,   \
-                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio)
+                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio, \
+                     S > 1 ? tile_cnt : nullptr)
   if (g_wgrad_mfma == 16) PLLM_WGRAD_LAUNCH(16, 0);
   else if (g_wgrad_ring == 1) PLLM_WGRAD_LAUNCH(32, 1);
   else if (g_wgrad_ring == 2) PLLM_WGRAD_LAUNCH(32, 2);
   else PLLM_WGRAD_LAUNCH(32, 0);
 #undef PLLM_WGRAD_LAUNCH
-  if (S == 1) return;
+  if (S == 1 || tile_cnt) return;
   const int64_t PQ = (int64_t)P * Q;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((PQ / 8 + 255) / 256)), dim3(256), 0, st, part, S, PQ,
                      (uint16_t*)out, (int)accumulate);

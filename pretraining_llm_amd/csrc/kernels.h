@@ -100,8 +100,9 @@ void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, v
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad_set_mfma(int mf);
+int wgrad_fused_reduce();  // 1: split-K slices summed in-kernel (needs tile_cnt), 0: separate pass
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool accumulate, hipStream_t st);
+           bool accumulate, int* tile_cnt, hipStream_t st);
 
 // transpose.hip: desc int64 [n][6] = (src, dst, rows, cols, first tile, tiles per row band)
 int transpose_tiles(int R, int C);

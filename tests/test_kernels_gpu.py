@@ -551,6 +551,15 @@ def test_wgrad_kernel(M, P, Q):
     ref = dy.float().t() @ x.float()
     out = torch.ops.pllm.wgrad(dy, x)
     assert _rel(out, ref) < 5e-3, _rel(out, ref)
+    # the in-kernel split-K reduction (A/B variant: last workgroup of a tile) is bit-identical
+    # to the default separate pass
+    try:
+        torch.ops.pllm.wgrad_set_mfma(32 + 1024)
+        out_sep = torch.ops.pllm.wgrad(dy, x)
+    finally:
+        torch.ops.pllm.wgrad_set_mfma(32)
+    assert torch.equal(out, out_sep)
+    assert torch.equal(out, torch.ops.pllm.wgrad(dy, x))  # deterministic across calls
     acc = torch.randn(P, Q, device=DEV).bfloat16()
     ref2 = acc.float() + ref
     torch.ops.pllm.wgrad(dy, x, acc)
