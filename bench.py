@@ -56,12 +56,39 @@ def parse(argv=None):
     ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
     ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
     ap.add_argument("--cuda-graph", action="store_true", help="replay the whole step as one captured hipGraph")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
+                    help="cpu: functional rehearsal on gloo (fp32, tiny shapes); never a measurement")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args, argv) -> int:
+    """``--gpus N`` without a torchrun environment: start N ranks (one process per GPU,
+    RCCL) through ``torch.distributed.run`` as a CHILD process -- this process never
+    touches the GPU -- and return the launcher's exit code."""
+    import subprocess
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
+
+
 def main(argv=None):
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return launch_ranks(args, argv)
     import torch
     import torch.distributed as dist
     from pretraining_llm_amd import ops
@@ -71,17 +98,22 @@ def main(argv=None):
     from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
     from pretraining_llm_amd.utils.dist import init_distributed
 
-    di = init_distributed("nccl", "cuda")
+    cpu = args.device == "cpu"
+    di = init_distributed("gloo" if cpu else "nccl", args.device)
     world = di.world_size
-    if args.gpus != world and di.is_master:
-        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; measuring {world} rank(s)", file=sys.stderr)
+    if args.gpus != world:
+        print(f"[bench] error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     dev = di.device
     tuned = False
+    if cpu:
+        args.no_tuned_gemm = True
+        torch.set_num_threads(max(1, min(4, os.cpu_count() or 1)))
     if not args.no_tuned_gemm:
         from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
         tuned = enable_tuned_gemms(dev.index or 0, tune_missing=args.tune_missing and args.warmup > 0)
     ops.set_backend(args.backend)
-    if args.backend == "auto":
+    if args.backend == "auto" and not cpu:
         ops._lib.require()  # the HIP path must be the one that runs: fail loudly if the extension is missing
 
     torch.manual_seed(1234)
@@ -93,7 +125,7 @@ def main(argv=None):
     if args.act_ckpt is not None:
         ac = args.act_ckpt
         mcfg = mcfg.replace(activation_checkpointing=ac if ac == "auto" else ac == "1" if ac in ("0", "1") else float(ac))
-    model = GPT(mcfg).to(device=dev, dtype=torch.bfloat16)
+    model = GPT(mcfg).to(device=dev, dtype=torch.float32 if cpu else torch.bfloat16)
     okw = dict(lr=6e-4, betas=(0.9, 0.95), eps=1e-8, weight_decay=0.1, decay_filter=no_decay_1d,
                max_grad_norm=args.grad_clip)
     if args.zero:
@@ -128,19 +160,20 @@ def main(argv=None):
             x, y = loader.next()
             return gstep(x, y, 6e-4)
 
+    sync = (lambda: None) if cpu else torch.cuda.synchronize
     model.train()
     for i in range(args.warmup):
         loss = step()
         if args.verbose and di.is_master:
-            torch.cuda.synchronize()
+            sync()
             print(f"[bench] warmup {i} loss {float(loss):.4f}", file=sys.stderr)
     if dist.is_initialized():
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
-    torch.cuda.synchronize()
+    sync()
     if dist.is_initialized():
         dist.barrier()
     elapsed = time.perf_counter() - t0
@@ -167,7 +200,8 @@ def main(argv=None):
             "vs_baseline": (round(tps / (EAGER_BASELINE_TOK_S_PER_GPU * world), 3)
                             if (args.model == "gpt2-small" and T == 1024 and args.backend == "auto") else None),
             "baseline": "reference-equivalent eager PyTorch on MI355X, 487.05K tok/s/GPU (BASELINE.md)",
-            "dtype": "bf16",
+            "dtype": "fp32" if cpu else "bf16",
+            "grad_dtype": str(opt.flat_grad.dtype).replace("torch.", ""),
             "data": "synthetic (native token loader over a generated uint16 shard), random-init weights",
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
                        "parallelism": f"dp{world}" + ("-zero1" if args.zero else ""), "micro_batch_per_gpu": B, "backend": args.backend,
@@ -177,7 +211,15 @@ def main(argv=None):
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),
             "params_M": round(sum(p.numel() for p in opt.params) / 1e6, 2),
             "final_loss": round(final_loss, 4),
-            "peak_mem_gb": round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+            "peak_mem_gb": None if cpu else round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
+            "comm": {"backend": di.backend if world > 1 else None, "world": world,
+                     "n_buckets": len(getattr(engine, "buckets", [])),
+                     "bucket_mb": [round(b, 2) for b in engine.bucket_sizes_mb()]
+                     if hasattr(engine, "bucket_sizes_mb") else None,
+                     # True once the bucket readiness counts were learned: later steps launch each
+                     # bucket's collective from the backward hooks (overlapped), not at the end
+                     "hook_launched_buckets": getattr(engine, "_expected", None) is not None},
+            "device": args.device,
         }
         print(json.dumps(rec), flush=True)
     loader.close()
@@ -186,4 +228,4 @@ def main(argv=None):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

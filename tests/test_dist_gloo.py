@@ -146,3 +146,23 @@ def test_comm_bench_sweep_gloo():
     recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert {x["op"] for x in recs} == {"all_reduce", "reduce_scatter", "all_gather", "all_to_all"}
     assert all(x["busbw_GBps"] > 0 and x["world"] == 2 for x in recs)
+
+
+def test_bench_self_launches_ranks_cpu():
+    """``bench.py --gpus 2`` with no torchrun environment starts 2 ranks itself (gloo on CPU here,
+    RCCL on GPUs) and rank 0 reports n_gpus 2 with the time taken as the max over ranks."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu",
+                        "--model", "gpt2-tiny", "--steps", "2", "--warmup", "1", "--batch", "2", "--seq", "64"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(recs) == 1, r.stdout
+    rec = recs[0]
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
+    assert rec["comm"]["world"] == 2 and rec["comm"]["hook_launched_buckets"]
+    assert rec["value"] > 0 and abs(rec["value"] - 2 * 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) / rec["value"] < 0.01
