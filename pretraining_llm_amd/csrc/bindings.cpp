@@ -29,6 +29,14 @@ void check_aligned16(const Tensor& t, const char* name) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0, name, " must be 16-byte aligned");
 }
 const void* opt_ptr(const std::optional<Tensor>& t) { return t.has_value() ? t->data_ptr() : nullptr; }
+// gradient accumulation targets (views of the optimizer's flat gradient): bf16 or fp32;
+// returns true for fp32
+bool check_grad(const Tensor& t, const char* name) {
+  check_gpu(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, name,
+              " must be bfloat16 or float32, got ", t.scalar_type());
+  return t.scalar_type() == at::kFloat;
+}
 
 // ---------------------------------------------------------------- norms
 std::vector<Tensor> norm_fwd(const Tensor& x, const std::optional<Tensor>& res, const Tensor& w,
@@ -81,13 +89,16 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   }
   const bool acc = dw_acc.has_value();
   TORCH_CHECK(!has_bias || acc == db_acc.has_value(), "norm_bwd: dw_acc and db_acc must be given together");
+  bool gf32 = false;
   if (acc) {
-    check_bf16(*dw_acc, "dw_acc");
+    gf32 = check_grad(*dw_acc, "dw_acc");
     TORCH_CHECK(dw_acc->numel() == C && dw_acc->is_contiguous(), "dw_acc shape");
     if (has_bias) {
-      check_bf16(*db_acc, "db_acc");
+      TORCH_CHECK(check_grad(*db_acc, "db_acc") == gf32, "db_acc dtype must match dw_acc");
       TORCH_CHECK(db_acc->numel() == C && db_acc->is_contiguous(), "db_acc shape");
     }
+  } else {
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16, "norm_bwd: bf16 weight");
   }
   Tensor dx = at::empty_like(dy);
   Tensor dw = acc ? *dw_acc : at::zeros({C}, w.options());
@@ -98,14 +109,14 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   Tensor dbp = has_bias ? at::empty({G, C}, f32) : Tensor();
   Tensor xbp;
   if (xb_acc) {  // fused bias gradient of the producer of x: accumulated into xb_acc
-    check_bf16(*xb_acc, "xb_acc");
+    TORCH_CHECK(acc && check_grad(*xb_acc, "xb_acc") == gf32, "xb_acc needs dw_acc targets of the same dtype");
     TORCH_CHECK(xb_acc->numel() == C && xb_acc->is_contiguous(), "xb_acc shape");
     xbp = at::empty({G, C}, f32);
   }
   if (N > 0) {
     pllm::norm_bwd(dy.data_ptr(), s.data_ptr(), w.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                    opt_ptr(ds), dx.data_ptr(), dwp.data_ptr<float>(), has_bias ? dbp.data_ptr<float>() : nullptr,
-                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, (int)N, (int)C, rms, acc,
+                   dw.data_ptr(), has_bias ? db.data_ptr() : nullptr, gf32, (int)N, (int)C, rms, acc,
                    xb_acc ? xbp.data_ptr<float>() : nullptr, xb_acc ? xb_acc->data_ptr() : nullptr, true,
                    cur_stream());
   }
@@ -122,8 +133,9 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
   const int64_t N = C ? dy.numel() / C : 0;
   TORCH_CHECK(C % 8 == 0, "bias_grad: C % 8");
   Tensor out;
+  bool of32 = false;
   if (out_acc) {
-    check_bf16(*out_acc, "out_acc");
+    of32 = check_grad(*out_acc, "out_acc");
     TORCH_CHECK(out_acc->numel() == C && out_acc->is_contiguous(), "out_acc shape");
     out = *out_acc;
   } else {
@@ -131,7 +143,7 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
   }
   if (N > 0) {
     Tensor part = at::empty({pllm::colsum_groups((int)N), C}, dy.options().dtype(at::kFloat));
-    pllm::bias_grad(dy.data_ptr(), (int)N, (int)C, part.data_ptr<float>(), out.data_ptr(), true, cur_stream());
+    pllm::bias_grad(dy.data_ptr(), (int)N, (int)C, part.data_ptr<float>(), out.data_ptr(), of32, true, cur_stream());
   }
   return out;
 }
@@ -149,9 +161,11 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   check_aligned16(dy, "dy");
   check_aligned16(x, "x");
   Tensor out;
+  bool of32 = false;
   if (out_acc) {
-    check_bf16(*out_acc, "out_acc");
+    of32 = check_grad(*out_acc, "out_acc");
     TORCH_CHECK(out_acc->numel() == P * Q && out_acc->is_contiguous(), "wgrad: out_acc shape");
+    check_aligned16(*out_acc, "out_acc");
     out = *out_acc;
   } else {
     out = at::empty({P, Q}, dy.options());
@@ -159,14 +173,9 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   int S = 1, slice = 1;
   pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
   Tensor part = at::empty({S > 1 ? S : 0, P, Q}, dy.options().dtype(at::kFloat));
-  Tensor cnt;  // per-output-tile arrival counters for the in-kernel split-K reduction
-  if (S > 1 && pllm::wgrad_fused_reduce())
-    cnt = at::zeros({((P + 255) / 256) * ((Q + 255) / 256)}, dy.options().dtype(at::kInt));
   if (M > 0)
     pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
-                S > 1 ? part.data_ptr<float>() : nullptr,
-                out.data_ptr(), out_acc.has_value(), cnt.defined() ? cnt.data_ptr<int>() : nullptr,
-                cur_stream());
+                S > 1 ? part.data_ptr<float>() : nullptr, out.data_ptr(), of32, out_acc.has_value(), cur_stream());
   else if (!out_acc)
     out.zero_();
   return out;
@@ -265,60 +274,6 @@ std::vector<Tensor> gemv(const Tensor& x, const Tensor& w, const std::optional<T
   return {y};
 }
 
-// ---------------------------------------------------------------- NT GEMM + MLP epilogues
-// epi 0: [a b^T (+bias)];  epi 1: [gelu(h), h] with h = a b^T + bias;
-// epi 2: [(a b^T) * gelu'(aux)], adding its column sums into ``bias_grad_acc`` (bf16, in place)
-std::vector<Tensor> gemm_nt(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
-                            const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_grad_acc) {
-  check_bf16(a, "a");
-  check_bf16(b, "b");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_nt: a [M,K], b [N,K]");
-  TORCH_CHECK(a.stride(1) == 1 && b.stride(1) == 1 && a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0,
-              "gemm_nt: K-contiguous operands, row strides % 8");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(K % 64 == 0 && N % 8 == 0, "gemm_nt: K % 64 == 0 and N % 8 == 0");
-  TORCH_CHECK(epi >= 0 && epi <= 2, "gemm_nt: epi 0..2");
-  check_aligned16(a, "a");
-  check_aligned16(b, "b");
-  GemmNTArgs g{};
-  g.A = (const uint16_t*)a.data_ptr();
-  g.B = (const uint16_t*)b.data_ptr();
-  g.M = (int)M; g.N = (int)N; g.K = (int)K;
-  g.lda = a.stride(0); g.ldb = b.stride(0); g.ldc = N;
-  Tensor c = at::empty({M, N}, a.options());
-  g.C = (uint16_t*)c.data_ptr();
-  std::vector<Tensor> outs{c};
-  if (bias && epi != 2) {
-    check_bf16(*bias, "bias");
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm_nt: bias [N]");
-    TORCH_CHECK(((uintptr_t)bias->data_ptr() & 7) == 0, "gemm_nt: bias must be 8-byte aligned");
-    g.bias = (const uint16_t*)bias->data_ptr();
-  }
-  Tensor part;
-  if (epi == 1) {
-    Tensor h = at::empty({M, N}, a.options());
-    g.aux = (uint16_t*)h.data_ptr();
-    outs.push_back(h);
-  } else if (epi == 2) {
-    TORCH_CHECK(aux.has_value(), "gemm_nt epi 2 needs aux (pre-activation)");
-    check_bf16(*aux, "aux");
-    TORCH_CHECK(aux->numel() == M * N && aux->is_contiguous(), "gemm_nt: aux [M,N] contiguous");
-    g.aux = (uint16_t*)aux->data_ptr();
-    TORCH_CHECK(bias_grad_acc.has_value(), "gemm_nt epi 2 needs bias_grad_acc");
-    check_bf16(*bias_grad_acc, "bias_grad_acc");
-    TORCH_CHECK(bias_grad_acc->numel() == N && bias_grad_acc->is_contiguous(), "gemm_nt: bias_grad_acc [N]");
-    part = at::empty({pllm::gemm_nt_part_rows((int)M), N}, a.options().dtype(at::kFloat));
-    g.part = part.data_ptr<float>();
-  }
-  if (M > 0) {
-    pllm::gemm_nt(g, (int)epi, cur_stream());
-    if (epi == 2)
-      pllm::col_reduce(g.part, pllm::gemm_nt_part_rows((int)M), (int)N, bias_grad_acc->data_ptr(), true,
-                       cur_stream());
-  }
-  return outs;
-}
-
 // ---------------------------------------------------------------- activations
 Tensor act_fwd(const Tensor& x, int64_t op) {
   check_bf16(x, "x");
@@ -345,7 +300,7 @@ Tensor act_bwd_bias(const Tensor& dy, const Tensor& xin, int64_t op, Tensor& bia
   check_bf16(xin, "x");
   check_contig(dy, "dy");
   check_contig(xin, "x");
-  check_bf16(bias_acc, "bias_acc");
+  const bool gf32 = check_grad(bias_acc, "bias_acc");
   const int64_t C = dy.size(-1);
   TORCH_CHECK(dy.sizes() == xin.sizes() && C % 8 == 0, "act_bwd_bias shapes");
   TORCH_CHECK(bias_acc.numel() == C && bias_acc.is_contiguous(), "bias_acc shape");
@@ -354,7 +309,7 @@ Tensor act_bwd_bias(const Tensor& dy, const Tensor& xin, int64_t op, Tensor& bia
   if (N > 0) {
     Tensor part = at::empty({pllm::colsum_groups((int)N), C}, dy.options().dtype(at::kFloat));
     pllm::act_bwd_bias((int)op, dy.data_ptr(), xin.data_ptr(), dx.data_ptr(), (int)N, (int)C, part.data_ptr<float>(),
-                       bias_acc.data_ptr(), true, cur_stream());
+                       bias_acc.data_ptr(), gf32, true, cur_stream());
   }
   return dx;
 }
@@ -522,11 +477,14 @@ std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V
   TORCH_CHECK(!has_wpe || n_pos >= T, "embedding bwd: n_pos < T");
   const bool acc = dwte_acc.has_value();
   TORCH_CHECK(!has_wpe || acc == dwpe_acc.has_value(), "embedding_bwd: both or neither accumulation targets");
+  bool gf32 = false;
   if (acc) {
-    check_bf16(*dwte_acc, "dwte_acc");
+    gf32 = check_grad(*dwte_acc, "dwte_acc");
+    check_aligned16(*dwte_acc, "dwte_acc");
     TORCH_CHECK(dwte_acc->numel() == V * C && dwte_acc->is_contiguous(), "dwte_acc shape");
     if (has_wpe) {
-      check_bf16(*dwpe_acc, "dwpe_acc");
+      TORCH_CHECK(check_grad(*dwpe_acc, "dwpe_acc") == gf32, "dwpe_acc dtype must match dwte_acc");
+      check_aligned16(*dwpe_acc, "dwpe_acc");
       TORCH_CHECK(dwpe_acc->numel() == n_pos * C && dwpe_acc->is_contiguous(), "dwpe_acc shape");
     }
   }
@@ -538,7 +496,7 @@ std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V
   Tensor dwpe = has_wpe ? (acc ? *dwpe_acc : at::zeros({n_pos, C}, dx.options())) : Tensor();
   if (Bn * T)
     pllm::embedding_bwd(dx.data_ptr(), sorted.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), dwte.data_ptr(),
-                        has_wpe ? dwpe.data_ptr() : nullptr, Bn * T, (int)Bn, (int)T, (int)C, V, cur_stream());
+                        has_wpe ? dwpe.data_ptr() : nullptr, gf32, Bn * T, (int)Bn, (int)T, (int)C, V, cur_stream());
   if (acc) return {};
   if (!has_wpe) return {dwte};
   return {dwte, dwpe};
@@ -737,9 +695,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
-  m.def("gemm_nt(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_grad_acc=None) -> Tensor[]");
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> Tensor[]");
-  m.def("gemm_nt_set_pipe(int p) -> ()", [](int64_t p) { pllm::gemm_nt_set_pipe((int)p); });
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
   m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
@@ -782,7 +738,6 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("sample", sample);
   m.impl("attn_fwd", attn_fwd);
   m.impl("attn_decode", attn_decode);
-  m.impl("gemm_nt", gemm_nt);
   m.impl("gemv", gemv);
   m.impl("attn_bwd", attn_bwd);
 }

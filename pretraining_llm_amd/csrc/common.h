@@ -63,6 +63,44 @@ PLLM_DEV void st16_nt(void* p, const u32x4& v) {
   __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
 }
 
+// ---- gradient buffers: bf16 or fp32 (FlatAdamW grad_dtype) ----------------
+// 8 consecutive gradient values <-> 8 floats: 16 B (bf16) or 32 B (fp32) per lane
+template <bool F32>
+PLLM_DEV void ld8g(const void* p, float* f) {
+  if constexpr (F32) {
+    const f32x4* q = reinterpret_cast<const f32x4*>(p);
+    const f32x4 a = q[0], b = q[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f[i] = a[i];
+      f[4 + i] = b[i];
+    }
+  } else {
+    unpack8(ld16(p), f);
+  }
+}
+template <bool F32>
+PLLM_DEV void st8g(void* p, const float* f) {
+  if constexpr (F32) {
+    f32x4* q = reinterpret_cast<f32x4*>(p);
+    q[0] = f32x4{f[0], f[1], f[2], f[3]};
+    q[1] = f32x4{f[4], f[5], f[6], f[7]};
+  } else {
+    st16(p, pack8(f));
+  }
+}
+// one gradient element
+template <bool F32>
+PLLM_DEV float ldg1(const void* p, int64_t i) {
+  if constexpr (F32) return reinterpret_cast<const float*>(p)[i];
+  else return bf2f(reinterpret_cast<const uint16_t*>(p)[i]);
+}
+template <bool F32>
+PLLM_DEV void stg1(void* p, int64_t i, float v) {
+  if constexpr (F32) reinterpret_cast<float*>(p)[i] = v;
+  else reinterpret_cast<uint16_t*>(p)[i] = f2bf_bits(v);
+}
+
 // ---- wave64 / block reductions -------------------------------------------
 PLLM_DEV float wave_sum(float v) {
 #pragma unroll

@@ -218,7 +218,7 @@ void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStr
 }
 
 void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int C, float* part, void* bias_grad,
-                  bool accumulate, hipStream_t st) {
+                  bool grad_f32, bool accumulate, hipStream_t st) {
   const int G = colsum_groups(N);
   dim3 grid((C + 511) / 512, G);
   if (op == 0)
@@ -227,7 +227,7 @@ void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int 
   else
     hipLaunchKernelGGL(act_bwd_colsum_kernel<1>, grid, dim3(256), 0, st, (const uint16_t*)dy, (const uint16_t*)xin,
                        (uint16_t*)dx, N, C, part);
-  col_reduce(part, G, C, bias_grad, accumulate, st);
+  col_reduce(part, G, C, bias_grad, grad_f32, accumulate, st);
 }
 
 void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st) {

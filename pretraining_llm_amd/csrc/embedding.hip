@@ -36,9 +36,13 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 
 // one wave per sorted position; only the first position of each run of equal
 // ids does work: it sums the dx rows of the whole run in sorted (stable) order.
+// dwte / dwpe are the optimizer's gradient views: bf16 or fp32 (F32)
+template <bool F32>
 __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(const uint16_t* __restrict__ dx, const int32_t* __restrict__ sorted,
-                                                            const int32_t* __restrict__ perm, uint16_t* __restrict__ dwte,
+                                                            const int32_t* __restrict__ perm, void* __restrict__ dwte,
                                                             int64_t N, int C, int64_t V) {
+  constexpr int ES = F32 ? 4 : 2;
+  char* const gw = reinterpret_cast<char*>(dwte);
   const int64_t i = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   if (i >= N) return;
@@ -50,33 +54,36 @@ __global__ __launch_bounds__(256) void embed_bwd_tok_kernel(const uint16_t* __re
   const int cv = C >> 3;
   for (int c = lane; c < cv; c += 64) {
     float acc[8];
-    unpack8(ld16(dwte + (int64_t)id * C + c * 8), acc);  // accumulate into the destination
+    ld8g<F32>(gw + ((int64_t)id * C + c * 8) * ES, acc);  // accumulate into the destination
     for (int64_t j = i; j < end; ++j) {
       float f[8];
       unpack8(ld16(dx + (int64_t)perm[j] * C + c * 8), f);
 #pragma unroll
       for (int k = 0; k < 8; ++k) acc[k] += f[k];
     }
-    st16(dwte + (int64_t)id * C + c * 8, pack8(acc));
+    st8g<F32>(gw + ((int64_t)id * C + c * 8) * ES, acc);
   }
 }
 
 // dwpe[t] = sum_b dx[b, t]   (thread per (t, 8-col chunk), fixed b order)
-__global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const uint16_t* __restrict__ dx, uint16_t* __restrict__ dwpe,
+template <bool F32>
+__global__ __launch_bounds__(256) void embed_bwd_pos_kernel(const uint16_t* __restrict__ dx, void* __restrict__ dwpe,
                                                             int Bn, int T, int C) {
+  constexpr int ES = F32 ? 4 : 2;
+  char* const gw = reinterpret_cast<char*>(dwpe);
   const int cv = C >> 3;
   const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   if (i >= (int64_t)T * cv) return;
   const int t = (int)(i / cv), c = (int)(i % cv);
   float acc[8];
-  unpack8(ld16(dwpe + (int64_t)t * C + c * 8), acc);  // accumulate into the destination
+  ld8g<F32>(gw + ((int64_t)t * C + c * 8) * ES, acc);  // accumulate into the destination
   for (int b = 0; b < Bn; ++b) {
     float f[8];
     unpack8(ld16(dx + ((int64_t)b * T + t) * C + c * 8), f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc[k] += f[k];
   }
-  st16(dwpe + (int64_t)t * C + c * 8, pack8(acc));
+  st8g<F32>(gw + ((int64_t)t * C + c * 8) * ES, acc);
 }
 
 }  // namespace
@@ -92,14 +99,15 @@ void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* o
                      (uint16_t*)out, N, T, C, pos_offset, V);
 }
 
-void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, int64_t N,
-                   int Bn, int T, int C, int64_t V, hipStream_t st) {
-  hipLaunchKernelGGL(embed_bwd_tok_kernel, dim3((unsigned)((N + 3) / 4)), dim3(256), 0, st, (const uint16_t*)dx, sorted,
-                     perm, (uint16_t*)dwte, N, C, V);
-  if (dwpe) {
-    const int64_t work = (int64_t)T * (C / 8);
-    hipLaunchKernelGGL(embed_bwd_pos_kernel, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, st,
-                       (const uint16_t*)dx, (uint16_t*)dwpe, Bn, T, C);
+void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, bool grad_f32,
+                   int64_t N, int Bn, int T, int C, int64_t V, hipStream_t st) {
+  const dim3 tg((unsigned)((N + 3) / 4)), pg((unsigned)(((int64_t)T * (C / 8) + 255) / 256));
+  if (grad_f32) {
+    hipLaunchKernelGGL(embed_bwd_tok_kernel<true>, tg, dim3(256), 0, st, (const uint16_t*)dx, sorted, perm, dwte, N, C, V);
+    if (dwpe) hipLaunchKernelGGL(embed_bwd_pos_kernel<true>, pg, dim3(256), 0, st, (const uint16_t*)dx, dwpe, Bn, T, C);
+  } else {
+    hipLaunchKernelGGL(embed_bwd_tok_kernel<false>, tg, dim3(256), 0, st, (const uint16_t*)dx, sorted, perm, dwte, N, C, V);
+    if (dwpe) hipLaunchKernelGGL(embed_bwd_pos_kernel<false>, pg, dim3(256), 0, st, (const uint16_t*)dx, dwpe, Bn, T, C);
   }
 }
 

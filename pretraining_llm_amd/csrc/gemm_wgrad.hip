@@ -20,13 +20,11 @@
 //    address instead;
 //  * both MFMA fragments come from ds_read_b64_tr_b16 transposed reads (the reduction
 //    index is the image row);
-//  * one slice: the tile is added straight into the bf16 gradient; several: fp32
-//    partial tiles go to a [S][P][Q] slab summed in a fixed slice order by wgrad_reduce_kernel
-//    (default), or the last workgroup of each tile to arrive
-//    (per-tile arrival counter, release/acquire fences) sums the slices in a fixed order
-//    into the bf16 gradient (deterministic, accumulate fused) -- no second launch, and the
-//    partials are re-read while still in the MALL.  That variant is an A/B switch
-//    (wgrad_set_mfma +1024) and measured slower than the default separate reduce pass.
+//  * one slice: the tile is added straight into the gradient (bf16 or fp32, the optimizer's
+//    gradient dtype); several: fp32 partial tiles go to a [S][P][Q] slab summed in a fixed
+//    slice order by wgrad_reduce_kernel (deterministic).  Measured and dropped in round 1: a
+//    4/5-slot staging ring (4-15 % slower, profiles/r1_wgrad_ring_ab.jsonl) and an in-kernel
+//    last-arriver reduction (1.0-3.2x slower, profiles/r1_wgrad_fused_reduce_negative.jsonl).
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include <type_traits>
 
@@ -71,31 +69,21 @@ constexpr int NT = 512;             // 8 waves
 constexpr int HALF = BKM * 128;     // elements of one [64][128] image
 constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 2,3 (64 KiB)
 
-// RING 0: 64-token stages in two slots (vmcnt(0) + barrier per stage, one stage of prefetch);
-// RING 1/2: 32-token stages in a 4/5-slot ring with 3/4 stages in flight across raw barriers
-// (counted vmcnt): more load latency covered per stage of MFMA work.  Measured 4-15 % SLOWER
-// than RING 0 on every GPT-2 / llama shape (profiles/r1_wgrad_ring_ab.jsonl): the extra
-// barriers cost more than the latency they hide, so RING 0 is the default.
-template <int MF, int RING>
+template <int MF, bool OF32>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
-                                                   int S, int slice, float* __restrict__ part,
-                                                   uint16_t* __restrict__ out, int accumulate, int g_prio,
-                                                   int* __restrict__ tile_cnt) {
-  constexpr int BK_ = RING == 0 ? BKM : 32;
-  constexpr int SLOTS = RING == 0 ? 2 : (RING == 1 ? 4 : 5);
-  constexpr int AHEAD = SLOTS - 1;
-  constexpr int HALF_ = BK_ * 128, STAGE_ = 4 * HALF_;
-  constexpr int QUADS = BK_ / 4;  // row-quads per image
-  constexpr int PPW = BK_ / 8;    // 1-KiB pieces per wave and stage
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[SLOTS * STAGE_];
+                                                   int S, int slice, float* __restrict__ part, void* __restrict__ out,
+                                                   int accumulate) {
+  constexpr int QUADS = BKM / 4;  // row-quads per image
+  constexpr int PPW = BKM / 8;    // 1-KiB pieces per wave and stage
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int s = lid / ntiles, t = lid % ntiles;
   const int p0 = (t / tiles_q) * BT, q0 = (t % tiles_q) * BT;
   const int m_begin = s * slice;
-  const int nstage = (min(M, m_begin + slice) - m_begin) / BK_;
+  const int nstage = (min(M, m_begin + slice) - m_begin) / BKM;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
   const int wp = w >> 2, wq = w & 3;  // wave's 128x64 sub-tile
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
@@ -113,23 +101,22 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
     const int col = half * 128 + (((lane & 15) ^ swz(row)) << 3);
     if (opnd == 0) src[k] = A + (int64_t)(m_begin + row) * lda + min(p0 + col, P - 8);
     else src[k] = B + (int64_t)(m_begin + row) * ldb + min(q0 + col, Q - 8);
-    dst[k] = (opnd * 2 + half) * HALF_ + quad * 512;
+    dst[k] = (opnd * 2 + half) * HALF + quad * 512;
   }
-  const int64_t astep = (int64_t)BK_ * lda, bstep = (int64_t)BK_ * ldb;
+  const int64_t astep = (int64_t)BKM * lda, bstep = (int64_t)BKM * ldb;
   const unsigned lds_base = (unsigned)(uintptr_t)smem;
   auto issue = [&](int st) {
-    const int slot = st % SLOTS;
+    const int slot = st & 1;
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
       const int opnd = (w * PPW + k) / (2 * QUADS);
       const uint16_t* g = src[k] + st * (opnd == 0 ? astep : bstep);
-      glds16(g, lds_base + 2u * (unsigned)(slot * STAGE_ + dst[k]));
+      glds16(g, lds_base + 2u * (unsigned)(slot * STAGE + dst[k]));
     }
   };
 
   // MF = 32: 4x2 v_mfma_f32_32x32x16_bf16 accumulators per wave (128x64 sub-tile);
-  // MF = 16: 8x4 v_mfma_f32_16x16x32_bf16 accumulators -- same LDS traffic per FLOP, but the
-  // 16x16 loop holds a higher clock under load (MI355X_MICROARCH 'DVFS give-back' item 7).
+  // MF = 16: 8x4 v_mfma_f32_16x16x32_bf16 accumulators -- same LDS traffic per FLOP.
   constexpr int NI = MF == 32 ? 4 : 8, NJ = MF == 32 ? 2 : 4;
   using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
   constexpr int NE = MF == 32 ? 16 : 4;
@@ -141,33 +128,18 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
-  if (g_prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // younger half: static priority (A/B: wgrad_set_mfma)
-#pragma unroll
-  for (int s0 = 0; s0 < AHEAD; ++s0)
-    if (s0 < nstage) issue(s0);
+  if (nstage > 0) issue(0);
   for (int st = 0; st < nstage; ++st) {
-    const int slot = st % SLOTS;
-    if constexpr (RING == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // stage st landed for every wave; nobody still reads the other slot
-    } else {
-      // retire stage st, keep the stages issued after it in flight across the barrier
-      const int pending = min(AHEAD - 1, nstage - 1 - st);
-      if (pending <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (pending == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else if (pending == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // stage st landed for every wave; slot of st-1 is free
-      asm volatile("" ::: "memory");
-    }
-    if (st + AHEAD < nstage) issue(st + AHEAD);
-    const uint16_t* Ai = smem + slot * STAGE_ + wp * HALF_;
-    const uint16_t* Bi = smem + slot * STAGE_ + (2 + (wq >> 1)) * HALF_;
+    const int slot = st & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage st landed for every wave; nobody still reads the other slot
+    if (st + 1 < nstage) issue(st + 1);
+    const uint16_t* Ai = smem + slot * STAGE + wp * HALF;
+    const uint16_t* Bi = smem + slot * STAGE + (2 + (wq >> 1)) * HALF;
     const int bcol = (wq & 1) * 64;
     if constexpr (MF == 32) {
 #pragma unroll
-      for (int k16 = 0; k16 < BK_ / 16; ++k16) {
+      for (int k16 = 0; k16 < BKM / 16; ++k16) {
         const int row = k16 * 16 + 8 * hh + tq;
         bf16x8 af[4], bfr[2];
 #pragma unroll
@@ -189,7 +161,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       // 16x16x32 operand: lane l holds column l%16, reduction rows 8*(l/16) .. +7
       const int gq = lane >> 4;
 #pragma unroll
-      for (int k32 = 0; k32 < BK_ / 32; ++k32) {
+      for (int k32 = 0; k32 < BKM / 32; ++k32) {
         const int row = k32 * 32 + 8 * gq + tq;
         bf16x8 af[8], bfr[4];
 #pragma unroll
@@ -215,7 +187,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   };
   auto qcol = [&](int j) { return MF == 32 ? q0 + wq * 64 + 32 * j + r : q0 + wq * 64 + 16 * j + (lane & 15); };
   if (S == 1) {
-    // single slice: add the tile straight into the bf16 gradient
+    // single slice: add the tile straight into the gradient
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
 #pragma unroll
@@ -225,12 +197,12 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int e = 0; e < NE; ++e) {  // all loads first (clamped, unconditional), then the stores
           const int p = min(prow(i, e), P - 1);
-          old[e] = accumulate ? bf2f(out[(int64_t)p * Q + qc]) : 0.f;
+          old[e] = accumulate ? ldg1<OF32>(out, (int64_t)p * Q + qc) : 0.f;
         }
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
           const int p = prow(i, e);
-          if (p < P && q < Q) out[(int64_t)p * Q + q] = f2bf_bits(acc[i][j][e] + old[e]);
+          if (p < P && q < Q) stg1<OF32>(out, (int64_t)p * Q + q, acc[i][j][e] + old[e]);
         }
       }
     }
@@ -250,51 +222,18 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       }
     }
   }
-  if (!tile_cnt) return;  // separate wgrad_reduce_kernel pass
-  // The last of the S workgroups of this tile to finish sums the S partial tiles in slice order
-  // (bit-identical to wgrad_reduce_kernel) while they are still in the MALL, saving the reduce
-  // launch and its HBM re-read.  Release: this workgroup's partial stores before its count;
-  // acquire: every wave of the last workgroup fences before reading the other slices' partials.
-  int* is_last = reinterpret_cast<int*>(smem);  // the staging ring is idle after the barrier below
-  __threadfence();
-  __syncthreads();
-  if (tid == 0) *is_last = atomicAdd(tile_cnt + t, 1) == S - 1;
-  __syncthreads();
-  if (!*is_last) return;
-  __threadfence();
-  const int64_t PQ = (int64_t)P * Q;
-  for (int c = tid; c < BT * (BT / 8); c += NT) {
-    const int p = p0 + c / (BT / 8), q = q0 + (c % (BT / 8)) * 8;
-    if (p >= P || q >= Q) continue;
-    const int64_t idx = (int64_t)p * Q + q;
-    float f[8];
-    if (accumulate) {
-      unpack8(ld16(out + idx), f);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) f[k] = 0.f;
-    }
-    for (int ss = 0; ss < S; ++ss) {
-      const f32x4* pp = reinterpret_cast<const f32x4*>(part + ss * PQ + idx);
-      const f32x4 a = pp[0], b = pp[1];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        f[k] += a[k];
-        f[4 + k] += b[k];
-      }
-    }
-    st16(out + idx, pack8(f));
-  }
 }
 
 // dW[p, q] (+)= sum_s slab[s][p][q]   (8 columns per thread, fixed slice order)
+template <bool OF32>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int S, int64_t PQ,
-                                                           uint16_t* __restrict__ out, int accumulate) {
+                                                           void* __restrict__ out, int accumulate) {
   const int64_t i = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) * 8;
   if (i >= PQ) return;
+  char* const o = reinterpret_cast<char*>(out) + i * (OF32 ? 4 : 2);
   float f[8];
   if (accumulate) {
-    unpack8(ld16(out + i), f);
+    ld8g<OF32>(o, f);
   } else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = 0.f;
@@ -308,7 +247,7 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
       f[4 + j] += b[j];
     }
   }
-  st16(out + i, pack8(f));
+  st8g<OF32>(o, f);
 }
 
 }  // namespace
@@ -318,27 +257,7 @@ namespace pllm {
 // MFMA shape of the wgrad main loop (16 or 32); 32x32 measured 0-6% faster on the GPT-2 shapes
 // (profiles/r1_wgrad_mfma_ab.jsonl), so it is the default
 static int g_wgrad_mfma = 32;
-// +64 on the argument: static s_setprio(1) for waves 4-7 (A/B switch)
-static int g_wgrad_prio = 0;
-static int g_wgrad_plan_fill = 0;  // A/B (+128): the older fill-efficiency-only split plan
-static int g_wgrad_ring = 0;       // A/B (+256 / +512): staging ring 1 / 2 (wgrad_kernel RING)
-// A/B (+1024): split-K slices summed in-kernel by the last workgroup of each tile instead of by
-// the separate wgrad_reduce_kernel.  Measured 1.0-3.2x SLOWER on every GPT-2 / llama shape
-// (profiles/r1_wgrad_fused_reduce_negative.jsonl): the sum of S slices of a tile lands on one
-// CU (9 of them for a 768x768 gradient) instead of spreading over the whole GPU, so the
-// separate pass stays the default.
-static int g_wgrad_split_reduce = 1;
-void wgrad_set_mfma(int mf) {
-  g_wgrad_split_reduce = (mf & 1024) ? 0 : 1;
-  mf &= 1023;
-  g_wgrad_ring = (mf & 512) ? 2 : ((mf & 256) ? 1 : 0);
-  mf &= 255;
-  g_wgrad_plan_fill = (mf & 128) ? 1 : 0;
-  mf &= 127;
-  g_wgrad_prio = mf >= 64 ? 1 : 0;
-  mf = mf >= 64 ? mf - 64 : mf;
-  g_wgrad_mfma = mf == 16 ? 16 : 32;
-}
+void wgrad_set_mfma(int mf) { g_wgrad_mfma = mf == 16 ? 16 : 32; }
 
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   // Split-K slice count from a cost model: rounds of 256 workgroups (one per CU) x stages per
@@ -354,14 +273,6 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
     if (s > 1 && kst / s < 8) break;
     const int n = ntiles * s;
     const int rounds = (n + 255) / 256;
-    if (g_wgrad_plan_fill) {
-      const double eff = (double)n / (256.0 * rounds);
-      if (eff > best_eff + 0.02) {
-        best_eff = eff;
-        best = s;
-      }
-      continue;
-    }
     const int st_per = (kst + s - 1) / s;
     double t = rounds * (double)st_per * 2.0e-6;
     if (s > 1) t += (double)P * Q * 4.0 * (2 * s + 1) / 4.0e12;
@@ -375,27 +286,27 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   *S = (kst + st_per - 1) / st_per;
 }
 
-int wgrad_fused_reduce() { return !g_wgrad_split_reduce; }
-
-// tile_cnt: ntiles zeroed ints when the slices are summed in-kernel (wgrad_fused_reduce()), else null
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool accumulate, int* tile_cnt, hipStream_t st) {
+           bool out_f32, bool accumulate, hipStream_t st) {
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
-#define PLLM_WGRAD_LAUNCH(MFV, RV)                                                                         \
-  hipLaunchKernelGGL((wgrad_kernel<MFV, RV>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda,   \
-                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, (uint16_t*)out, (int)accumulate, g_wgrad_prio, \
-                     S > 1 ? tile_cnt : nullptr)
-  if (g_wgrad_mfma == 16) PLLM_WGRAD_LAUNCH(16, 0);
-  else if (g_wgrad_ring == 1) PLLM_WGRAD_LAUNCH(32, 1);
-  else if (g_wgrad_ring == 2) PLLM_WGRAD_LAUNCH(32, 2);
-  else PLLM_WGRAD_LAUNCH(32, 0);
+#define PLLM_WGRAD_LAUNCH(MFV, OF)                                                                          \
+  hipLaunchKernelGGL((wgrad_kernel<MFV, OF>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda, \
+                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate)
+  if (g_wgrad_mfma == 16) {
+    if (out_f32) PLLM_WGRAD_LAUNCH(16, true);
+    else PLLM_WGRAD_LAUNCH(16, false);
+  } else {
+    if (out_f32) PLLM_WGRAD_LAUNCH(32, true);
+    else PLLM_WGRAD_LAUNCH(32, false);
+  }
 #undef PLLM_WGRAD_LAUNCH
-  if (S == 1 || tile_cnt) return;
+  if (S == 1) return;
   const int64_t PQ = (int64_t)P * Q;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((unsigned)((PQ / 8 + 255) / 256)), dim3(256), 0, st, part, S, PQ,
-                     (uint16_t*)out, (int)accumulate);
+  const dim3 rg((unsigned)((PQ / 8 + 255) / 256));
+  if (out_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rg, dim3(256), 0, st, part, S, PQ, out, (int)accumulate);
+  else hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rg, dim3(256), 0, st, part, S, PQ, out, (int)accumulate);
 }
 
 }  // namespace pllm

@@ -16,17 +16,6 @@ struct AttnFwdArgs {
   int causal;
 };
 
-// C[M, N] = A[M, K] . B[N, K]^T with fused MLP epilogues (gemm_nt.hip)
-struct GemmNTArgs {
-  const uint16_t *A, *B;
-  uint16_t* C;
-  uint16_t* aux;            // EPI 1: pre-activation out; EPI 2: pre-activation in
-  const uint16_t* bias;     // EPI 0/1 (optional)
-  float* part;              // EPI 2: [gemm_nt_part_rows(M), N] bias-gradient partials
-  int M, N, K;
-  int64_t lda, ldb, ldc;
-};
-
 // q [B, H, D] (one query per sequence), k/v rows of a [B, S_max, Hkv, D]-strided cache
 struct DecodeArgs {
   const uint16_t *q, *k, *v;
@@ -58,21 +47,23 @@ void norm_fwd(const void* x, const void* res, const void* w, const void* b, void
               float* rstd, int N, int C, float eps, bool rms, hipStream_t st);
 int norm_bwd_grid(int N);
 // xb_part/xb: optional column sums of dx (bias grad of the layer that produced x)
+// Gradient outputs (dw, db, xb, bias grads, wgrad, embedding grads) are bf16 or fp32 (grad_f32 /
+// out_f32: the optimizer's flat-gradient dtype); activations and their gradients are bf16.
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
-              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate,
-              float* xb_part, void* xb, bool xb_accumulate, hipStream_t st);
-// fp32 [G, C] slab -> bf16 [C] column sums (optionally added into out)
-void col_reduce(const float* part, int G, int C, void* out, bool accumulate, hipStream_t st);
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, bool grad_f32, int N, int C, bool rms,
+              bool accumulate, float* xb_part, void* xb, bool xb_accumulate, hipStream_t st);
+// fp32 [G, C] slab -> [C] column sums (bf16 or fp32 out; optionally added into out)
+void col_reduce(const float* part, int G, int C, void* out, bool out_f32, bool accumulate, hipStream_t st);
 // bias gradient = column sums of a bf16 [N, C] matrix; part: fp32 [colsum_groups(N), C] workspace
 int colsum_groups(int N);
-void bias_grad(const void* x, int N, int C, float* part, void* out, bool accumulate, hipStream_t st);
+void bias_grad(const void* x, int N, int C, float* part, void* out, bool out_f32, bool accumulate, hipStream_t st);
 
 // elementwise.hip (op: 0 relu, 1 gelu-tanh)
 void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st);
 void act_bwd(int op, const void* dy, const void* xin, void* dx, size_t n, hipStream_t st);
 // activation backward + fused bias gradient (column sums of dx) of the producing linear layer
 void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int C, float* part, void* bias_grad,
-                  bool accumulate, hipStream_t st);
+                  bool grad_f32, bool accumulate, hipStream_t st);
 void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st);
 void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st);
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
@@ -94,15 +85,14 @@ void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t N, int T, int C,
                    int pos_offset, int64_t V, hipStream_t st);
-void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, int64_t N,
-                   int Bn, int T, int C, int64_t V, hipStream_t st);
+void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, bool grad_f32,
+                   int64_t N, int Bn, int T, int C, int64_t V, hipStream_t st);
 
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad_set_mfma(int mf);
-int wgrad_fused_reduce();  // 1: split-K slices summed in-kernel (needs tile_cnt), 0: separate pass
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool accumulate, int* tile_cnt, hipStream_t st);
+           bool out_f32, bool accumulate, hipStream_t st);
 
 // transpose.hip: desc int64 [n][6] = (src, dst, rows, cols, first tile, tiles per row band)
 int transpose_tiles(int R, int C);
@@ -142,11 +132,6 @@ struct GemvArgs {
 };
 int gemv_max_rows();
 void gemv(const GemvArgs& a, hipStream_t st);
-
-// gemm_nt.hip
-int gemm_nt_part_rows(int M);
-void gemm_nt_set_pipe(int p);
-void gemm_nt(const GemmNTArgs& a, int epi, hipStream_t st);
 
 // attention.hip
 bool attn_supported_head_dim(int D);

@@ -8,6 +8,9 @@
 //   fwd:  s = x + r  (stored, bf16) ;  y = (s - mean) * rstd * w + b
 //   bwd:  dx = d(norm)/ds . dy + ds_next      (ds_next = grad of the residual stream)
 //
+// Gradients of the affine parameters are written/accumulated in the optimizer's gradient
+// dtype (bf16 or fp32, FlatAdamW grad_dtype); activations stay bf16.
+//
 // Layout / mapping: one wave64 per row, 8 bf16 (16 B) per lane per chunk, the
 // row held in registers between the two reduction passes (exact two-pass
 // variance, no E[x^2]-E[x]^2 cancellation).  dw/db are reduced per workgroup
@@ -211,11 +214,12 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
   if (XB) flush(xba, xb_part);
 }
 
-// column sums of an fp32 [G, C] slab -> bf16 [C].  One 1024-thread block per 64
-// columns: 16 waves each sum a strided subset of the G rows (coalesced 256 B per
+// column sums of an fp32 [G, C] slab -> [C] gradient (bf16 or fp32: OF32).  One 1024-thread
+// block per 64 columns: 16 waves each sum a strided subset of the G rows (coalesced 256 B per
 // wave-row), then a fixed-order LDS combine -> deterministic.
+template <bool OF32>
 __global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restrict__ part, int G, int C,
-                                                          uint16_t* __restrict__ out, int accumulate) {
+                                                          void* __restrict__ out, int accumulate) {
   __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, g0 = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + lane;
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restric
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s += red[i][lane];
-    out[c] = f2bf_bits(accumulate ? s + bf2f(out[c]) : s);
+    stg1<OF32>(out, c, accumulate ? s + ldg1<OF32>(out, c) : s);
   }
 }
 
@@ -299,14 +303,18 @@ int norm_bwd_grid(int N) {
   return g < 512 ? g : 512;
 }
 
-void col_reduce(const float* part, int G, int C, void* out, bool accumulate, hipStream_t st) {
-  hipLaunchKernelGGL(col_reduce_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, (uint16_t*)out,
-                     (int)accumulate);
+void col_reduce(const float* part, int G, int C, void* out, bool out_f32, bool accumulate, hipStream_t st) {
+  if (out_f32)
+    hipLaunchKernelGGL(col_reduce_kernel<true>, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, out,
+                       (int)accumulate);
+  else
+    hipLaunchKernelGGL(col_reduce_kernel<false>, dim3((C + 63) / 64), dim3(1024), 0, st, part, G, C, out,
+                       (int)accumulate);
 }
 
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
-              void* dx, float* dw_part, float* db_part, void* dw, void* db, int N, int C, bool rms, bool accumulate,
-              float* xb_part, void* xb, bool xb_accumulate, hipStream_t st) {
+              void* dx, float* dw_part, float* db_part, void* dw, void* db, bool grad_f32, int N, int C, bool rms,
+              bool accumulate, float* xb_part, void* xb, bool xb_accumulate, hipStream_t st) {
   const int G = norm_bwd_grid(N);
   const int K = (C + 511) / 512;
   const size_t lds = (size_t)4 * C * sizeof(float);
@@ -320,9 +328,9 @@ void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, c
   else if (K <= 4) { if (xbf) L(4, true); else L(4, false); }
   else { if (xbf) L(8, true); else L(8, false); }
 #undef L
-  col_reduce(dw_part, G, C, dw, accumulate, st);
-  if (db_part && db) col_reduce(db_part, G, C, db, accumulate, st);
-  if (xbf && xb) col_reduce(xb_part, G, C, xb, xb_accumulate, st);
+  col_reduce(dw_part, G, C, dw, grad_f32, accumulate, st);
+  if (db_part && db) col_reduce(db_part, G, C, db, grad_f32, accumulate, st);
+  if (xbf && xb) col_reduce(xb_part, G, C, xb, grad_f32, xb_accumulate, st);
 }
 
 int colsum_groups(int N) {
@@ -330,11 +338,11 @@ int colsum_groups(int N) {
   return g < 1 ? 1 : (g > 256 ? 256 : g);
 }
 
-void bias_grad(const void* x, int N, int C, float* part, void* out, bool accumulate, hipStream_t st) {
+void bias_grad(const void* x, int N, int C, float* part, void* out, bool out_f32, bool accumulate, hipStream_t st) {
   const int G = colsum_groups(N);
   hipLaunchKernelGGL(colsum_partial_kernel, dim3((C + 511) / 512, G), dim3(256), 0, st, (const uint16_t*)x, N, C,
                      part);
-  col_reduce(part, G, C, out, accumulate, st);
+  col_reduce(part, G, C, out, out_f32, accumulate, st);
 }
 
 }  // namespace pllm

@@ -9,7 +9,7 @@ Reference parity (Flink-ddd/pretraining-llm):
 
 MI355X-first structure (not a translation of the reference's per-head modules):
 * one packed QKV GEMM per layer (hipBLASLt) feeding a HIP flash-attention kernel that
-  reads Q/K/V strided out of it (RoPE applied in-kernel for llama);
+  reads Q/K/V strided out of it (llama: RoPE rotates the packed q/k heads first);
 * the residual add is fused into the next norm kernel: blocks pass ``(hidden, residual)``
   pairs so no standalone add kernel exists in forward or backward;
 * the LM head + cross-entropy writes dlogits during the forward (one pass over logits).
@@ -19,6 +19,7 @@ reference's per-head ``attn.heads.{h}.{key,query,value}.weight`` (+ ``tril``) la
 from __future__ import annotations
 
 import math
+import numbers
 from typing import Optional, Tuple
 
 import torch
@@ -28,6 +29,13 @@ from torch.utils.checkpoint import checkpoint
 
 from .. import ops
 from .config import ModelConfig
+
+
+def hbm_free_bytes(device) -> int:
+    """Free HBM as the caching allocator sees it: the driver's free bytes plus blocks the
+    allocator has reserved but holds no tensor in (an eval pass leaves such blocks behind)."""
+    free, _ = torch.cuda.mem_get_info(device)
+    return int(free + torch.cuda.memory_reserved(device) - torch.cuda.memory_allocated(device))
 
 
 class Norm(nn.Module):
@@ -297,15 +305,16 @@ class GPT(nn.Module):
         L = self.config.n_blocks
         if isinstance(mode, bool) or mode is None:
             return L if mode else 0
-        if isinstance(mode, float):
-            return min(L, max(0, math.ceil(mode * L)))
+        if isinstance(mode, numbers.Integral):  # e.g. --activation_checkpointing=1 from the CLI
+            return L if mode else 0
+        if isinstance(mode, numbers.Real):
+            return min(L, max(0, math.ceil(float(mode) * L)))
         if mode != "auto":
             raise ValueError(f"activation_checkpointing={mode!r}: expected bool, float fraction or 'auto'")
         if not idx.is_cuda:
             return 0
         if getattr(self, "_ckpt_auto", None) is None or self._ckpt_auto[0] != idx.numel():
-            free, _ = torch.cuda.mem_get_info(idx.device)
-            self._ckpt_auto = (idx.numel(), self.auto_checkpoint_blocks(idx.numel(), 0.5 * free))
+            self._ckpt_auto = (idx.numel(), self.auto_checkpoint_blocks(idx.numel(), 0.5 * hbm_free_bytes(idx.device)))
         return self._ckpt_auto[1]
 
     def auto_checkpoint_blocks(self, tokens: int, budget_bytes: float) -> int:

@@ -57,17 +57,17 @@ def _ops():
 # ---------------------------------------------------------------------------
 # Direct gradient accumulation.  When the optimizer owns a flat gradient
 # buffer (train/optim.py FlatAdamW marks its params ``_pllm_flat_grad``), the
-# backward kernels/GEMMs ADD their weight gradients straight into ``p.grad``
-# (a view of that buffer: hipBLASLt beta=1 epilogue, in-kernel read-add-write)
-# instead of returning a fresh tensor that autograd's AccumulateGrad would then
-# add in a separate pass.  ``_notify`` tells the data-parallel engine that a
-# contribution landed (it replaces the post-accumulate-grad hook for these).
+# backward kernels/GEMMs ADD their weight gradients straight into
+# ``p._pllm_gradbuf`` (a view of that buffer, fp32 by default: in-kernel
+# read-add-write epilogues) instead of returning a fresh tensor that autograd's
+# AccumulateGrad would then add in a separate pass.  ``_notify`` tells the
+# data-parallel engine that a contribution landed (it replaces the
+# post-accumulate-grad hook for these).
 # ---------------------------------------------------------------------------
 def _acc_target(p):
     if p is None or not getattr(p, "_pllm_flat_grad", False):
         return None
-    g = p.grad
-    return g if g is not None else None
+    return getattr(p, "_pllm_gradbuf", None)
 
 
 def _notify(p):
@@ -176,10 +176,12 @@ def _dgrad(dy, weight):
 
 
 def _weight_grad(dy2, x2, tgt):
-    """dW = dy2^T @ x2, added into ``tgt`` when given (returns None) else returned."""
-    use_hip = (WGRAD_ENGINE == "hip" and dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0
-               and dy2.shape[0] % 64 == 0
-               and (dy2.shape[0], dy2.shape[1], x2.shape[1]) not in WGRAD_BLAS_SHAPES)
+    """dW = dy2^T @ x2, added into ``tgt`` (bf16 or fp32) when given (returns None) else returned."""
+    hip_ok = dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.shape[0] % 64 == 0
+    f32_tgt = tgt is not None and tgt.dtype == torch.float32 and dy2.dtype != torch.float32
+    # an fp32 gradient target always takes the hand-written kernel (fp32 read-add-write epilogue)
+    use_hip = hip_ok and (f32_tgt or (WGRAD_ENGINE == "hip" and
+                                      (dy2.shape[0], dy2.shape[1], x2.shape[1]) not in WGRAD_BLAS_SHAPES))
     if use_hip:
         dy2, x2 = dy2.contiguous(), x2.contiguous()
         if tgt is not None:
@@ -187,7 +189,11 @@ def _weight_grad(dy2, x2, tgt):
             return None
         return _ops().wgrad(dy2, x2)
     if tgt is not None:
-        tgt.addmm_(dy2.t(), x2)
+        if f32_tgt:
+            tgt.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32) if dy2.is_cuda
+                     else dy2.t().float() @ x2.float())
+        else:
+            tgt.addmm_(dy2.t(), x2)
         return None
     return dy2.t() @ x2
 
@@ -643,7 +649,16 @@ class _LMHeadCEFn(torch.autograd.Function):
             if tgt is not None:
                 _notify(ctx.w)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = (dlogits.float().sum(0) * g).to(weight.dtype)
+            # column sums of dlogits by the colsum kernel (fp32 partials), never an fp32 copy
+            # of the [N, V] gradient
+            tgt = _acc_target(ctx.b)
+            col = _ops().bias_grad(dlogits, torch.zeros(dlogits.shape[1], dtype=torch.float32,
+                                                        device=dlogits.device))
+            if tgt is not None:
+                tgt.add_(col * g)
+                _notify(ctx.b)
+            else:
+                db = (col * g).to(weight.dtype)
         ctx.w = ctx.b = None
         return dh, dw, db, None, None
 

@@ -25,8 +25,10 @@ Layout (MI355X-first, built for RCCL over point-to-point xGMI):
   runs under bucket b+1's AdamW; the compute stream waits on all of them (no host sync);
 * gradient clipping: sum of squares of the owned reduced gradients, one scalar
   all-reduce, device-side clip coefficient;
-* ``state_dict``/``load_state_dict`` are COLLECTIVE: they gather/scatter the shards so the
-  checkpoint keeps FlatAdamW's (torch.optim.AdamW-shaped) single-file format.
+* ``state_dict`` is COLLECTIVE: the shards are all-gathered one bucket at a time into host
+  memory of the writing rank, so the checkpoint keeps FlatAdamW's (torch.optim.AdamW-shaped)
+  single-file format without any rank materialising the full state on its GPU;
+  ``load_state_dict`` copies each rank's owned parts straight out of the full file.
 """
 from __future__ import annotations
 
@@ -142,39 +144,66 @@ class ShardedFlatAdamW(FlatAdamW):
         self.refresh_shadows()
 
     # ------------------------------------------------------------------
-    def _gather_full(self, shard: torch.Tensor) -> torch.Tensor:
-        full = torch.zeros(self.total, dtype=shard.dtype, device=shard.device)
+    def _gather_full_cpu(self, shard: torch.Tensor, keep: bool) -> Optional[torch.Tensor]:
+        """All-gather a sharded fp32 state vector ONE BUCKET AT A TIME through a bucket-sized
+        device buffer into host memory (only on the rank that keeps it): no rank ever holds the
+        full unsharded state on its GPU, which is what ZeRO-1 exists to avoid."""
+        full = torch.zeros(self.total, dtype=shard.dtype) if keep else None
         for (bs, be), (fs, fe, o) in zip(self.buckets, self.own):
             n = fe - fs
             if self.world > 1:
-                dist.all_gather_into_tensor(full[bs:be], shard[o:o + n].contiguous(), group=self.pg)
+                tmp = torch.empty(be - bs, dtype=shard.dtype, device=shard.device)
+                dist.all_gather_into_tensor(tmp, shard[o:o + n].contiguous(), group=self.pg)
             else:
-                full[bs:be].copy_(shard[o:o + n])
+                tmp = shard[o:o + n]
+            if keep:
+                full[bs:be].copy_(tmp)
         return full
 
-    @contextlib.contextmanager
-    def _full_state(self):
+    def state_dict(self, writer_rank: int = 0) -> dict:
+        """COLLECTIVE: every rank must call it.  Returns the full (unsharded) AdamW-format state
+        on ``writer_rank`` (in host memory) and ``{}`` elsewhere."""
+        keep = self.rank == writer_rank
+        full = [self._gather_full_cpu(t, keep) for t in (self.master, self.exp_avg, self.exp_avg_sq)]
+        if not keep:
+            return {}
         saved = (self.master, self.exp_avg, self.exp_avg_sq)
-        self.master, self.exp_avg, self.exp_avg_sq = (self._gather_full(t) for t in saved)
+        self.master, self.exp_avg, self.exp_avg_sq = full
         try:
-            yield
-        finally:
-            full = (self.master, self.exp_avg, self.exp_avg_sq)
-            self.master, self.exp_avg, self.exp_avg_sq = saved
-            for dst, src in zip(saved, full):
-                for fs, fe, o in self.own:
-                    dst[o:o + fe - fs].copy_(src[fs:fe])
-
-    def state_dict(self) -> dict:
-        """COLLECTIVE: every rank must call it; returns the full (unsharded) state on every rank."""
-        with self._full_state():
             return super().state_dict()
+        finally:
+            self.master, self.exp_avg, self.exp_avg_sq = saved
 
     @torch.no_grad()
     def load_state_dict(self, sd: dict):
-        """COLLECTIVE: every rank loads the same full state and keeps its own shard."""
-        with self._full_state():
-            super().load_state_dict(sd)
+        """Every rank reads the same full state and copies only the parts it owns (no collective,
+        no unsharded device copy)."""
+        st = sd["state"]
+        steps = []
+        for i, p in enumerate(self.params):
+            if i not in st and str(i) not in st:
+                continue
+            e = st[i] if i in st else st[str(i)]
+            o, n = self.offsets[i], p.numel()
+            src = {k: e[k].reshape(-1).to(self.master.device, torch.float32)
+                   for k in ("exp_avg", "exp_avg_sq", "master") if k in e}
+            if "master" not in src:
+                src["master"] = self.flat_param[o:o + n].float()
+            for fs, fe, so in self.own:
+                lo, hi = max(o, fs), min(o + n, fe)
+                if lo >= hi:
+                    continue
+                for name, dst in (("master", self.master), ("exp_avg", self.exp_avg),
+                                  ("exp_avg_sq", self.exp_avg_sq)):
+                    dst[so + lo - fs:so + hi - fs].copy_(src[name][lo - o:hi - o])
+            self.flat_param[o:o + n].copy_(src["master"].to(self.flat_param.dtype))
+            steps.append(float(e["step"]))
+        if steps:
+            self.step_count = int(max(steps))
+        if sd.get("param_groups"):
+            self.param_groups[0]["lr"] = sd["param_groups"][0].get("lr", self.lr)
+            self._sync_lr()
+        self.refresh_shadows()
 
     @torch.no_grad()
     def sync_master_from_params(self):

@@ -9,9 +9,16 @@ MI355X-first layout instead:
 * all parameters live in ONE contiguous buffer in the compute dtype (bf16 on
   the GPU); each ``nn.Parameter`` becomes a view into it, every segment 16-byte
   aligned;
-* all gradients live in ONE contiguous buffer (``p.grad`` are views), so the
-  data-parallel engine reduces contiguous buckets with no packing copies and
-  zero_grad is one memset;
+* all gradients live in ONE contiguous buffer, fp32 by default (``grad_dtype``),
+  so the data-parallel engine reduces contiguous buckets with no packing copies and
+  zero_grad is one memset.  Like the reference (fp32 params under bf16 autocast ->
+  fp32 ``.grad``, fp32 DDP all-reduce: scripts/train_transformer.py:66-69,122-126),
+  micro-step accumulation, the tied embedding's two gradient pieces and the DP sum
+  are all kept in fp32.  The backward kernels add straight into that buffer
+  (``p._pllm_gradbuf``, see ops._acc_target); where grad and param dtypes agree it is
+  also ``p.grad``, otherwise (bf16 params, fp32 grads -- torch forbids a ``.grad``
+  of another dtype) any gradient autograd still produces is folded into the buffer
+  by a post-accumulate hook and released;
 * fp32 master weights and the two moments are flat fp32 buffers; one HIP
   kernel per param group (``torch.ops.pllm.adamw_``) reads the gradient,
   updates master/m/v and writes the bf16 compute weights in the same pass;
@@ -80,16 +87,23 @@ class FlatAdamW:
         dev = params[0].device
         pdtype = params[0].dtype
         self.param_dtype = pdtype
-        self.grad_dtype = grad_dtype or pdtype
+        self.grad_dtype = grad_dtype or torch.float32
         self.flat_param = torch.zeros(total, dtype=pdtype, device=dev)
         self.flat_grad = torch.zeros(total, dtype=self.grad_dtype, device=dev)
+        self.grad_is_param_grad = self.grad_dtype == pdtype
+        self._fold_hooks = []
         for i, p in enumerate(params):
             o = self.offsets[i]
             seg = self.flat_param[o:o + p.numel()].view_as(p)
             seg.copy_(p.data)
             p.data = seg
-            p.grad = self.flat_grad[o:o + p.numel()].view_as(p)
-            p._pllm_flat_grad = True  # backward kernels may add straight into p.grad (ops._acc_target)
+            p._pllm_gradbuf = self.flat_grad[o:o + p.numel()].view_as(p)
+            p._pllm_flat_grad = True  # backward kernels add straight into p._pllm_gradbuf (ops._acc_target)
+            if self.grad_is_param_grad:
+                p.grad = p._pllm_gradbuf
+            else:
+                p.grad = None
+                self._fold_hooks.append(p.register_post_accumulate_grad_hook(_fold_grad))
         self.master = self.flat_param.float() if pdtype != torch.float32 else self.flat_param.clone()
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
@@ -152,8 +166,11 @@ class FlatAdamW:
         # set_to_none is ignored on purpose: grads are views into the flat buffer
         self.flat_grad.zero_()
         for i, p in enumerate(self.params):
-            if p.grad is None or p.grad.data_ptr() != self.grad_view(i).data_ptr():
-                p.grad = self.grad_view(i).view_as(p)
+            if self.grad_is_param_grad:
+                if p.grad is None or p.grad.data_ptr() != self.grad_view(i).data_ptr():
+                    p.grad = self.grad_view(i).view_as(p)
+            else:
+                p.grad = None
 
     def _sync_lr(self):
         self.lr = self.param_groups[0]["lr"]
@@ -177,9 +194,23 @@ class FlatAdamW:
         bc2 = 1.0 - b2 ** self.step_count
         if getattr(self, "hyper", None) is None:
             self.hyper = torch.zeros(4, dtype=torch.float32, device=self.flat_param.device)
-            self._hyper_host = torch.zeros(4, dtype=torch.float32).pin_memory()
-        self._hyper_host.copy_(torch.tensor([lr, 1.0 / bc1, 1.0 / math.sqrt(bc2), 0.0]))
-        self.hyper.copy_(self._hyper_host, non_blocking=True)
+            # a ring of pinned staging buffers, each guarded by the event of the H2D copy that
+            # last read it: the host may run several steps ahead of the GPU (graph replays are
+            # asynchronous) and must never overwrite a buffer whose copy is still queued
+            self._hyper_ring = [torch.zeros(4, dtype=torch.float32).pin_memory() for _ in range(4)]
+            self._hyper_ev = [None] * 4
+            self._hyper_i = 0
+        i = self._hyper_i
+        self._hyper_i = (i + 1) % len(self._hyper_ring)
+        if self._hyper_ev[i] is not None:
+            self._hyper_ev[i].synchronize()
+        host = self._hyper_ring[i]
+        host.copy_(torch.tensor([lr, 1.0 / bc1, 1.0 / math.sqrt(bc2), 0.0]))
+        self.hyper.copy_(host, non_blocking=True)
+        if self.hyper.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record()
+            self._hyper_ev[i] = ev
 
     def step(self, grad_scale: float = 1.0, graph: bool = False):
         """One AdamW step. ``grad_scale`` multiplies the raw flat gradient (e.g. 1/world for a
@@ -266,6 +297,14 @@ class FlatAdamW:
         """Call after loading model weights directly into the params."""
         self.master.copy_(self.flat_param.float())
         self.refresh_shadows()
+
+
+def _fold_grad(p):
+    """Post-accumulate hook (grad dtype != param dtype): add the gradient autograd produced
+    for ``p`` into its slot of the flat gradient buffer and release it."""
+    if p.grad is not None:
+        p._pllm_gradbuf.add_(p.grad)
+        p.grad = None
 
 
 def no_decay_1d(name: str, p: torch.Tensor) -> bool:

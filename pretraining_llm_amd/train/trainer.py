@@ -265,7 +265,7 @@ class Trainer:
         osd = self.opt.state_dict() if getattr(self.opt, "collective_state", False) else None
         if self.di.is_master:
             save_checkpoint(path, self.model, self.opt if osd is None else None, step=self.step, config=self.cfg,
-                            data_state=data_state, optimizer_state=osd)
+                            data_state=data_state, optimizer_state=osd, params=self.opt.params)
             self.log(f"saved checkpoint to {path} (step {self.step})")
         if dist.is_initialized():
             dist.barrier()

@@ -8,8 +8,9 @@ readiness counting learned on the first backward, in-order bucket launch from ho
 the tied-embedding two-piece gradient, the 1/world scale and the init broadcast --
 not the transport; RCCL over xGMI is exercised by the driver's multi-GPU bench.
 
-Checks (bf16 kernels, so tolerances are bf16-sized):
-* DP gradient == single-process gradient of the concatenated batch;
+Checks:
+* DP gradient == single-process gradient of the concatenated batch, at fp32 level: both sum
+  the same per-rank fp32 gradients (FlatAdamW's default fp32 flat gradient, fp32 all-reduce);
 * replicas stay bit-identical after several optimizer steps (SURVEY.md D5 regression).
 """
 import os
@@ -120,7 +121,7 @@ def test_dp_engine_on_hip_kernels():
     for k in ("g0", "g1"):
         got = out[k]
         err = (got - ref).abs().max().item()
-        assert err <= 2e-2 * ref.abs().max().item() + 1e-4, (k, err)
+        assert err <= 1e-6 * ref.abs().max().item(), (k, err)
         # the overlapped (hook-launched) iteration reduces exactly what the end-of-backward one did
     assert torch.equal(out["g0"], out["g1"])
     for step_sums in out["sums"]:

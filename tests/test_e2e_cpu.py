@@ -160,3 +160,36 @@ def test_lr_schedule_reference_semantics():
     assert lr_at(100, cfg) == 1e-3 and lr_at(999, cfg) == 1e-3
     step = dict(cfg, lr_schedule="step", t_lr_decay_step=500, t_lr_decayed=1e-4)
     assert lr_at(499, step) == 1e-3 and lr_at(500, step) == 1e-4
+
+
+def test_checkpoint_model_weights_are_fp32_masters(tmp_path):
+    """A bf16-trained model's checkpoint carries fp32 weights taken from the optimizer's masters
+    (reference saves its fp32 model, scripts/train_transformer.py:106-108); loading them into a
+    bf16 model reproduces the bf16 compute weights bit-exactly (reference arch: per-head split
+    keys included)."""
+    import torch
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    from pretraining_llm_amd.utils.checkpoint import load_checkpoint, save_checkpoint
+    for preset in ("gpt2-tiny", "ref-small"):
+        cfg = get_preset(preset).replace(vocab_size=256, context_length=32, n_embed=64, n_head=2, n_blocks=2)
+        torch.manual_seed(0)
+        m = GPT(cfg).to(torch.bfloat16)
+        opt = FlatAdamW(m, lr=1e-2)
+        x = torch.randint(0, 256, (2, 32))
+        for _ in range(2):
+            _, loss = m(x, x.roll(-1, 1))
+            loss.backward()
+            opt.step()
+            opt.zero_grad()
+        path = save_checkpoint(str(tmp_path / f"{preset}.pt"), m, opt, step=2)
+        sd = load_checkpoint(path)["model_state_dict"]
+        floats = {k: v for k, v in sd.items() if v.is_floating_point() and not k.endswith("tril")}
+        assert all(v.dtype == torch.float32 for v in floats.values())
+        # fp32 values are NOT all bf16-representable: they are the masters, not the compute copy
+        assert any(not torch.equal(v, v.bfloat16().float()) for v in floats.values())
+        m2 = GPT(cfg).to(torch.bfloat16)
+        m2.load_state_dict(sd)
+        for (n, a), b in zip(m.named_parameters(), m2.parameters()):
+            assert torch.equal(a, b), n
+        assert m.token_embed.weight.dtype == torch.bfloat16  # the live model was restored

@@ -302,38 +302,6 @@ def test_attention_decode_kernel(D, H, Hkv, B, S):
     assert torch.equal(o2, o) or _rel(o2, ref_o) < 1e-2
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
-@pytest.mark.parametrize("M,N,K", [(1000, 776, 128), (512, 3072, 768), (300, 256, 3072)])
-def test_gemm_nt_epilogues(pipe, M, N, K):
-    """NT GEMM (csrc/gemm_nt.hip) vs fp32 torch: plain + bias, GELU with pre-activation
-    output, dGELU with the bias-gradient column sums (ragged M and N edges included)."""
-    torch.manual_seed(M + N)
-    ops = _ops()
-    ops.gemm_nt_set_pipe(pipe)
-    try:
-        a = torch.randn(M, K, device=DEV, dtype=torch.bfloat16)
-        b = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
-        bias = torch.randn(N, device=DEV, dtype=torch.bfloat16) * 0.1
-        ref = a.float() @ b.float().t()
-        (c0,) = ops.gemm_nt(a, b, None, 0)
-        assert _rel(c0, ref) < 5e-3
-        (c0b,) = ops.gemm_nt(a, b, bias, 0)
-        assert _rel(c0b, ref + bias.float()) < 5e-3
-        g, h = ops.gemm_nt(a, b, bias, 1)
-        href = ref + bias.float()
-        assert _rel(h, href) < 5e-3
-        assert _rel(g, F.gelu(h.float(), approximate="tanh")) < 5e-3
-        bg = torch.full((N,), 0.25, device=DEV, dtype=torch.bfloat16)   # accumulates into it
-        (dh,) = ops.gemm_nt(a, b, None, 2, h, bg)
-        hf = h.float().requires_grad_()
-        gl = F.gelu(hf, approximate="tanh")
-        (dref,) = torch.autograd.grad(gl, hf, ref)
-        assert _rel(dh, dref) < 1e-2
-        assert _rel(bg.float() - 0.25, dh.float().sum(0)) < 1e-2
-    finally:
-        ops.gemm_nt_set_pipe(0)
-
-
 @pytest.mark.parametrize("M", [1, 2, 3, 5, 8])
 @pytest.mark.parametrize("N,K", [(777, 768), (2000, 512), (3072, 768), (768, 3072), (9000, 256), (50304, 768)])
 def test_gemv_skinny_gemm(M, N, K):
@@ -463,29 +431,6 @@ def test_model_hip_matches_reference_path():
         assert _rel(g1[n], p.grad) < 6e-2, n
 
 
-def test_gemv_kv_cache_append():
-    """QKV decode projection appends its K/V columns to the caches at the device position;
-    other cache rows stay untouched and an out-of-range position writes nothing."""
-    torch.manual_seed(3)
-    B, S, Hkv, D, H, K = 3, 16, 2, 64, 4, 256
-    N = (H + 2 * Hkv) * D
-    x = torch.randn(B, K, device=DEV, dtype=torch.bfloat16)
-    w = torch.randn(N, K, device=DEV, dtype=torch.bfloat16) * K ** -0.5
-    g = torch.ones(K, device=DEV, dtype=torch.bfloat16)
-    kc = torch.zeros(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
-    vc = torch.zeros_like(kc)
-    pos = torch.tensor([5], device=DEV)
-    y = _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, pos, H * D)[0]
-    assert torch.equal(kc[:, 5].reshape(B, -1), y[:, H * D:(H + Hkv) * D])
-    assert torch.equal(vc[:, 5].reshape(B, -1), y[:, (H + Hkv) * D:])
-    kc[:, 5] = 0
-    vc[:, 5] = 0
-    assert not kc.any() and not vc.any()
-    _ops().gemv(x, w, None, None, g, None, 1e-5, 1, 0, kc, vc, torch.tensor([S], device=DEV), H * D)
-    torch.cuda.synchronize()
-    assert not kc.any() and not vc.any()
-
-
 @pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny", "ref-small"])
 def test_model_direct_grad_accumulation_matches_reference(preset):
     """With FlatAdamW the HIP backward adds weight/bias gradients straight into the flat buffer
@@ -538,6 +483,15 @@ def test_bias_grad_kernels():
     torch.nn.functional.gelu(xf, approximate="tanh").backward(d.float())
     assert _rel(dx, xf.grad) < 1e-2
     assert _rel(b, xf.grad.sum(0)) < 1e-2
+    # fp32 targets: sums of the bf16 values added in fp32
+    acc32 = torch.randn(2304, device=DEV)
+    ref32 = acc32.double() + dy.double().sum(0)
+    torch.ops.pllm.bias_grad(dy, acc32)
+    assert _rel(acc32.double(), ref32) < 1e-6
+    b32 = torch.zeros(3072, device=DEV)
+    dx2 = torch.ops.pllm.act_bwd_bias(d, x, 1, b32)
+    assert torch.equal(dx2, dx)
+    assert _rel(b32.double(), dx.double().sum(0)) < 1e-6
 
 
 # (2048, 200, 136): tiles past P and Q; (4096, 768, 768) / (2048, 512, 2304): split-K slab path;
@@ -551,19 +505,22 @@ def test_wgrad_kernel(M, P, Q):
     ref = dy.float().t() @ x.float()
     out = torch.ops.pllm.wgrad(dy, x)
     assert _rel(out, ref) < 5e-3, _rel(out, ref)
-    # the in-kernel split-K reduction (A/B variant: last workgroup of a tile) is bit-identical
-    # to the default separate pass
-    try:
-        torch.ops.pllm.wgrad_set_mfma(32 + 1024)
-        out_sep = torch.ops.pllm.wgrad(dy, x)
-    finally:
-        torch.ops.pllm.wgrad_set_mfma(32)
-    assert torch.equal(out, out_sep)
     assert torch.equal(out, torch.ops.pllm.wgrad(dy, x))  # deterministic across calls
     acc = torch.randn(P, Q, device=DEV).bfloat16()
     ref2 = acc.float() + ref
     torch.ops.pllm.wgrad(dy, x, acc)
     assert _rel(acc, ref2) < 5e-3
+    # fp32 gradient target (FlatAdamW's default): accumulated in fp32, error at fp32 level
+    acc32 = torch.randn(P, Q, device=DEV)
+    ref3 = acc32.double() + dy.double().t() @ x.double()
+    torch.ops.pllm.wgrad(dy, x, acc32)
+    assert _rel(acc32.double(), ref3) < 1e-5, _rel(acc32.double(), ref3)
+    # the 16x16x32 MFMA variant computes the same product
+    try:
+        torch.ops.pllm.wgrad_set_mfma(16)
+        assert _rel(torch.ops.pllm.wgrad(dy, x), ref) < 5e-3
+    finally:
+        torch.ops.pllm.wgrad_set_mfma(32)
     # strided (non-contiguous rows) operands, e.g. a column slice of a packed buffer
     big = torch.randn(M, P + 64, device=DEV).bfloat16()
     v = big[:, 32:32 + P]
@@ -713,3 +670,102 @@ def test_batched_transpose_kernel():
     with pytest.raises(RuntimeError):
         _ops().transpose_plan([torch.randn(12, 20, device=DEV).bfloat16()],
                               [torch.empty(20, 12, device=DEV, dtype=torch.bfloat16)])
+
+
+def test_norm_and_embedding_fp32_grad_targets():
+    """norm backward / embedding backward add their parameter gradients into fp32 targets (the
+    optimizer's default flat-gradient dtype) at fp32 accuracy."""
+    torch.manual_seed(25)
+    N, C = 1000, 768
+    x = torch.randn(N, C, device=DEV).bfloat16()
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16()
+    b = (0.1 * torch.randn(C, device=DEV)).bfloat16()
+    y, s, mean, rstd = _ops().norm_fwd(x, None, w, b, 1e-5, False)
+    dy = torch.randn(N, C, device=DEV).bfloat16()
+    dx16, dw16, db16 = _ops().norm_bwd(dy, s, w, mean, rstd, None, True, False)
+    dw32 = torch.full((C,), 0.5, device=DEV)
+    db32 = torch.full((C,), -0.5, device=DEV)
+    xb32 = torch.zeros(C, device=DEV)
+    (dx32,) = _ops().norm_bwd(dy, s, w, mean, rstd, None, True, False, dw32, db32, xb32)
+    assert torch.equal(dx32, dx16)
+    xh = (s.double() - mean.double()[:, None]) * rstd.double()[:, None]
+    assert _rel(dw32.double() - 0.5, (dy.double() * xh).sum(0)) < 1e-4
+    assert _rel(db32.double() + 0.5, dy.double().sum(0)) < 1e-6
+    assert _rel(xb32.double(), dx32.double().sum(0)) < 1e-6
+    # embedding
+    V, T, B = 500, 64, 8
+    wte = torch.randn(V, C, device=DEV).bfloat16()
+    wpe = torch.randn(T, C, device=DEV).bfloat16()
+    idx = torch.randint(0, 40, (B, T), device=DEV)
+    d = torch.randn(B, T, C, device=DEV).bfloat16()
+    gte = torch.ones(V, C, device=DEV)
+    gpe = torch.ones(T, C, device=DEV)
+    _ops().embedding_bwd(d, idx, V, T, True, gte, gpe)
+    ref_te = torch.ones(V, C, device=DEV, dtype=torch.float64).index_add_(0, idx.reshape(-1), d.double().reshape(-1, C))
+    assert _rel(gte.double(), ref_te) < 1e-6
+    assert _rel(gpe.double(), 1 + d.double().sum(0)) < 1e-6
+
+
+def test_fp32_grad_accumulation_matches_big_batch():
+    """8 micro-steps of batch 1 accumulated into the fp32 flat gradient == one step of batch 8
+    (HIP path), to within what bf16 activations allow; and the fp32 buffer reproduces the
+    bf16-gradient run's accumulation error with far less drift."""
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    cfg = get_preset("gpt2-tiny").replace(context_length=128, vocab_size=1024)
+    x = torch.randint(0, 1024, (8, 128), device=DEV)
+    y = torch.randint(0, 1024, (8, 128), device=DEV)
+    errs = {}
+    for gd in (torch.float32, torch.bfloat16):
+        torch.manual_seed(26)
+        m = GPT(cfg).to(DEV, torch.bfloat16)
+        opt = FlatAdamW(m, lr=1e-3, grad_dtype=gd)
+        assert opt.flat_grad.dtype == gd
+        _, loss = m(x, y, return_logits=False)
+        loss.backward()
+        big = opt.flat_grad.double().clone()
+        opt.zero_grad()
+        for i in range(8):
+            _, loss = m(x[i:i + 1], y[i:i + 1], return_logits=False)
+            loss.backward()
+        acc = opt.flat_grad.double() / 8
+        errs[gd] = _rel(acc, big)
+    assert errs[torch.float32] < 1e-2, errs
+    assert errs[torch.float32] <= errs[torch.bfloat16], errs
+
+
+def test_graphed_steps_without_host_sync_match_eager():
+    """Several hipGraph replays queued back to back with NO host synchronisation in between
+    (the host runs ahead of the GPU) reproduce eager steps: each replay must read its own
+    step's lr / bias corrections (FlatAdamW.prepare_graph_step's guarded staging ring)."""
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.parallel.dp import DataParallelEngine
+    from pretraining_llm_amd.train.graph import GraphedTrainStep
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    cfg = get_preset("gpt2-tiny").replace(context_length=128, vocab_size=1024, n_head=2)
+    xs = [torch.randint(0, 1024, (4, 128), device=DEV) for _ in range(10)]
+    lrs = [1e-3 * (1 + 0.3 * i) for i in range(10)]
+
+    def make():
+        torch.manual_seed(27)
+        m = GPT(cfg).to(DEV, torch.bfloat16)
+        o = FlatAdamW(m, lr=1e-3, max_grad_norm=1.0)
+        return m, o, DataParallelEngine(o)
+
+    m1, o1, e1 = make()
+    g = GraphedTrainStep(m1, o1, e1, 4, 128, torch.device(DEV), warmup=1).capture(xs[0], xs[0].roll(-1, 1), lrs[0])
+    losses = [g(xs[i], xs[i].roll(-1, 1), lrs[i]).clone() for i in range(1, 10)]  # no sync in between
+    torch.cuda.synchronize()
+    m2, o2, e2 = make()
+    ref = []
+    for i in range(10):
+        o2.param_groups[0]["lr"] = lrs[i]
+        _, loss = m2(xs[i], xs[i].roll(-1, 1), return_logits=False)
+        loss.backward()
+        o2.step(grad_scale=e2.finish_grad_sync())
+        o2.zero_grad()
+        ref.append(loss.item())
+    got = [l.item() for l in losses]
+    for a, b in zip(got, ref[1:]):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (got, ref)
+    assert _rel(o1.master, o2.master) < 1e-4

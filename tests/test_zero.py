@@ -78,6 +78,10 @@ def _worker(rank, world, port, outdir, accum):
     out = {"diff": (o_ref.flat_param[:o_ref.total] - o_z.flat_param[:o_ref.total]).abs().max().item(),
            "shard_frac": o_z.master.numel() / o_z.total, "nbuckets": len(o_z.buckets)}
     sd_ref, sd_z = o_ref.state_dict(), o_z.state_dict()  # collective for the sharded one
+    out["writer_only"] = (rank == 0) == bool(sd_z)  # full state on the writer rank only
+    box = [sd_z]
+    dist.broadcast_object_list(box, src=0)
+    sd_z = box[0]
     out["sd_diff"] = max((sd_ref["state"][i][k] - sd_z["state"][i][k]).abs().max().item()
                          for i in sd_ref["state"] for k in ("exp_avg", "exp_avg_sq", "master"))
     # resume: fresh sharded optimizer loaded from the consolidated state continues identically
@@ -108,6 +112,7 @@ def _check(res, world):
     for r in res:
         assert r["diff"] < 1e-4, r  # grad-norm summation order differs (shard sums + all-reduce)
         assert r["sd_diff"] < 1e-4, r
+        assert r["writer_only"], r
         assert r["resume_diff"] == 0.0, r
         assert abs(r["shard_frac"] - 1.0 / world) < 1e-9
         assert r["nbuckets"] > 2
