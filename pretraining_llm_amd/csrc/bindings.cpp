@@ -371,8 +371,10 @@ void scale_(Tensor& x, const Tensor& s) {
 // ---------------------------------------------------------------- cross entropy
 // returns per-row losses (fp32, 0 for ignored rows); if dlogits is given it is
 // overwritten with d(mean loss)/dlogits (it may alias logits).
+// ``inv_n``: optional fp32 [1] device scalar scaling dlogits (1 / #valid targets of the WHOLE
+// batch when the rows are processed in chunks); default 1 / #valid targets of these rows.
 Tensor cross_entropy(const Tensor& logits, const Tensor& targets, const std::optional<Tensor>& dlogits,
-                     int64_t ignore_index) {
+                     int64_t ignore_index, const std::optional<Tensor>& inv_n_opt) {
   check_bf16(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "logits must be [N, V] with unit column stride");
   const int64_t N = logits.size(0), V = logits.size(1);
@@ -386,7 +388,14 @@ Tensor cross_entropy(const Tensor& logits, const Tensor& targets, const std::opt
     TORCH_CHECK(dlogits->sizes() == logits.sizes() && dlogits->strides() == logits.strides(), "dlogits layout");
   }
   Tensor loss = at::empty({N}, logits.options().dtype(at::kFloat));
-  Tensor inv_n = (tg != ignore_index).sum().to(at::kFloat).clamp_min(1.0).reciprocal().reshape({1});
+  Tensor inv_n;
+  if (inv_n_opt) {
+    TORCH_CHECK(inv_n_opt->is_cuda() && inv_n_opt->scalar_type() == at::kFloat && inv_n_opt->numel() == 1,
+                "cross_entropy: inv_n must be a 1-element fp32 device tensor");
+    inv_n = inv_n_opt->reshape({1});
+  } else {
+    inv_n = (tg != ignore_index).sum().to(at::kFloat).clamp_min(1.0).reciprocal().reshape({1});
+  }
   if (N)
     pllm::cross_entropy(logits.data_ptr(), logits.stride(0), tg.data_ptr<int64_t>(), (int)N, (int)V, (int)ignore_index,
                         loss.data_ptr<float>(), dlogits ? dlogits->data_ptr() : nullptr, inv_n.data_ptr<float>(),
@@ -703,7 +712,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse, bool inplace) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
-  m.def("cross_entropy(Tensor logits, Tensor targets, Tensor? dlogits, int ignore_index) -> Tensor");
+  m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");

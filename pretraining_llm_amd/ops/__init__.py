@@ -619,56 +619,120 @@ def embedding(idx, wte, wpe=None, pos_offset: int = 0):
 
 
 # ---------------------------------------------------------------------------
-# LM head + fused cross entropy.  The HIP kernel computes the per-row loss AND
-# overwrites the logits buffer with d(mean loss)/dlogits in the same pass, so
-# the training step never holds probabilities or a second logits-sized buffer;
-# the backward is two GEMMs on the stored gradient.
+# LM head + fused cross entropy, chunked over rows.
+# The reference materialises [B*T, V] fp32 logits and a softmax (transformer.py:71-77:
+# 3+ GiB at its own config).  Here the rows are processed in chunks of CE_CHUNK_ROWS:
+# per chunk the LM-head GEMM writes bf16 logits into ONE reused [rows, V] workspace, the
+# HIP CE kernel turns them in place into dlogits (never storing probabilities), and the
+# two backward GEMMs (dh = dlogits W, dW += dlogits^T h) plus the head-bias column sums
+# run right away on the same workspace while it is hot.  Nothing logits-sized outlives a
+# chunk; the backward only scales the saved dh / fp32 dW / db by the upstream gradient.
 # ---------------------------------------------------------------------------
+# Chunk size: the fewest equal chunks (multiples of 64 rows) whose bf16 logits workspace fits
+# CE_WORKSPACE_MB, or exactly CE_CHUNK_ROWS rows when that is set.  Measured on MI355X
+# (GPT-2 small, 65,536 rows x 50,304, profiles/r2_ce_chunk_sweep.jsonl): 63.4 ms/step unchunked
+# (29.9 GB peak) vs 64.5 / 65.3 / 70.6 / 73.8 ms at 16K / 8K / 4K / 2K rows (24.8-23.1 GB): the
+# backward GEMMs lose efficiency at small M, so the default budget (8 GiB) keeps every shipped
+# config in one chunk and only bounds the workspace when batch x vocab grows past it.
+CE_CHUNK_ROWS = int(_os.environ.get("PLLM_CE_CHUNK_ROWS", "0"))
+CE_WORKSPACE_MB = float(_os.environ.get("PLLM_CE_WORKSPACE_MB", "8192"))
+
+
+def _ce_chunk_rows(N: int, V: int = 50304) -> int:
+    if CE_CHUNK_ROWS > 0:
+        r = max(64, CE_CHUNK_ROWS // 64 * 64)
+        return N if N <= r else r
+    per_row = 2 * V
+    n_chunks = max(1, math.ceil(N * per_row / (CE_WORKSPACE_MB * 2 ** 20)))
+    if n_chunks == 1:
+        return N
+    return max(64, (math.ceil(N / n_chunks) + 63) // 64 * 64)
+
+
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, weight, bias, targets, ignore_index):
-        logits = F.linear(h, weight, bias)
-        rows = _ops().cross_entropy(logits, targets, logits, ignore_index)
+        N, C = h.shape
+        V = weight.shape[0]
         n_valid = (targets != ignore_index).sum().clamp_min(1)
-        ctx.save_for_backward(h, weight, logits)
-        ctx.has_bias = bias is not None
+        inv_n = n_valid.to(torch.float32).reciprocal().reshape(1)
+        need_h = ctx.needs_input_grad[0]
+        need_w = ctx.needs_input_grad[1]
+        need_b = bias is not None and ctx.needs_input_grad[2]
+        R = _ce_chunk_rows(N, V)
+        ws = torch.empty(R, V, dtype=h.dtype, device=h.device)
+        dh = torch.empty_like(h) if need_h else None
+        dw = torch.zeros(V, C, dtype=torch.float32, device=h.device) if need_w else None
+        db = torch.zeros(V, dtype=torch.float32, device=h.device) if need_b else None
+        rows = torch.empty(N, dtype=torch.float32, device=h.device)
+        wt = getattr(weight, "_pllm_wT", None)
+        wt = wt if wt is not None and getattr(weight, "_pllm_wT_ver", None) == weight._version else None
+        for r0 in range(0, N, R):
+            r1 = min(N, r0 + R)
+            hc, lg = h[r0:r1], ws[:r1 - r0]
+            if bias is not None:
+                torch.addmm(bias, hc, weight.t(), out=lg)
+            else:
+                torch.mm(hc, weight.t(), out=lg)
+            rows[r0:r1] = _ops().cross_entropy(lg, targets[r0:r1], lg, ignore_index, inv_n)
+            if need_h:  # dh = dlogits @ W (through the W^T shadow when present, see _dgrad)
+                torch.mm(lg, wt.t() if wt is not None else weight, out=dh[r0:r1])
+            if need_w:
+                _weight_grad(lg, hc, dw)
+            if need_b:
+                _ops().bias_grad(lg, db)
+        ctx.save_for_backward(dh, dw, db)
         ctx.w, ctx.b = weight, bias
-        return rows.sum() / n_valid
+        ctx.wdtype = weight.dtype
+        return rows.sum() * inv_n[0]
 
     @staticmethod
     def backward(ctx, dloss):
-        h, weight, dlogits = ctx.saved_tensors
-        g = dloss.to(torch.float32)
-        gh = g.to(h.dtype)
-        dh = _dgrad(dlogits, weight).mul_(gh) if ctx.needs_input_grad[0] else None
-        dw = db = None
-        if ctx.needs_input_grad[1]:
-            hs = h * gh  # fold the upstream scalar into the small operand, not the [N, V] gradient
+        dh, dw, db = ctx.saved_tensors
+        g = dloss.to(torch.float32).reshape(())
+        gh = None
+        if dh is not None:
+            gh = dh.mul_(g.to(dh.dtype))
+        gw = gb = None
+        if dw is not None:
             tgt = _acc_target(ctx.w)
-            dw = _weight_grad(dlogits, hs, tgt)
             if tgt is not None:
+                tgt.view(-1).addcmul_(dw.view(-1), g)
                 _notify(ctx.w)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
-            # column sums of dlogits by the colsum kernel (fp32 partials), never an fp32 copy
-            # of the [N, V] gradient
+            else:
+                gw = dw.mul_(g).to(ctx.wdtype)
+        if db is not None:
             tgt = _acc_target(ctx.b)
-            col = _ops().bias_grad(dlogits, torch.zeros(dlogits.shape[1], dtype=torch.float32,
-                                                        device=dlogits.device))
             if tgt is not None:
-                tgt.add_(col * g)
+                tgt.addcmul_(db, g)
                 _notify(ctx.b)
             else:
-                db = (col * g).to(weight.dtype)
+                gb = db.mul_(g).to(ctx.wdtype)
         ctx.w = ctx.b = None
-        return dh, dw, db, None, None
+        return gh, gw, gb, None, None
 
 
 def lm_head_cross_entropy(h, weight, bias, targets, ignore_index: int = -100):
-    """mean CE of ``h @ weight^T + bias`` against ``targets`` without returning logits."""
+    """mean CE of ``h @ weight^T + bias`` against ``targets`` without returning logits
+    (chunked over rows on the HIP path: no [N, V] buffer in training or evaluation)."""
     targets = targets.reshape(-1)
     h = h.reshape(-1, h.shape[-1])
     if _hip(h) and torch.is_grad_enabled() and (h.requires_grad or weight.requires_grad):
         return _LMHeadCEFn.apply(h, weight, bias, targets, ignore_index)
+    if _hip(h):
+        N, V = h.shape[0], weight.shape[0]
+        R = _ce_chunk_rows(N, V)
+        ws = torch.empty(R, V, dtype=h.dtype, device=h.device)
+        rows = torch.empty(N, dtype=torch.float32, device=h.device)
+        for r0 in range(0, N, R):
+            r1 = min(N, r0 + R)
+            lg = ws[:r1 - r0]
+            if bias is not None:
+                torch.addmm(bias, h[r0:r1], weight.t(), out=lg)
+            else:
+                torch.mm(h[r0:r1], weight.t(), out=lg)
+            rows[r0:r1] = _ops().cross_entropy(lg, targets[r0:r1], None, ignore_index)
+        return rows.sum() / (targets != ignore_index).sum().clamp_min(1)
     logits = F.linear(h, weight, bias)
     return cross_entropy(logits, targets, ignore_index)
 
