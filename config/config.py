@@ -79,6 +79,7 @@ default_config = {
     'synthetic_data': False,          # force synthetic token shards
     'allow_synthetic': True,          # fall back to synthetic shards when the data files are missing
     'synthetic_tokens': 2_000_000,
+    'synthetic_kind': 'auto',         # markov (order-2 source, learnable) | fast (vectorised) | auto (by size)
     'synthetic_dir': 'data/synthetic',
     'bucket_mb': 64.0,                # DP all-reduce bucket size (xGMI-sized, see parallel/dp.py)
     'first_bucket_mb': 4.0,

@@ -117,10 +117,13 @@ class Trainer:
                 raise FileNotFoundError(path)
             n = int(self.cfg.get("synthetic_tokens", 2_000_000))
             syn = self.cfg.get("synthetic_dir", "data/synthetic")
-            path = os.path.join(syn, f"{os.path.basename(path) or 'tokens'}.{self.mcfg.vocab_size}.{n}.bin")
+            kind = self.cfg.get("synthetic_kind", "auto")
+            path = os.path.join(syn, f"{os.path.basename(path) or 'tokens'}.{self.mcfg.vocab_size}.{n}"
+                                     f"{'' if kind == 'auto' else '.' + kind}.bin")
+            kind = self.cfg.get("synthetic_kind", "auto")  # auto | markov | fast (data/shards.py)
             if self.di.is_master:
                 ensure_synthetic_shard(path, n, self.mcfg.vocab_size, seed=int(self.cfg.get("seed", 1337)),
-                                       stream=stream)
+                                       stream=stream, fast=None if kind == "auto" else kind == "fast")
             if dist.is_initialized():
                 dist.barrier()
         return TokenLoader(path, self.cfg["t_batch_size"], self.seq_len, self.di.rank,
