@@ -88,6 +88,9 @@ default_config = {
     'profile_dir': None,              # torch.profiler (ROCm activity) chrome traces + kernel table per rank
     'profile_steps': '3:6',           # [start:end) optimizer steps to profile
     'deterministic': False,           # torch.use_deterministic_algorithms + fixed-order kernels only
+    'compile': None,                  # None -> env TORCH_COMPILE=="1" (reference toggle): hipGraph step on GPU,
+                                      # torch.compile(model) on CPU
+    'compile_backend': 'inductor',    # torch.compile backend for the CPU path
     'debug_sync': False,              # AMD_SERIALIZE_KERNEL=3 + HIP_LAUNCH_BLOCKING=1 (set before HIP init)
 }
 

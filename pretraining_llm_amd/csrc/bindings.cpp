@@ -59,7 +59,7 @@ std::vector<Tensor> norm_fwd(const Tensor& x, const std::optional<Tensor>& res, 
     TORCH_CHECK(res->sizes() == x.sizes(), "residual shape");
     s = at::empty_like(x);
   } else {
-    s = x;
+    s = at::empty({0}, x.options());  // no residual: the residual stream is x itself (never aliased)
   }
   Tensor y = at::empty_like(x);
   auto f32 = x.options().dtype(at::kFloat);
@@ -145,7 +145,8 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
     Tensor part = at::empty({pllm::colsum_groups((int)N), C}, dy.options().dtype(at::kFloat));
     pllm::bias_grad(dy.data_ptr(), (int)N, (int)C, part.data_ptr<float>(), out.data_ptr(), of32, true, cur_stream());
   }
-  return out;
+  // accumulate mode returns an empty tensor: a custom op's output must not alias an input
+  return out_acc ? at::empty({0}, dy.options()) : out;
 }
 
 // ---------------------------------------------------------------- weight-gradient GEMM
@@ -178,7 +179,7 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
                 S > 1 ? part.data_ptr<float>() : nullptr, out.data_ptr(), of32, out_acc.has_value(), cur_stream());
   else if (!out_acc)
     out.zero_();
-  return out;
+  return out_acc ? at::empty({0}, dy.options()) : out;
 }
 
 // ---------------------------------------------------------------- skinny GEMM (decode)
@@ -341,7 +342,7 @@ Tensor swiglu_bwd(const Tensor& dy, const Tensor& gu) {
 
 // packed rows [..., n_heads_total * D]; rotates the first n_rot heads; T = positions per sequence
 Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_heads_total, int64_t n_rot, int64_t T,
-            int64_t pos_offset, bool inverse, bool inplace) {
+            int64_t pos_offset, bool inverse) {
   check_bf16(x, "x");
   check_contig(x, "x");
   TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "rope tables must be fp32");
@@ -353,7 +354,7 @@ Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_hea
   TORCH_CHECK(cos.size(-1) == D / 2 && cos.size(0) >= T + pos_offset, "rope: table shape");
   const int64_t rows = x.numel() / W;
   TORCH_CHECK(rows % T == 0, "rope: rows must be a multiple of T");
-  Tensor out = inplace ? x : at::empty_like(x);
+  Tensor out = at::empty_like(x);
   if (rows)
     pllm::rope(x.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), rows, (int)T,
                (int)n_heads_total, (int)n_rot, (int)D, (int)pos_offset, inverse, cur_stream());
@@ -710,7 +711,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
-  m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse, bool inplace) -> Tensor");
+  m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");

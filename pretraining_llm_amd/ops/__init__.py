@@ -206,7 +206,7 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
         # (csrc/gemv.hip) instead of the training-sized library tiles
         K = x.shape[-1]
         rows = x.numel() // K if K else 0
-        if 0 < rows <= 8 and K % 8 == 0 and weight.is_contiguous() and weight.data_ptr() % 16 == 0:
+        if 0 < rows <= 8 and K % 8 == 0 and weight.is_contiguous() and _aligned16(weight):
             y = _ops().gemv(x.reshape(rows, K).contiguous(), weight, bias)[0]
             return y.view(*x.shape[:-1], weight.shape[0])
     return F.linear(x, weight, bias)
@@ -215,11 +215,17 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
 _ACT_IDS = {None: 0, "gelu": 1, "relu": 2}
 
 
+def _aligned16(t) -> bool:
+    """16-byte alignment of a view, from its storage offset (allocations are 256-B aligned);
+    unlike data_ptr() this is well-defined on FakeTensors (torch.compile tracing)."""
+    return (t.storage_offset() * t.element_size()) % 16 == 0
+
+
 def _gemv_ok(x, weight):
     K = x.shape[-1]
     rows = x.numel() // K if K else 0
     return (_hip(x) and not torch.is_grad_enabled() and 0 < rows <= 8 and K % 8 == 0
-            and weight.is_contiguous() and weight.data_ptr() % 16 == 0)
+            and weight.is_contiguous() and _aligned16(weight))
 
 
 def norm_linear(x, residual, norm_weight, norm_bias, eps: float, rms: bool, weight, bias=None,
@@ -280,6 +286,8 @@ class _NormFn(torch.autograd.Function):
         x2 = x.reshape(-1, C)
         r2 = residual.reshape(-1, C) if residual is not None else None
         y, s, mean, rstd = _ops().norm_fwd(x2, r2, weight, bias, eps, rms)
+        if residual is None:
+            s = x2  # the op returns an empty s: the normalised stream is x itself
         ctx.save_for_backward(s, weight, mean, rstd)
         ctx.w, ctx.b, ctx.xb = weight, bias, x_bias
         ctx.has_bias = bias is not None
@@ -401,7 +409,7 @@ class _RopePackedFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, cos, sin, H, Hkv):
         B, T, W = qkv.shape
-        out = _ops().rope(qkv.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, False, False)
+        out = _ops().rope(qkv.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, False)
         ctx.save_for_backward(cos, sin)
         ctx.cfg = (H, Hkv, T)
         return out
@@ -410,7 +418,7 @@ class _RopePackedFn(torch.autograd.Function):
     def backward(ctx, dout):
         cos, sin = ctx.saved_tensors
         H, Hkv, T = ctx.cfg
-        d = _ops().rope(dout.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, True, False)
+        d = _ops().rope(dout.contiguous(), cos, sin, H + 2 * Hkv, H + Hkv, T, 0, True)
         return d, None, None, None, None
 
 
@@ -758,7 +766,7 @@ def apply_rope(x, cos, sin, pos_offset: int = 0):
     """x [B,T,H,D] -> rotated copy (no autograd; used by decode). cos/sin index from pos_offset."""
     if _hip(x):
         B, T, H, D = x.shape
-        y = _ops().rope(x.contiguous().view(B, T, H * D), cos, sin, H, H, T, pos_offset, False, False)
+        y = _ops().rope(x.contiguous().view(B, T, H * D), cos, sin, H, H, T, pos_offset, False)
         return y.view(B, T, H, D)
     T = x.shape[1]
     return ref.rope(x, cos[pos_offset:pos_offset + T], sin[pos_offset:pos_offset + T])

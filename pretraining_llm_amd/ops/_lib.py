@@ -37,6 +37,8 @@ def load(raise_on_error: bool = False) -> bool:
         else:
             try:
                 torch.ops.load_library(SO_PATH)
+                from . import fake  # meta implementations for FakeTensor tracing (torch.compile)
+                fake.register()
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box

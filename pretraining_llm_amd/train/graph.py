@@ -33,7 +33,8 @@ class GraphedTrainStep:
         return loss.detach()
 
     def capture(self, x, y, lr: float):
-        """Run ``warmup`` eager steps on (x, y) (real optimizer steps) on a side stream, then capture."""
+        """Run ``warmup`` eager steps on (x, y) (real optimizer steps) on a side stream, then capture.
+        The loss of the last warmup step is kept in ``warmup_loss``."""
         self.x.copy_(x)
         self.y.copy_(y)
         side = torch.cuda.Stream()
@@ -41,7 +42,7 @@ class GraphedTrainStep:
         with torch.cuda.stream(side):
             for _ in range(self.warmup):
                 self.opt.prepare_graph_step(lr)
-                self._body()
+                self.warmup_loss = self._body().clone()
         torch.cuda.current_stream().wait_stream(side)
         torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()

@@ -102,6 +102,27 @@ class Trainer:
             self.engine = DataParallelEngine(self.opt, **bkw)
         self.accum = int(self.cfg.get("grad_accum_steps", 1))
         self.step = 0
+        # TORCH_COMPILE (reference: torch.compile(model) when the env var is "1",
+        # scripts/train_transformer.py:31-33,118-120).  The hot ops here are hand-written kernels, so
+        # what a compiler would still remove is per-launch host cost: on the GPU the whole step
+        # (fwd, bwd, bucketed all-reduce, clip, AdamW, zero_grad) is captured once as a hipGraph
+        # and replayed (train/graph.py); on the CPU the model goes through torch.compile.
+        comp = self.cfg.get("compile")
+        if comp is None:
+            comp = os.environ.get("TORCH_COMPILE", "0") == "1"
+        self.compile = bool(comp)
+        self.gstep = None
+        self.use_graph = False
+        self.fwd = self.model
+        if self.compile and self.device.type == "cuda":
+            why = ("grad_accum_steps > 1" if self.accum > 1 else "ZeRO-1 (collectives inside the optimizer step)"
+                   if int(self.cfg.get("zero_stage", 0)) >= 1 else None)
+            if why is None:
+                self.use_graph = True
+            elif self.di.is_master:
+                self.log(f"TORCH_COMPILE: hipGraph step disabled ({why}); running eagerly")
+        elif self.compile:
+            self.fwd = torch.compile(self.model, backend=self.cfg.get("compile_backend", "inductor"))
         self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
         self.train_loader = self._loader(self.cfg["train_path"], seed, 0)
         vp = self.cfg.get("val_path") or self.cfg.get("dev_path")
@@ -136,13 +157,15 @@ class Trainer:
     def train_step(self) -> torch.Tensor:
         """One optimizer step (``grad_accum_steps`` micro-batches). Returns the mean loss (device tensor)."""
         lr = self.lr(self.step)
+        if self.use_graph:
+            return self._graph_step(lr)
         self.opt.param_groups[0]["lr"] = lr
         total = torch.zeros((), device=self.device, dtype=torch.float32)
         for micro in range(self.accum):
             x, y = self.train_loader.next()
             ctx = self.engine.no_sync() if micro < self.accum - 1 else contextlib.nullcontext()
             with ctx:
-                _, loss = self.model(x, y, return_logits=False)
+                _, loss = self.fwd(x, y, return_logits=False)
                 loss.backward()
             total += loss.detach().float()
         scale = self.engine.finish_grad_sync()
@@ -150,6 +173,20 @@ class Trainer:
         self.opt.zero_grad()
         self.step += 1
         return total / self.accum
+
+    def _graph_step(self, lr: float) -> torch.Tensor:
+        """hipGraph-replayed step.  The first call runs one real (eager, side-stream) step on its
+        batch -- it also teaches the DP engine its bucket order -- then captures the step; every
+        later call copies its batch into the static inputs and replays."""
+        from .graph import GraphedTrainStep
+        x, y = self.train_loader.next()
+        self.step += 1
+        if self.gstep is None:
+            B, T = x.shape
+            self.gstep = GraphedTrainStep(self.model, self.opt, self.engine, B, T, self.device, warmup=1)
+            self.gstep.capture(x, y, lr)
+            return self.gstep.warmup_loss
+        return self.gstep(x, y, lr).clone()
 
     @torch.no_grad()
     def evaluate(self, iters: Optional[int] = None) -> float:
@@ -160,7 +197,7 @@ class Trainer:
         acc = torch.zeros((), device=self.device, dtype=torch.float32)
         for _ in range(iters):
             x, y = self.val_loader.next()
-            _, loss = self.model(x, y, return_logits=False)
+            _, loss = self.fwd(x, y, return_logits=False)
             acc += loss.float()
         self.model.train()
         return float(all_reduce_mean(acc / iters))
