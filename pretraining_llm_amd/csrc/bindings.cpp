@@ -125,6 +125,22 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   return {dx, dw, db};
 }
 
+// Op entry points (a mutable custom op may not return a Tensor list: torch.compile's
+// auto-functionalisation only handles single-Tensor returns).
+// norm_bwd: pure -> (dx, dw, db) (db empty without bias);  norm_bwd_acc: adds into the targets,
+// returns dx.
+std::tuple<Tensor, Tensor, Tensor> norm_bwd_op(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& mean,
+                                               const Tensor& rstd, const std::optional<Tensor>& ds, bool has_bias,
+                                               bool rms) {
+  auto o = norm_bwd(dy, s, w, mean, rstd, ds, has_bias, rms, std::nullopt, std::nullopt, std::nullopt);
+  return {o[0], o[1], has_bias ? o[2] : at::empty({0}, w.options())};
+}
+Tensor norm_bwd_acc_op(const Tensor& dy, const Tensor& s, const Tensor& w, const Tensor& mean, const Tensor& rstd,
+                       const std::optional<Tensor>& ds, bool has_bias, bool rms, Tensor& dw_acc,
+                       const std::optional<Tensor>& db_acc, const std::optional<Tensor>& xb_acc) {
+  return norm_bwd(dy, s, w, mean, rstd, ds, has_bias, rms, dw_acc, db_acc, xb_acc)[0];
+}
+
 // column sums of dy [..., C] (bias gradient); added into out_acc if given, else returned
 Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
   check_bf16(dy, "dy");
@@ -185,7 +201,7 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 // ---------------------------------------------------------------- skinny GEMM (decode)
 // y[M, N] = act(in[M, K] w[N, K]^T (+ bias)) for M <= 8 token rows; in = x, or (gamma given)
 // norm(x (+ res)) -- then also returns the residual stream s = x + res when res is given
-std::vector<Tensor> gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias,
+std::tuple<Tensor, Tensor> gemv(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias,
                          const std::optional<Tensor>& res, const std::optional<Tensor>& gamma,
                          const std::optional<Tensor>& beta, double eps, int64_t rms, int64_t act,
                          const std::optional<Tensor>& kc, const std::optional<Tensor>& vc,
@@ -271,8 +287,8 @@ std::vector<Tensor> gemv(const Tensor& x, const Tensor& w, const std::optional<T
     TORCH_CHECK(!a.kc || a.act == 0, "gemv: KV-cache append takes no activation");
     pllm::gemv(a, cur_stream());
   }
-  if (res) return {y, s};
-  return {y};
+  if (!res) s = at::empty({0}, x.options());
+  return {y, s};
 }
 
 // ---------------------------------------------------------------- activations
@@ -512,6 +528,18 @@ std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V
   return {dwte, dwpe};
 }
 
+// embedding_bwd: pure -> (dwte, dwpe) (dwpe empty without positions); embedding_bwd_acc: adds
+// into the targets
+std::tuple<Tensor, Tensor> embedding_bwd_op(const Tensor& dx, const Tensor& idx, int64_t V, int64_t n_pos,
+                                            bool has_wpe) {
+  auto o = embedding_bwd(dx, idx, V, n_pos, has_wpe, std::nullopt, std::nullopt);
+  return {o[0], has_wpe ? o[1] : at::empty({0}, dx.options())};
+}
+void embedding_bwd_acc_op(const Tensor& dx, const Tensor& idx, int64_t V, int64_t n_pos, bool has_wpe,
+                          Tensor& dwte_acc, const std::optional<Tensor>& dwpe_acc) {
+  embedding_bwd(dx, idx, V, n_pos, has_wpe, dwte_acc, dwpe_acc);
+}
+
 // ---------------------------------------------------------------- batched transpose
 // Builds the descriptor table for dst[i] = src[i]^T (bf16 2-D, dims % 8 == 0, 16-B aligned);
 // returns it as a device int64 tensor [n, 6] whose last row-count column is the tile total.
@@ -700,12 +728,13 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
 
 TORCH_LIBRARY(pllm, m) {
   m.def("norm_fwd(Tensor x, Tensor? residual, Tensor weight, Tensor? bias, float eps, bool rms) -> Tensor[]");
-  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!)? dw_acc=None, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor[]");
+  m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms) -> (Tensor, Tensor, Tensor)");
+  m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
-  m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> Tensor[]");
+  m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
   m.def("act_bwd_bias(Tensor dy, Tensor x, int op, Tensor(a!) bias_acc) -> Tensor");
@@ -717,7 +746,8 @@ TORCH_LIBRARY(pllm, m) {
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
-  m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!)? dwte_acc=None, Tensor(b!)? dwpe_acc=None) -> Tensor[]");
+  m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe) -> (Tensor, Tensor)");
+  m.def("embedding_bwd_acc(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!) dwte_acc, Tensor(b!)? dwpe_acc=None) -> ()");
   m.def("transpose_plan(Tensor[] src, Tensor[] dst) -> Tensor");
   m.def("transpose_run(Tensor desc, int total_tiles) -> ()");
   m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
@@ -728,7 +758,8 @@ TORCH_LIBRARY(pllm, m) {
 
 TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("norm_fwd", norm_fwd);
-  m.impl("norm_bwd", norm_bwd);
+  m.impl("norm_bwd", norm_bwd_op);
+  m.impl("norm_bwd_acc", norm_bwd_acc_op);
   m.impl("bias_grad", bias_grad);
   m.impl("wgrad", wgrad);
   m.impl("act_fwd", act_fwd);
@@ -742,7 +773,8 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("adamw_", adamw_);
   m.impl("sumsq", sumsq);
   m.impl("embedding_fwd", embedding_fwd);
-  m.impl("embedding_bwd", embedding_bwd);
+  m.impl("embedding_bwd", embedding_bwd_op);
+  m.impl("embedding_bwd_acc", embedding_bwd_acc_op);
   m.impl("transpose_plan", transpose_plan);
   m.impl("transpose_run", transpose_run);
   m.impl("sample", sample);

@@ -310,7 +310,7 @@ class _NormFn(torch.autograd.Function):
         direct = tw is not None and (not ctx.has_bias or tb is not None)
         dxb = None
         if direct:
-            outs = _ops().norm_bwd(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms, tw, tb, txb)
+            outs = (_ops().norm_bwd_acc(dy2, s, weight, mean, rstd, ds2, ctx.has_bias, ctx.rms, tw, tb, txb),)
             dw = db = None
             _notify(ctx.w)
             if ctx.has_bias:
@@ -607,7 +607,7 @@ class _EmbeddingFn(torch.autograd.Function):
         tp = _acc_target(ctx.wpe) if has_pos else None
         if tt is not None and (not has_pos or tp is not None):
             sync_side_streams()  # a tied LM head's dW may still be accumulating into wte's gradient
-            _ops().embedding_bwd(dx.contiguous(), idx, ctx.V, ctx.n_pos, has_pos, tt, tp)
+            _ops().embedding_bwd_acc(dx.contiguous(), idx, ctx.V, ctx.n_pos, has_pos, tt, tp)
             _notify(ctx.wte)
             if has_pos:
                 _notify(ctx.wpe)

@@ -34,15 +34,13 @@ def register() -> None:
         return [torch.empty_like(x), s, x.new_empty((N,), dtype=f32), x.new_empty((N,), dtype=f32)]
 
     @_reg("norm_bwd")
-    def _(dy, s, weight, mean, rstd, ds, has_bias, rms, dw_acc=None, db_acc=None, xb_acc=None):
-        dx = torch.empty_like(dy)
-        if dw_acc is not None:
-            return [dx]
+    def _(dy, s, weight, mean, rstd, ds, has_bias, rms):
         C = dy.shape[1]
-        out = [dx, weight.new_empty((C,))]
-        if has_bias:
-            out.append(weight.new_empty((C,)))
-        return out
+        return (torch.empty_like(dy), weight.new_empty((C,)), weight.new_empty((C,) if has_bias else (0,)))
+
+    @_reg("norm_bwd_acc")
+    def _(dy, s, weight, mean, rstd, ds, has_bias, rms, dw_acc, db_acc=None, xb_acc=None):
+        return torch.empty_like(dy)
 
     @_reg("bias_grad")
     def _(dy, out_acc=None):
@@ -101,14 +99,13 @@ def register() -> None:
         return wte.new_empty((idx.shape[0], idx.shape[1], wte.shape[1]))
 
     @_reg("embedding_bwd")
-    def _(dx, idx, V, n_pos, has_wpe, dwte_acc=None, dwpe_acc=None):
-        if dwte_acc is not None:
-            return []
+    def _(dx, idx, V, n_pos, has_wpe):
         C = dx.shape[-1]
-        out = [dx.new_empty((V, C))]
-        if has_wpe:
-            out.append(dx.new_empty((n_pos, C)))
-        return out
+        return (dx.new_empty((V, C)), dx.new_empty((n_pos, C) if has_wpe else (0,)))
+
+    @_reg("embedding_bwd_acc")
+    def _(dx, idx, V, n_pos, has_wpe, dwte_acc, dwpe_acc=None):
+        return None
 
     @_reg("transpose_plan")
     def _(src, dst):
@@ -139,6 +136,4 @@ def register() -> None:
     def _(x, w, bias, res=None, gamma=None, beta=None, eps=1e-5, rms=0, act=0, kc=None, vc=None, pos=None,
           q_cols=0):
         y = x.new_empty((x.shape[0], w.shape[0]))
-        if res is not None:
-            return [y, x.new_empty(x.shape)]
-        return [y]
+        return (y, x.new_empty(x.shape if res is not None else (0,)))

@@ -31,8 +31,8 @@ def _op_cases():
         ("norm_fwd", (x, r(N, C), w, b, 1e-5, False)),
         ("norm_fwd", (x, None, w, None, 1e-5, True)),
         ("norm_bwd", (r(N, C), x, w, mean, rstd, None, True, False)),
-        ("norm_bwd", (r(N, C), x, w, mean, rstd, r(N, C), True, False, torch.zeros(C, device=DEV),
-                      torch.zeros(C, device=DEV), torch.zeros(C, device=DEV))),
+        ("norm_bwd_acc", (r(N, C), x, w, mean, rstd, r(N, C), True, False, torch.zeros(C, device=DEV),
+                          torch.zeros(C, device=DEV), torch.zeros(C, device=DEV))),
         ("bias_grad", (r(N, C),)),
         ("bias_grad", (r(N, C), torch.zeros(C, device=DEV))),
         ("wgrad", (r(N, 256), r(N, C))),
@@ -49,7 +49,8 @@ def _op_cases():
         ("sumsq", (r(4096, dt=f32),)),
         ("embedding_fwd", (idx, r(V, C), r(T, C), 0)),
         ("embedding_bwd", (r(B, T, C), idx, V, T, True)),
-        ("embedding_bwd", (r(B, T, C), idx, V, T, True, torch.zeros(V, C, device=DEV), torch.zeros(T, C, device=DEV))),
+        ("embedding_bwd_acc", (r(B, T, C), idx, V, T, True, torch.zeros(V, C, device=DEV),
+                               torch.zeros(T, C, device=DEV))),
         ("attn_fwd", (q, k, v, True, 0.125)),
         ("attn_bwd", (r(B, T, H, D), q, k, v, o, lse, torch.empty_like(q), torch.empty_like(k), torch.empty_like(v),
                       True, 0.125)),
