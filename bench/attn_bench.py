@@ -63,7 +63,7 @@ def main():
             for vv, o_ in outs.items():
                 res[f"v{vv}_max_rel_diff_vs_v{v0}"] = max(((a - b).norm() / b.norm()).item()
                                                           for a, b in zip(o_, outs[v0]))
-            torch.ops.pllm.attn_bwd_set_variant(2)  # the default (D<=64: 0, D=128: BQ=64)
+            torch.ops.pllm.attn_bwd_set_variant(0)  # the default (D<=64: V 0, D=128: V 1)
             print(json.dumps(res), flush=True)
             continue
         if args.only:

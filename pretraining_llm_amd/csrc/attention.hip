@@ -27,7 +27,8 @@
 //    skips it outright (zeros into the dS^T image), and dQ k-steps past the
 //    diagonal are skipped.  dQ per key block is summed over its keys on chip and written to a
 //    per-key-block fp32 slab; a second kernel sums the slabs in a fixed order
-//    (deterministic; the first version's fp32 atomics were its floor).
+//    (deterministic; the first version's fp32 atomics were its floor).  The key blocks run
+//    in passes so the slab workspace is bounded independently of T (O(T) memory).
 #include <type_traits>
 
 #include "common.h"
@@ -61,6 +62,37 @@ PLLM_DEV bf16x8 pack_frag(const f32x16& x, int s) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = (bf16)x[8 * s + j];
   return f;
+}
+
+// ---------------------------------------------------------------------------
+// Fused RoPE (rotate-half convention, ops/reference.py rope): element i < D/2 of a head row
+// pairs with i + D/2; a' = a cos - b sin, b' = b cos + a sin at the row's position.  The kernels
+// rotate q and k while staging them (registers / LDS images) and un-rotate dq and dk before
+// the final stores, so the packed QKV tensor and its gradient stay unrotated and no separate
+// RoPE pass over [B, T, H, D] exists in forward or backward.
+// Rotates 8 + 8 bf16 values (a = elements i0..i0+7, b = i0+D/2..) held as two 16-B chunks.
+PLLM_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, float dir) {
+  float a[8], b[8], c[8], sn[8];
+  unpack8(lo, a);
+  unpack8(hi, b);
+  const f32x4* cp = reinterpret_cast<const f32x4*>(cosr);
+  const f32x4* sp = reinterpret_cast<const f32x4*>(sinr);
+  const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    c[e] = c0[e];
+    c[4 + e] = c1[e];
+    sn[e] = s0[e] * dir;
+    sn[4 + e] = s1[e] * dir;
+  }
+  float o1[8], o2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    o1[e] = a[e] * c[e] - b[e] * sn[e];
+    o2[e] = b[e] * c[e] + a[e] * sn[e];
+  }
+  lo = pack8(o1);
+  hi = pack8(o2);
 }
 
 // ---------------------------------------------------------------------------
@@ -102,16 +134,15 @@ struct FwdCfg {
   static constexpr int QB = D <= 64 ? 2 : 1;
   static constexpr int BM = NW * 32 * QB, BN = 64;
   static constexpr int CPR = D / 8;   // 16 B chunks per row
-  static constexpr int LPT = BN * CPR / 256;
   static constexpr int TILE = BN * D;  // elements per K (or V) tile
   static constexpr int LDS_ELEMS = 4 * TILE;
 };
 
-template <int D>
+template <int D, bool ROPE>
 __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   using C = FwdCfg<D>;
   using I = Img<D>;
-  constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, LPT = C::LPT, TILE = C::TILE, QB = C::QB, NW = C::NW;
+  constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, TILE = C::TILE, QB = C::QB, NW = C::NW;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
 
@@ -139,22 +170,37 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
     const int qi = qw[j] + r;
+    u32x4 raw[NKS];
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks)
-      qf[j][ks] = qi < a.T ? as_frag(ld16(qp + (int64_t)qi * a.q_st + 16 * ks + 8 * hh)) : zero_frag();
+      raw[ks] = qi < a.T ? ld16(qp + (int64_t)qi * a.q_st + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
+    if (ROPE && qi < a.T) {
+      // the lane's chunks ks and ks + NKS/2 hold head-dim elements i and i + D/2
+      const int64_t tab = (int64_t)(qi + off) * (D / 2);
+#pragma unroll
+      for (int ks = 0; ks < NKS / 2; ++ks)
+        rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
+              1.f);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) qf[j][ks] = as_frag(raw[ks]);
   }
 
   int kv_end = a.S;
   if (a.causal) kv_end = min(a.S, q0 + BM + off);
   const int ntiles = (kv_end + BN - 1) / BN;
 
-  u32x4 kr[LPT], vr[LPT];
+  // chunk i of this thread: row c / CPR, column chunk (c % CPR2) + (i odd ? CPR2 : 0) with
+  // c = tid + 256 * (i / 2) and CPR2 = CPR / 2, so a thread holds both RoPE partners of a row
+  constexpr int CPR2 = CPR / 2;
+  constexpr int NPAIR = (BN * CPR2 + 255) / 256;
+  u32x4 kr[2 * NPAIR], vr[2 * NPAIR];
   auto gload = [&](int t) {
     const int kv0 = t * BN;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, col = c % CPR, key = kv0 + row;
-      if (key < a.S) {
+    for (int i = 0; i < 2 * NPAIR; ++i) {
+      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2, key = kv0 + row;
+      if (c < BN * CPR2 && key < a.S) {
         kr[i] = ld16(kp + (int64_t)key * a.k_st + col * 8);
         vr[i] = ld16(vp + (int64_t)key * a.v_st + col * 8);
       } else {
@@ -163,14 +209,22 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       }
     }
   };
-  auto swrite = [&](int buf) {
+  auto swrite = [&](int buf, int t) {
     uint16_t* Kb = smem + buf * TILE;
     uint16_t* Vb = smem + 2 * TILE + buf * TILE;
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, col = c % CPR;
+    for (int i = 0; i < 2 * NPAIR; i += 2) {
+      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2;
+      if (c >= BN * CPR2) continue;
+      if (ROPE) {
+        const int key = t * BN + row;
+        const int64_t tab = (int64_t)min(key, a.S - 1) * (D / 2) + col * 8;
+        rope8(kr[i], kr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
+      }
       st16(Kb + I::off(row, col * 8), kr[i]);
+      st16(Kb + I::off(row, (col + CPR2) * 8), kr[i + 1]);
       st16(Vb + I::off(row, col * 8), vr[i]);
+      st16(Vb + I::off(row, (col + CPR2) * 8), vr[i + 1]);
     }
   };
 
@@ -188,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
 
   if (ntiles > 0) {
     gload(0);
-    swrite(0);
+    swrite(0, 0);
   }
   __syncthreads();
   for (int t = 0; t < ntiles; ++t) {
@@ -281,7 +335,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     if (mask == 3) tile(std::integral_constant<int, 3>{});
     else if (mask == 1) tile(std::integral_constant<int, 1>{});
     else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
-    if (t + 1 < ntiles) swrite(buf ^ 1);
+    if (t + 1 < ntiles) swrite(buf ^ 1, t + 1);
     __syncthreads();
   }
 
@@ -339,37 +393,38 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 
 // Backward tiling.  NW waves per workgroup, each owning 32 keys (BK = 32*NW keys per
 // workgroup); BQ query rows per iteration processed as NQB sub-blocks of 32.
-//   D <= 64 : 8 waves, 256 keys, 128 queries per iteration -> every dQ task (32 q x 32 d)
-//             sums all 256 keys on chip; half the dQ slabs of a 128-key block.
-//   D = 128 : 4 waves, 128 keys, 32 queries (register budget: dK^T/dV^T alone are 128 regs).
-//   V = 1 (D <= 64): 4 waves, 128 keys, 64 queries: 48 KiB of LDS, so TWO workgroups share a
-//             CU and one's barrier waits overlap the other's MFMA work (more dQ slabs).
-//   V = 1, 2 (D = 128): 4 waves, 128 keys, 64 / 128 queries per iteration (1/2, 1/4 of the
-//             barriers per query of V = 0; every wave runs 2 / 4 dQ tasks).  V = 1 measured
-//             1349 -> 1083 us at B=8 H=16 T=2048 (profiles/r1_attn_bwd_d128_bq_ab.jsonl).
+//   D <= 64, V 0: 8 waves, 256 keys, 128 queries per iteration (two waves per SIMD).
+//            V 1: 4 waves, 128 keys, 64 queries: 48 KiB of LDS, two workgroups per CU.
+//   D = 128, V 1 / 2: 4 waves, 128 keys, 64 / 128 queries per iteration (one wave per SIMD).
+// KH (32-key halves per wave) is kept as a parameter of the code: 4 waves x 64 keys (KH = 2,
+// one wave per SIMD, every Q/dO fragment feeding two MFMAs) measured 24-33 % SLOWER than V 0
+// at every D = 64 shape (profiles/r2_attn_bwd_variants.jsonl), so every variant uses KH = 1.
 template <int D, int V = 0>
 struct BwdCfg {
-  static constexpr int NW = D <= 64 ? (V == 0 ? 8 : 4) : 4;
+  static constexpr int KH = 1;
+  static constexpr int NW = (D <= 64 && V == 0) ? 8 : 4;
   static constexpr int NT = 64 * NW;
-  static constexpr int BK = 32 * NW;
+  static constexpr int BK = 32 * KH * NW;
   static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : (32 << V);
-  static constexpr int MIN_WAVES = (D == 128 && NW == 4) ? 1 : 2;
+  static constexpr int MIN_WAVES = D == 128 ? 1 : 2;
   static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
-  static constexpr int QLPT = (BQ * CPR + NT - 1) / NT;
-  static constexpr int KLPT = (BK * CPR + NT - 1) / NT;
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;
 };
 
-// D=128 keeps dK^T/dV^T (128 regs) + K/V fragments (64) + S/dP in registers: one wave per
-// SIMD with the full register file instead of spilling at the 2-waves/SIMD budget.
-template <int D, int V>
+// dQ: each key block's partial dQ (summed over its BK keys on chip, rounded once to bf16) goes
+// to a slab of the current PASS: the host runs the key blocks in passes of at most
+// ``nkb_pass`` blocks so the workspace is bounded independently of T; attn_dq_reduce_kernel adds
+// the slabs in fp32 in a fixed order (deterministic, no atomics) into an fp32 running sum / the
+// bf16 dQ.  fp32 slabs (no partial rounding) measured +12 % (T 1024, D 64) to +34 % (T 4096)
+// on the whole backward: the slab bytes are its second cost after the MFMAs.
+// ROPE: q and k are rotated while staged, dk is rotated back before its store (dq in the reduce).
+template <int D, int V, bool ROPE>
 __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D, V>;
   using I = Img<D>;
   using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
-  constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
-  constexpr int QLPT = C::QLPT, KLPT = C::KLPT;
+  constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR, KH = C::KH;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
   __shared__ __attribute__((aligned(16))) float rowc[2 * BQ];  // -lse/scale, -delta
@@ -380,43 +435,66 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
 
   const int BH = a.B * a.Hkv;
   const int id = blockIdx.x;
-  const int kb = id / BH;                 // key block 0 (most query blocks under causal) first
+  const int kb = a.kb0 + id / BH;         // key block (lowest first: most query blocks under causal)
   const int bh = id % BH;
   const int b = bh / a.Hkv, hk = bh % a.Hkv;
   const int G = a.H / a.Hkv;
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int k0 = kb * BK, kl = w * 32 + r, key = k0 + kl;
-  const int kw0 = k0 + w * 32;            // first key of this wave
+  const int k0 = kb * BK;
+  const int kw0 = k0 + w * 32 * KH;       // first key of this wave
   const int off = a.S - a.T;
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
-  // this lane's key row of K and V as B-operand fragments (k = head dim).  The 8-wave D=128
-  // variant reads its K fragments from the LDS K image instead (32 fewer VGPRs: no spills at
-  // two waves per SIMD).
-  constexpr bool KF_LDS = false;  // true: K fragments from the LDS image (32 fewer VGPRs)
-  bf16x8 kf[KF_LDS ? 1 : NKS], vf[NKS];
+  // this lane's key rows (one per 32-key half) of K and V as B-operand fragments (k = head dim)
+  bf16x8 kf[KH][NKS], vf[KH][NKS];
 #pragma unroll
-  for (int ks = 0; ks < NKS; ++ks) {
-    if constexpr (!KF_LDS) kf[ks] = key < a.S ? as_frag(ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh)) : zero_frag();
-    vf[ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
+  for (int kh = 0; kh < KH; ++kh) {
+    const int key = kw0 + 32 * kh + r;
+    u32x4 raw[NKS];
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      raw[ks] = key < a.S ? ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
+      vf[kh][ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
+    }
+    if (ROPE && key < a.S) {
+      const int64_t tab = (int64_t)key * (D / 2);
+#pragma unroll
+      for (int ks = 0; ks < NKS / 2; ++ks)
+        rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
+              1.f);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) kf[kh][ks] = as_frag(raw[ks]);
   }
-  // whole K block into LDS for the dQ product
+  // whole (rotated) K block into LDS for the dQ product; a thread stages both RoPE partners
+  constexpr int CPR2 = CPR / 2;
 #pragma unroll
-  for (int i = 0; i < KLPT; ++i) {
-    const int c = tid + NT * i, row = c / CPR, col = c % CPR, kk = k0 + row;
-    if (c < BK * CPR) {
-      u32x4 v = kk < a.S ? ld16(kp + (int64_t)kk * a.k_st + col * 8) : u32x4{0u, 0u, 0u, 0u};
-      st16(Kl + I::off(row, col * 8), v);
+  for (int i = 0; i < (BK * CPR2 + NT - 1) / NT; ++i) {
+    const int c = tid + NT * i, row = c / CPR2, col = c % CPR2, kk = k0 + row;
+    if (c < BK * CPR2) {
+      u32x4 lo = u32x4{0u, 0u, 0u, 0u}, hi = lo;
+      if (kk < a.S) {
+        lo = ld16(kp + (int64_t)kk * a.k_st + col * 8);
+        hi = ld16(kp + (int64_t)kk * a.k_st + (col + CPR2) * 8);
+        if (ROPE) {
+          const int64_t tab = (int64_t)kk * (D / 2) + col * 8;
+          rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
+        }
+      }
+      st16(Kl + I::off(row, col * 8), lo);
+      st16(Kl + I::off(row, (col + CPR2) * 8), hi);
     }
   }
 
-  f32x16 dk[NDB], dv[NDB];
+  f32x16 dk[KH][NDB], dv[KH][NDB];
 #pragma unroll
-  for (int db = 0; db < NDB; ++db) {
-    dk[db] = zero16();
-    dv[db] = zero16();
-  }
+  for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      dk[kh][db] = zero16();
+      dv[kh][db] = zero16();
+    }
   const float inv_scale = 1.f / a.scale, c2 = a.scale_log2;
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int nqb = (a.T + BQ - 1) / BQ;
@@ -425,7 +503,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   const int per_head = nqb - qb_start;
   const int total = per_head * G;
 
-  u32x4 qr[QLPT], dor[QLPT];
+  // Q / dO tile chunks: as in the forward, chunk i of a thread is row c / CPR2, column chunk
+  // (c % CPR2) + (i odd ? CPR2 : 0), c = tid + NT * (i / 2): both RoPE partners in one thread
+  constexpr int QPAIR = (BQ * CPR2 + NT - 1) / NT;
+  u32x4 qr[2 * QPAIR], dor[2 * QPAIR];
   float rc = 0.f;
   auto gload = [&](int it) {
     const int h = hk * G + it / per_head;
@@ -433,9 +514,9 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     const uint16_t* qp = a.q + b * a.q_sb + (int64_t)h * a.q_sh;
     const uint16_t* dop = a.dO + b * a.do_sb + (int64_t)h * a.do_sh;
 #pragma unroll
-    for (int i = 0; i < QLPT; ++i) {
-      const int c = tid + NT * i, row = c / CPR, col = c % CPR, q = q0 + row;
-      if (c < BQ * CPR && q < a.T) {
+    for (int i = 0; i < 2 * QPAIR; ++i) {
+      const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2, q = q0 + row;
+      if (c < BQ * CPR2 && q < a.T) {
         qr[i] = ld16(qp + (int64_t)q * a.q_st + col * 8);
         dor[i] = ld16(dop + (int64_t)q * a.do_st + col * 8);
       } else {
@@ -464,11 +545,17 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     const int q0 = (qb_start + it % per_head) * BQ;
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done
 #pragma unroll
-    for (int i = 0; i < QLPT; ++i) {
-      const int c = tid + NT * i, row = c / CPR, col = c % CPR;
-      if (c < BQ * CPR) {
+    for (int i = 0; i < 2 * QPAIR; i += 2) {
+      const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
+      if (c < BQ * CPR2) {
+        if (ROPE && q0 + row < a.T) {
+          const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
+          rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
+        }
         st16(Ql + I::off(row, col * 8), qr[i]);
+        st16(Ql + I::off(row, (col + CPR2) * 8), qr[i + 1]);
         st16(Ol + I::off(row, col * 8), dor[i]);
+        st16(Ol + I::off(row, (col + CPR2) * 8), dor[i + 1]);
       }
     }
     if (tid < 2 * BQ) rowc[tid] = rc;
@@ -479,72 +566,103 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
       const int qj0 = q0 + 32 * j;
-      // causal: every key of this wave lies after every query of the sub-block -> P = dS = 0
-      const bool dead = a.causal && kw0 > qj0 + 31 + off;
-      if (dead) {
+      // causal: the key halves of this wave that lie after every query of the sub-block have
+      // P = dS = 0; keys grow with kh, so the live halves are a prefix (a compile-time count per
+      // code path: no MFMA is predicated)
+      int live = KH;
+      if (a.causal) {
+        live = 0;
+#pragma unroll
+        for (int kh = 0; kh < KH; ++kh)
+          if (kw0 + 32 * kh <= qj0 + 31 + off) live = kh + 1;
+      }
+#pragma unroll
+      for (int kh = 0; kh < KH; ++kh) {
+        if (kh < live) continue;
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<u32x2*>(Sl + IS::off(kl, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
-        continue;
+          *reinterpret_cast<u32x2*>(Sl + IS::off(w * 32 * KH + 32 * kh + r, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
       }
-      // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
-      // accumulator rows 4g..4g+3 are 4 consecutive queries: one 16-B LDS read each
-      f32x16 s, dp;
+      auto body = [&](auto live_c) {
+        constexpr int NL = decltype(live_c)::value;
+        // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
+        // accumulator rows 4g..4g+3 are 4 consecutive queries: one 16-B LDS read each
+        f32x16 s[NL], dp[NL];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
-        const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * g + 4 * hh]);
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
+          const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * g + 4 * hh]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s[4 * g + e] = rs[e];
-          dp[4 * g + e] = rd[e];
+          for (int kh = 0; kh < NL; ++kh)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              s[kh][4 * g + e] = rs[e];
+              dp[kh][4 * g + e] = rd[e];
+            }
         }
-      }
 #pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const bf16x8 qa = as_frag(ld16(Ql + I::off(32 * j + r, 16 * ks + 8 * hh)));
-        if constexpr (KF_LDS) s = mfma32(qa, as_frag(ld16(Kl + I::off(kl, 16 * ks + 8 * hh))), s);
-        else s = mfma32(qa, kf[ks], s);
-        const bf16x8 oa = as_frag(ld16(Ol + I::off(32 * j + r, 16 * ks + 8 * hh)));
-        dp = mfma32(oa, vf[ks], dp);
-      }
+        for (int ks = 0; ks < NKS; ++ks) {
+          const bf16x8 qa = as_frag(ld16(Ql + I::off(32 * j + r, 16 * ks + 8 * hh)));
+          const bf16x8 oa = as_frag(ld16(Ol + I::off(32 * j + r, 16 * ks + 8 * hh)));
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        float p = fast_exp2(c2 * s[i]);
-        if (need_mask) {
-          const int q = qj0 + acc_row(i, hh);
-          if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+          for (int kh = 0; kh < NL; ++kh) {
+            s[kh] = mfma32(qa, kf[kh][ks], s[kh]);
+            dp[kh] = mfma32(oa, vf[kh][ks], dp[kh]);
+          }
         }
-        s[i] = p;           // P
-        dp[i] = p * dp[i];  // dS (unscaled)
-      }
-      const bf16x8 pf0 = pack_frag(s, 0), pf1 = pack_frag(s, 1);
-      const bf16x8 sf0 = pack_frag(dp, 0), sf1 = pack_frag(dp, 1);
-      // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] images)
+        bf16x8 pf[NL][2], sf[NL][2];
 #pragma unroll
-      for (int db = 0; db < NDB; ++db) {
+        for (int kh = 0; kh < NL; ++kh) {
+          const int key = kw0 + 32 * kh + r;
 #pragma unroll
-        for (int st = 0; st < 2; ++st) {
-          const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
-          const bf16x8 oA = cat_tr(ds_tr(Ol + I::off(rowq, col)), ds_tr(Ol + I::off(rowq + 8, col)));
-          const bf16x8 qA = cat_tr(ds_tr(Ql + I::off(rowq, col)), ds_tr(Ql + I::off(rowq + 8, col)));
-          dv[db] = mfma32(oA, st ? pf1 : pf0, dv[db]);
-          dk[db] = mfma32(qA, st ? sf1 : sf0, dk[db]);
+          for (int i = 0; i < 16; ++i) {
+            float p = fast_exp2(c2 * s[kh][i]);
+            if (need_mask) {
+              const int q = qj0 + acc_row(i, hh);
+              if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+            }
+            s[kh][i] = p;               // P
+            dp[kh][i] = p * dp[kh][i];  // dS (unscaled)
+          }
+          pf[kh][0] = pack_frag(s[kh], 0);
+          pf[kh][1] = pack_frag(s[kh], 1);
+          sf[kh][0] = pack_frag(dp[kh], 0);
+          sf[kh][1] = pack_frag(dp[kh], 1);
         }
-      }
-      // dS^T image: the lane's key row, 4 consecutive queries per 8-byte store
+        // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] images,
+        // each shared by the wave's NL key halves)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u32x2 v2;
-        v2[0] = pack_bf16x2(dp[4 * g], dp[4 * g + 1]);
-        v2[1] = pack_bf16x2(dp[4 * g + 2], dp[4 * g + 3]);
-        *reinterpret_cast<u32x2*>(Sl + IS::off(kl, 32 * j + 8 * g + 4 * hh)) = v2;
-      }
+        for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
+            const bf16x8 oA = cat_tr(ds_tr(Ol + I::off(rowq, col)), ds_tr(Ol + I::off(rowq + 8, col)));
+            const bf16x8 qA = cat_tr(ds_tr(Ql + I::off(rowq, col)), ds_tr(Ql + I::off(rowq + 8, col)));
+#pragma unroll
+            for (int kh = 0; kh < NL; ++kh) {
+              dv[kh][db] = mfma32(oA, pf[kh][st], dv[kh][db]);
+              dk[kh][db] = mfma32(qA, sf[kh][st], dk[kh][db]);
+            }
+          }
+        }
+        // dS^T image: the lane's key rows, 4 consecutive queries per 8-byte store
+#pragma unroll
+        for (int kh = 0; kh < NL; ++kh)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            u32x2 v2;
+            v2[0] = pack_bf16x2(dp[kh][4 * g], dp[kh][4 * g + 1]);
+            v2[1] = pack_bf16x2(dp[kh][4 * g + 2], dp[kh][4 * g + 3]);
+            *reinterpret_cast<u32x2*>(Sl + IS::off(w * 32 * KH + 32 * kh + r, 32 * j + 8 * g + 4 * hh)) = v2;
+          }
+      };
+      if (live == KH) body(std::integral_constant<int, KH>{});
+      else if (KH > 1 && live == 1) body(std::integral_constant<int, 1>{});
     }
     __syncthreads();
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
-    // the key block's slab.
+    // this pass's fp32 slab of the key block.
     for (int task = w; task < NTASK; task += C::NW) {
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
@@ -562,9 +680,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         acc = mfma32(A, Bf, acc);
       }
       const int64_t slab = (int64_t)a.B * a.T * a.H * D;
-      // bf16 slab: a partial over 256 keys rounded once (rel. 2^-9), summed in fp32 by the
-      // reduce -- half the slab bytes of fp32 on both the store and the reduce side
-      uint16_t* dq = a.dq_acc + kb * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
+      uint16_t* dq = a.dq_acc + (kb - a.kb0) * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = qt0 + acc_row(i, hh);
@@ -572,8 +688,26 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       }
     }
   }
-  // write dK (scaled) and dV for this lane's key
-  if (key < a.S) {
+  // write dK (scaled) and dV for this lane's keys; with RoPE, dK is rotated back (R^T): the
+  // lane's d-blocks db and db + NDB/2 hold the partner elements i and i + D/2
+#pragma unroll
+  for (int kh = 0; kh < KH; ++kh) {
+    const int key = kw0 + 32 * kh + r;
+    if (key >= a.S) continue;
+    if (ROPE) {
+      const float* cr = a.rope_cos + (int64_t)key * (D / 2);
+      const float* sr = a.rope_sin + (int64_t)key * (D / 2);
+#pragma unroll
+      for (int db = 0; db < NDB / 2; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int d = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+          const float c = cr[d], sn = sr[d];
+          const float x = dk[kh][db][i], y = dk[kh][db + NDB / 2][i];
+          dk[kh][db][i] = x * c + y * sn;
+          dk[kh][db + NDB / 2][i] = y * c - x * sn;
+        }
+    }
     uint16_t* dkp = a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh;
     uint16_t* dvp = a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh;
 #pragma unroll
@@ -581,10 +715,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         u32x2 k2, v2;
-        k2[0] = pack_bf16x2(dk[db][4 * g] * a.scale, dk[db][4 * g + 1] * a.scale);
-        k2[1] = pack_bf16x2(dk[db][4 * g + 2] * a.scale, dk[db][4 * g + 3] * a.scale);
-        v2[0] = pack_bf16x2(dv[db][4 * g], dv[db][4 * g + 1]);
-        v2[1] = pack_bf16x2(dv[db][4 * g + 2], dv[db][4 * g + 3]);
+        k2[0] = pack_bf16x2(dk[kh][db][4 * g] * a.scale, dk[kh][db][4 * g + 1] * a.scale);
+        k2[1] = pack_bf16x2(dk[kh][db][4 * g + 2] * a.scale, dk[kh][db][4 * g + 3] * a.scale);
+        v2[0] = pack_bf16x2(dv[kh][db][4 * g], dv[kh][db][4 * g + 1]);
+        v2[1] = pack_bf16x2(dv[kh][db][4 * g + 2], dv[kh][db][4 * g + 3]);
         *reinterpret_cast<u32x2*>(dkp + db * 32 + 8 * g + 4 * hh) = k2;
         *reinterpret_cast<u32x2*>(dvp + db * 32 + 8 * g + 4 * hh) = v2;
       }
@@ -592,10 +726,11 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   }
 }
 
-// dq (bf16, strided) = scale * sum over contributing key blocks of the fp32 slabs
-// [nkb][B,T,H,D]; under the causal mask row t only reads blocks kb <= (t+off)/BK
-// (the others were never written for it).
-template <int D, int V>
+// Sum this pass's fp32 dQ slabs [nkb_pass][B,T,H,D] in key-block order (deterministic); under
+// the causal mask row t only reads blocks kb <= (t+off)/BK (the others were never written for
+// it).  Not the last pass: the sum goes on into the fp32 running sum ``dq_sum``; the last pass
+// adds the running sum (if any) and writes dq (bf16, strided) = scale * total.
+template <int D, int V, bool ROPE>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   constexpr int CPR = D / 8;
   constexpr int BK = BwdCfg<D, V>::BK;
@@ -609,19 +744,50 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   const int t = (int)(bt % a.T);
   const int b = (int)(bt / a.T);
   const int nkb = (a.S + BK - 1) / BK;
-  int kmax = nkb - 1;
+  int kmax = min(nkb - 1, a.kb0 + a.nkb_pass - 1);
   if (a.causal) kmax = min(kmax, (t + a.S - a.T) / BK);
   const int64_t slab = nrows * D;
-  float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float f[8];
+  if (a.kb0 > 0) {
+    const f32x4* p = reinterpret_cast<const f32x4*>(a.dq_sum + row * D + c * 8);
+    const f32x4 x0 = p[0], x1 = p[1];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f[j] = x0[j];
+      f[4 + j] = x1[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = 0.f;
+  }
   const uint16_t* src = a.dq_acc + row * D + c * 8;
-  for (int kb = 0; kb <= kmax; ++kb) {
+  for (int kb = a.kb0; kb <= kmax; ++kb) {
     float x[8];
-    unpack8(ld16(src + kb * slab), x);
+    unpack8(ld16(src + (kb - a.kb0) * slab), x);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] += x[j];
   }
+  if (a.kb0 + a.nkb_pass < nkb) {  // more passes follow
+    f32x4* p = reinterpret_cast<f32x4*>(a.dq_sum + row * D + c * 8);
+    p[0] = f32x4{f[0], f[1], f[2], f[3]};
+    p[1] = f32x4{f[4], f[5], f[6], f[7]};
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] *= a.scale;
+  if (ROPE) {
+    // R^T: the partner chunk (c +- CPR/2) of this row is held by lane ^ CPR/2
+    const int lo = c < CPR / 2;
+    const int64_t tab = (int64_t)(t + a.S - a.T) * (D / 2) + (c % (CPR / 2)) * 8;
+    float g[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) g[j] = __shfl_xor(f[j], CPR / 2, 64);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cs = a.rope_cos[tab + j], sn = a.rope_sin[tab + j];
+      f[j] = lo ? f[j] * cs + g[j] * sn : f[j] * cs - g[j] * sn;
+    }
+  }
   st16(a.dq + b * a.dq_sb + (int64_t)t * a.dq_st + (int64_t)h * a.dq_sh + c * 8, pack8(f));
 }
 
@@ -631,31 +797,47 @@ namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-// backward tiling variant for D <= 64 (BwdCfg): 0 = 8-wave 256-key workgroups, 1 = 4-wave
-// 128-key workgroups two per CU
-// v & 1: variant for D <= 64 (default 0); (v >> 1) & 3: variant for D = 128 (default 1) (BwdCfg)
-static int g_bwd_variant = 1 << 1;
-void attn_bwd_set_variant(int v) { g_bwd_variant = v & 7; }
+// backward tiling variants (BwdCfg): bit 0 = variant for D <= 64 (0 / 1), bit 2 = for D = 128
+// (0 -> V 1, 1 -> V 2)
+static int g_bwd_variant = 0;
+void attn_bwd_set_variant(int v) { g_bwd_variant = v & 5; }
+static int v64() { return g_bwd_variant & 1; }
+static int v128() { return 1 + ((g_bwd_variant >> 2) & 1); }
 
 int attn_bwd_key_block(int D) {
-  if (D <= 64) return (g_bwd_variant & 1) ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
-  return BwdCfg<128>::BK;  // 128 keys in every D = 128 variant
+  if (D <= 64) return v64() ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
+  return BwdCfg<128, 1>::BK;  // 128 keys in every D = 128 variant
 }
 
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
-  hipLaunchKernelGGL(attn_fwd_kernel<D>, dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
+  if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
 }
 
-template <int D, int V>
-static void attn_bwd_t(const AttnBwdArgs& a, hipStream_t st) {
+template <int D, int V, bool ROPE>
+static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
   const int nkb = (a.S + BwdCfg<D, V>::BK - 1) / BwdCfg<D, V>::BK;
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((attn_bwd_kernel<D, V>), dim3(nkb * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st, a);
-  hipLaunchKernelGGL((attn_dq_reduce_kernel<D, V>), dim3(pre_grid), dim3(256), 0, st, a);
+  // key blocks in passes of at most a.nkb_pass (bounded slab workspace)
+  const int per = a.nkb_pass;
+  for (int kb0 = 0; kb0 < nkb; kb0 += per) {
+    a.kb0 = kb0;
+    a.nkb_pass = min(per, nkb - kb0);
+    hipLaunchKernelGGL((attn_bwd_kernel<D, V, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st,
+                       a);
+    hipLaunchKernelGGL((attn_dq_reduce_kernel<D, V, ROPE>), dim3(pre_grid), dim3(256), 0, st, a);
+    a.nkb_pass = per;
+  }
+}
+
+template <int D, int V>
+static void attn_bwd_r(const AttnBwdArgs& a, hipStream_t st) {
+  if (a.rope_cos) attn_bwd_t<D, V, true>(a, st);
+  else attn_bwd_t<D, V, false>(a, st);
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
@@ -665,14 +847,9 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
-  if (a.D == 32) (g_bwd_variant & 1) ? attn_bwd_t<32, 1>(a, st) : attn_bwd_t<32, 0>(a, st);
-  else if (a.D == 64) (g_bwd_variant & 1) ? attn_bwd_t<64, 1>(a, st) : attn_bwd_t<64, 0>(a, st);
-  else {
-    const int v = (g_bwd_variant >> 1) & 3;
-    if (v == 0) attn_bwd_t<128, 0>(a, st);
-    else if (v == 1) attn_bwd_t<128, 1>(a, st);
-    else attn_bwd_t<128, 2>(a, st);
-  }
+  if (a.D == 32) v64() ? attn_bwd_r<32, 1>(a, st) : attn_bwd_r<32, 0>(a, st);
+  else if (a.D == 64) v64() ? attn_bwd_r<64, 1>(a, st) : attn_bwd_r<64, 0>(a, st);
+  else v128() == 1 ? attn_bwd_r<128, 1>(a, st) : attn_bwd_r<128, 2>(a, st);
 }
 
 }  // namespace pllm

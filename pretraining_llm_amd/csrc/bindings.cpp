@@ -4,6 +4,7 @@
 // (a wrong shape must fail here, never fault on the GPU) and launches on the
 // current HIP stream, so the ops compose with torch streams and hipGraph capture.
 #include <ATen/ATen.h>
+#include <cstdlib>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
 
@@ -606,7 +607,20 @@ void check_head_view(const Tensor& t, const char* name, int64_t D) {
   check_aligned16(t, name);
 }
 
-std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal, double scale) {
+// fused RoPE tables: fp32 contiguous [>= S, D/2] on the device (both or neither)
+void check_rope(const std::optional<Tensor>& c, const std::optional<Tensor>& sn, int64_t S, int64_t D) {
+  TORCH_CHECK(c.has_value() == sn.has_value(), "attention: rope_cos and rope_sin go together");
+  if (!c) return;
+  for (const Tensor* t : {&*c, &*sn}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->dim() == 2,
+                "attention: rope tables must be contiguous fp32 [positions, D/2] GPU tensors");
+    TORCH_CHECK(t->size(1) == D / 2 && t->size(0) >= S, "attention: rope table shape [>= S, D/2]");
+    check_aligned16(*t, "rope table");
+  }
+}
+
+std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, bool causal, double scale,
+                             const std::optional<Tensor>& rope_cos, const std::optional<Tensor>& rope_sin) {
   const int64_t D = q.size(3);
   TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128, got ", D);
   check_head_view(q, "q", D);
@@ -616,6 +630,7 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   TORCH_CHECK(k.size(0) == B && v.size(0) == B && v.size(1) == S && v.size(2) == Hkv, "k/v shape");
   TORCH_CHECK(H % Hkv == 0, "H % Hkv");
   TORCH_CHECK(!causal || S >= T, "causal attention needs S >= T");
+  check_rope(rope_cos, rope_sin, S, D);
   Tensor o = at::empty({B, T, H, D}, q.options());
   Tensor lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
   AttnFwdArgs a{};
@@ -624,6 +639,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   a.v = (const uint16_t*)v.data_ptr();
   a.o = (uint16_t*)o.data_ptr();
   a.lse = lse.data_ptr<float>();
+  a.rope_cos = rope_cos ? rope_cos->data_ptr<float>() : nullptr;
+  a.rope_sin = rope_sin ? rope_sin->data_ptr<float>() : nullptr;
   a.B = B; a.H = H; a.Hkv = Hkv; a.T = T; a.S = S; a.D = D;
   a.q_sb = q.stride(0); a.q_st = q.stride(1); a.q_sh = q.stride(2);
   a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
@@ -679,9 +696,21 @@ Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, double sca
   return o;
 }
 
+// dQ slab workspace budget of the attention backward (bytes); PLLM_ATTN_BWD_WS_MB or the
+// attn_bwd_set_workspace_mb op (tests force multi-pass runs with it)
+int64_t g_attn_ws_bytes = -1;
+int64_t attn_bwd_ws_bytes() {
+  if (g_attn_ws_bytes < 0) {
+    const char* e = std::getenv("PLLM_ATTN_BWD_WS_MB");
+    g_attn_ws_bytes = (int64_t)((e ? std::atof(e) : 1024.0) * (1 << 20));
+  }
+  return g_attn_ws_bytes;
+}
+
 // dq/dk/dv are written into caller-provided views (e.g. slices of a packed dQKV buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
-              Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale) {
+              Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale, const std::optional<Tensor>& rope_cos,
+              const std::optional<Tensor>& rope_sin) {
   const int64_t D = q.size(3);
   TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128");
   for (auto& pr : std::vector<std::pair<const Tensor*, const char*>>{
@@ -691,12 +720,20 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(), "attn bwd q-side shapes");
   TORCH_CHECK(dk.sizes() == k.sizes() && dv.sizes() == v.sizes() && v.sizes() == k.sizes(), "attn bwd kv-side shapes");
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse shape");
+  check_rope(rope_cos, rope_sin, S, D);
   auto f32 = q.options().dtype(at::kFloat);
   Tensor delta = at::empty({B, H, T}, f32);
-  // per-key-block dQ partial slabs (attention.hip: plain stores + ordered reduce, no atomics)
+  // per-key-block bf16 dQ partial slabs (attention.hip: plain stores + ordered fp32 reduce, no
+  // atomics), run in passes of at most `per` key blocks: the workspace is bounded by
+  // PLLM_ATTN_BWD_WS_MB (default 1024 MiB) however long the sequence, plus one fp32 running
+  // sum when more than one pass is needed
   const int64_t kbk = pllm::attn_bwd_key_block((int)D);
   const int64_t nkb = (S + kbk - 1) / kbk;
-  Tensor dq_acc = at::empty({nkb, B, T, H, D}, q.options());  // bf16 partial slabs
+  const int64_t slab_bytes = B * T * H * D * 2;
+  const int64_t ws_budget = attn_bwd_ws_bytes();
+  const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nkb, ws_budget / std::max<int64_t>(1, slab_bytes)));
+  Tensor dq_acc = at::empty({per, B, T, H, D}, q.options());  // bf16 partial slabs
+  Tensor dq_sum = per < nkb ? at::empty({B, T, H, D}, q.options().dtype(at::kFloat)) : Tensor();
   AttnBwdArgs a{};
   a.q = (const uint16_t*)q.data_ptr();
   a.k = (const uint16_t*)k.data_ptr();
@@ -704,8 +741,13 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.o = (const uint16_t*)o.data_ptr();
   a.dO = (const uint16_t*)dout.data_ptr();
   a.lse = lse.data_ptr<float>();
+  a.rope_cos = rope_cos ? rope_cos->data_ptr<float>() : nullptr;
+  a.rope_sin = rope_sin ? rope_sin->data_ptr<float>() : nullptr;
   a.delta = delta.data_ptr<float>();
   a.dq_acc = (uint16_t*)dq_acc.data_ptr();
+  a.dq_sum = dq_sum.defined() ? dq_sum.data_ptr<float>() : nullptr;
+  a.kb0 = 0;
+  a.nkb_pass = (int)per;
   a.dq = (uint16_t*)dq.data_ptr();
   a.dk = (uint16_t*)dk.data_ptr();
   a.dv = (uint16_t*)dv.data_ptr();
@@ -734,6 +776,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_variant(int v) -> ()", [](int64_t v) { pllm::attn_bwd_set_variant((int)v); });
+  m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");
   m.def("act_fwd(Tensor x, int op) -> Tensor");
   m.def("act_bwd(Tensor dy, Tensor x, int op) -> Tensor");
@@ -751,9 +794,9 @@ TORCH_LIBRARY(pllm, m) {
   m.def("transpose_plan(Tensor[] src, Tensor[] dst) -> Tensor");
   m.def("transpose_run(Tensor desc, int total_tiles) -> ()");
   m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
-  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale) -> Tensor[]");
+  m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None) -> Tensor[]");
   m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, Tensor? seqlen=None) -> Tensor");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(pllm, CUDA, m) {

@@ -10,6 +10,9 @@ struct AttnFwdArgs {
   const uint16_t *q, *k, *v;
   uint16_t* o;
   float* lse;  // [B, H, T] natural-log LSE, may be null
+  // optional fused RoPE (rotate-half) of q and k: fp32 tables [>= S, D/2]; query row t sits at
+  // position t + S - T, key row j at position j
+  const float *rope_cos, *rope_sin;
   int B, H, Hkv, T, S, D;
   int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
   float scale, scale_log2;
@@ -30,8 +33,11 @@ struct DecodeArgs {
 struct AttnBwdArgs {
   const uint16_t *q, *k, *v, *o, *dO;
   const float* lse;
+  const float *rope_cos, *rope_sin;  // optional fused RoPE (as AttnFwdArgs); dq/dk un-rotated
   float* delta;   // [B, H, T] scratch
-  uint16_t* dq_acc;  // [nkb][B, T, H, D] bf16 per-key-block dQ partial slabs
+  uint16_t* dq_acc;  // [nkb_pass][B, T, H, D] bf16 per-key-block dQ partial slabs of one pass
+  float* dq_sum;  // [B, T, H, D] fp32 running dQ sum across passes (null when one pass)
+  int kb0, nkb_pass;  // first key block of the pass / key blocks per pass (set by the host)
   uint16_t *dq, *dk, *dv;
   int B, H, Hkv, T, S, D;
   int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh, do_sb, do_st, do_sh;

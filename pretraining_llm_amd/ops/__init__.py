@@ -381,26 +381,30 @@ def _split_qkv(qkv, H, Hkv, D):
 
 
 class _FlashAttnPacked(torch.autograd.Function):
+    """Attention over the packed QKV projection; with ``cos``/``sin`` the q and k heads are
+    rotated (RoPE) inside the kernels -- forward and backward -- and the gradient comes back
+    for the unrotated packed tensor (no separate RoPE launches, csrc/attention.hip)."""
+
     @staticmethod
-    def forward(ctx, qkv, H, Hkv, causal, scale):
+    def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin):
         B, T, W = qkv.shape
         D = W // (H + 2 * Hkv)
         q, k, v = _split_qkv(qkv, H, Hkv, D)
-        o, lse = _ops().attn_fwd(q, k, v, causal, scale)
-        ctx.save_for_backward(qkv, o, lse)
+        o, lse = _ops().attn_fwd(q, k, v, causal, scale, cos, sin)
+        ctx.save_for_backward(qkv, o, lse, cos, sin)
         ctx.cfg = (H, Hkv, D, causal, scale)
         return o.view(B, T, H * D)
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse = ctx.saved_tensors
+        qkv, o, lse, cos, sin = ctx.saved_tensors
         H, Hkv, D, causal, scale = ctx.cfg
         B, T, _ = qkv.shape
         q, k, v = _split_qkv(qkv, H, Hkv, D)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = _split_qkv(dqkv, H, Hkv, D)
-        _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale)
-        return dqkv, None, None, None, None
+        _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin)
+        return dqkv, None, None, None, None, None, None
 
 
 class _RopePackedFn(torch.autograd.Function):
@@ -440,10 +444,11 @@ def attention_packed(qkv, n_head: int, n_kv_head: int, causal: bool = True, scal
     B, T, W = qkv.shape
     D = W // (n_head + 2 * n_kv_head)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    if _hip(qkv):
+        # RoPE fused into the attention kernels (q/k rotated while staged, dq/dk rotated back)
+        return _FlashAttnPacked.apply(qkv, n_head, n_kv_head, causal, scale, rope_cos, rope_sin)
     if rope_cos is not None:
         qkv = rope_packed(qkv, rope_cos, rope_sin, n_head, n_kv_head)
-    if _hip(qkv):
-        return _FlashAttnPacked.apply(qkv, n_head, n_kv_head, causal, scale)
     q, k, v = _split_qkv(qkv, n_head, n_kv_head, D)
     if _BACKEND == "torch" and qkv.is_cuda:
         # stock-PyTorch baseline path (SDPA), used only by the explicit torch backend

@@ -120,7 +120,7 @@ def register() -> None:
         return logits.new_empty((logits.shape[0], 1), dtype=torch.int64)
 
     @_reg("attn_fwd")
-    def _(q, k, v, causal, scale):
+    def _(q, k, v, causal, scale, rope_cos=None, rope_sin=None):
         B, T, H, _ = q.shape
         return [q.new_empty(q.shape), q.new_empty((B, H, T), dtype=f32)]
 
@@ -129,7 +129,7 @@ def register() -> None:
         return q.new_empty(q.shape)
 
     @_reg("attn_bwd")
-    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale):
+    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, rope_cos=None, rope_sin=None):
         return None
 
     @_reg("gemv")

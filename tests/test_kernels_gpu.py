@@ -813,3 +813,70 @@ def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
     ops.lm_head_cross_entropy(h, W, b, t).backward()
     assert W.grad is None
     assert _rel(W._pllm_gradbuf.double() - 1, 2 * Wf.grad.double()) < 3e-2
+
+
+def _bwd_variants(D):
+    # attn_bwd_set_variant encoding: bit 0 = D <= 64 variant, bit 2 = D = 128 variant
+    return [0, 1] if D <= 64 else [0, 4]
+
+
+@pytest.mark.parametrize("D,T,H,Hkv,B", [(32, 1024, 4, 4, 2), (64, 2048, 4, 2, 1), (64, 4096, 2, 2, 1),
+                                         (128, 2048, 4, 1, 1), (128, 4096, 2, 2, 1), (64, 1000, 4, 4, 2)])
+def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
+    """Backward at the shipped sequence lengths (2048 / 4096, several key blocks and dQ slabs),
+    D = 32 / 64 / 128, GQA, ragged T, every tiling variant, vs fp32 torch; a forced multi-pass
+    run (bounded dQ workspace) is bit-identical to the single-pass one."""
+    torch.manual_seed(T + D)
+    q = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    k = torch.randn(B, T, Hkv, D, device=DEV).bfloat16()
+    v = torch.randn(B, T, Hkv, D, device=DEV).bfloat16()
+    do = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    o, lse = torch.ops.pllm.attn_fwd(q, k, v, True, scale)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = _attn_ref(qf, kf, vf, True, scale)
+    of.backward(do.float())
+    try:
+        for var in _bwd_variants(D):
+            torch.ops.pllm.attn_bwd_set_variant(var)
+            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+            torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, True, scale)
+            for a, b, n in ((dq, qf.grad, "dq"), (dk, kf.grad, "dk"), (dv, vf.grad, "dv")):
+                assert _rel(a, b) < 2e-2, (var, n, _rel(a, b))
+        torch.ops.pllm.attn_bwd_set_variant(0)
+        ref = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *ref, True, scale)
+        torch.ops.pllm.attn_bwd_set_workspace_mb(1e-3)  # one key block per pass
+        got = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *got, True, scale)
+        for a, b in zip(got, ref):
+            assert torch.equal(a, b)
+    finally:
+        torch.ops.pllm.attn_bwd_set_variant(0)
+        torch.ops.pllm.attn_bwd_set_workspace_mb(1024)
+
+
+@pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1)])
+def test_attention_fused_rope_fwd_bwd(D, Hkv):
+    """RoPE applied inside the attention kernels (q/k rotated while staged, dq/dk rotated back)
+    == rotate-half RoPE + attention in fp32 torch, gradients w.r.t. the UNROTATED packed qkv."""
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.ops import reference as ref
+    torch.manual_seed(29 + D)
+    B, T, H = 2, 640, 4
+    qkv = (torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV) * 0.8).bfloat16().requires_grad_()
+    cos, sin = ops.rope_cache(T + 64, D, 10000.0, DEV)  # table longer than T, as in the model
+    o = ops.attention_packed(qkv, H, Hkv, causal=True, rope_cos=cos, rope_sin=sin)
+    do = torch.randn_like(o)
+    o.backward(do)
+    qkvf = qkv.detach().float().requires_grad_()
+    q, k, v = ops._split_qkv(qkvf, H, Hkv, D)
+    qr, kr = ref.rope(q, cos[:T], sin[:T]), ref.rope(k, cos[:T], sin[:T])
+    of, _ = _attn_ref(qr, kr, v, True, 1 / math.sqrt(D))
+    of = of.reshape(B, T, H * D)
+    of.backward(do.float())
+    assert _rel(o, of) < 1.5e-2, _rel(o, of)
+    gq, gk, gv = ops._split_qkv(qkv.grad, H, Hkv, D)
+    rq, rk, rv = ops._split_qkv(qkvf.grad, H, Hkv, D)
+    for a, b, n in ((gq, rq, "q"), (gk, rk, "k"), (gv, rv, "v")):
+        assert _rel(a, b) < 3e-2, (n, _rel(a, b))
