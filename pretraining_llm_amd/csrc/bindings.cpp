@@ -702,7 +702,7 @@ int64_t g_attn_ws_bytes = -1;
 int64_t attn_bwd_ws_bytes() {
   if (g_attn_ws_bytes < 0) {
     const char* e = std::getenv("PLLM_ATTN_BWD_WS_MB");
-    g_attn_ws_bytes = (int64_t)((e ? std::atof(e) : 1024.0) * (1 << 20));
+    g_attn_ws_bytes = (int64_t)((e ? std::atof(e) : 4096.0) * (1 << 20));
   }
   return g_attn_ws_bytes;
 }
@@ -725,7 +725,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   Tensor delta = at::empty({B, H, T}, f32);
   // per-key-block bf16 dQ partial slabs (attention.hip: plain stores + ordered fp32 reduce, no
   // atomics), run in passes of at most `per` key blocks: the workspace is bounded by
-  // PLLM_ATTN_BWD_WS_MB (default 1024 MiB) however long the sequence, plus one fp32 running
+  // PLLM_ATTN_BWD_WS_MB (default 4096 MiB: one pass for every shipped config -- passes split the
+  // causal work unevenly, 2 passes cost llama-1.3B +20 %) however long the sequence, plus one fp32 running
   // sum when more than one pass is needed
   const int64_t kbk = pllm::attn_bwd_key_block((int)D);
   const int64_t nkb = (S + kbk - 1) / kbk;

@@ -853,7 +853,7 @@ def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
             assert torch.equal(a, b)
     finally:
         torch.ops.pllm.attn_bwd_set_variant(0)
-        torch.ops.pllm.attn_bwd_set_workspace_mb(1024)
+        torch.ops.pllm.attn_bwd_set_workspace_mb(4096)
 
 
 @pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1)])
