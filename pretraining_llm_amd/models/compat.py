@@ -49,6 +49,9 @@ def strip_wrapper_prefixes(sd: dict) -> dict:
 
 def _split_state(model, state_dict, prefix, local_metadata):
     cfg: ModelConfig = model.config
+    pg = getattr(model, "parallel", None)
+    if pg is not None and pg.tp > 1:
+        return state_dict  # a tensor-parallel shard keeps its packed local layout
     H, D, T = cfg.n_head, cfg.head_dim, cfg.context_length
     tril = None
     for key in [k for k in list(state_dict.keys()) if k.startswith(prefix)]:

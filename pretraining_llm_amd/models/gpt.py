@@ -175,7 +175,7 @@ class Block(nn.Module):
         projection's bias by ln2's backward; with ``fuse_mlp_out_bias`` the caller promises to pass
         this block's ``mlp.proj.bias`` as ``x_bias`` of the next norm."""
         fuse = ops._hip(x) and torch.is_grad_enabled() and self.attn.proj is not None \
-            and self.attn.proj.bias is not None
+            and self.attn.proj.bias is not None and getattr(self.attn, "fused_bias_ok", True)
         h, res = self.ln1(x, residual, x_bias=x_bias)
         a = self.attn(h, rope, fuse_out_bias=fuse)
         h2, res2 = self.ln2(a, res, x_bias=self.attn.proj.bias if fuse else None)
@@ -184,7 +184,8 @@ class Block(nn.Module):
     def fused_out_bias(self, x):
         """The bias the next norm must take as ``x_bias`` when fuse_mlp_out_bias=True (or None)."""
         if ops._hip(x) and torch.is_grad_enabled() and self.mlp.proj.bias is not None \
-                and self.attn.proj is not None and self.attn.proj.bias is not None:
+                and self.attn.proj is not None and self.attn.proj.bias is not None \
+                and getattr(self.attn, "fused_bias_ok", True) and getattr(self.mlp, "fused_bias_ok", True):
             return self.mlp.proj.bias
         return None
 
@@ -243,6 +244,7 @@ class GPT(nn.Module):
             from .compat import install_ref_state_dict_hooks
             install_ref_state_dict_hooks(self)
         self._rope = None
+        self.parallel = None  # ParallelGroups once parallel.model_parallel.parallelize_gpt ran
         self.reset_parameters()
 
     # ------------------------------------------------------------------
@@ -337,16 +339,51 @@ class GPT(nn.Module):
         return sum(p.numel() for p in self.parameters())
 
     # ------------------------------------------------------------------
-    def _embed(self, idx):
+    def _embed(self, idx, positions=None):
         wpe = self.position_embed.weight if self.position_embed is not None else None
         T = idx.shape[1]
-        if T > self.config.context_length and wpe is not None:
+        if T > self.config.context_length and wpe is not None and positions is None:
             raise ValueError(f"sequence length {T} > context_length {self.config.context_length}")
+        if positions is not None and wpe is not None:
+            wpe = wpe.index_select(0, positions)  # a CP / SP shard's global positions
         return ops.embedding(idx, self.token_embed.weight, wpe)
 
+    def _cp_positions(self, idx):
+        pg = self.parallel
+        if pg is None or pg.cp == 1:
+            return None
+        from ..parallel.context import zigzag_positions
+        return zigzag_positions(idx.shape[1], pg.cp_group, idx.device)
+
+    def _shard_inputs(self, idx, targets):
+        """Model parallelism: every rank of a TP / CP group receives the same full batch; CP keeps
+        this rank's zigzag sequence shard (sequence parallelism splits after the embedding)."""
+        pg = self.parallel
+        if pg is not None and pg.cp > 1:
+            from ..parallel.context import zigzag_shard
+            idx = zigzag_shard(idx, 1, pg.cp_group)
+            targets = zigzag_shard(targets, 1, pg.cp_group) if targets is not None else None
+        return idx, targets
+
     def _trunk(self, idx):
-        x = self._embed(idx)
-        rope = self.rope_tables(idx.device, idx.shape[1])
+        pos = self._cp_positions(idx)
+        pg = self.parallel
+        if pg is not None and pg.sequence_parallel:
+            # sequence parallelism: embed only this rank's T/tp tokens (no collective; the
+            # replicated embedding tables get this shard's partial gradient like every other
+            # replicated parameter, summed over the TP group by sync_replicated_grads)
+            from ..parallel.tensor import _split_dim
+            T = idx.shape[1]
+            if T % pg.tp:
+                raise ValueError(f"sequence_parallel: seq_len {T} must be divisible by tp_size {pg.tp}")
+            Tl = T // pg.tp
+            x = self._embed(_split_dim(idx, 1, pg.tp_group),
+                            torch.arange(pg.tp_rank * Tl, (pg.tp_rank + 1) * Tl, device=idx.device))
+        else:
+            x = self._embed(idx, pos)
+        rope = self.rope_tables(idx.device, idx.shape[1] if pos is None else self.config.context_length)
+        if rope is not None and pos is not None:
+            rope = (rope[0].index_select(0, pos).contiguous(), rope[1].index_select(0, pos).contiguous())
         res = None
         n_ckpt = self.checkpointed_blocks(idx) if self.training and torch.is_grad_enabled() else 0
         x_bias = None  # bias of the layer that produced x (fused into the next norm's backward)
@@ -361,7 +398,14 @@ class GPT(nn.Module):
 
     def forward(self, idx: torch.Tensor, targets: Optional[torch.Tensor] = None,
                 return_logits: bool = True) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+        """Under tensor/sequence/context parallelism the loss is the mean over THIS rank's tokens
+        (SP / CP: its sequence shard); the Trainer scales the gradients accordingly."""
+        idx, targets = self._shard_inputs(idx, targets)
         h = self._trunk(idx)
+        pg = self.parallel
+        if targets is not None and pg is not None and pg.sequence_parallel:
+            from ..parallel.tensor import _split_dim
+            targets = _split_dim(targets, 1, pg.tp_group)
         B, T, C = h.shape
         if targets is None:
             logits = ops.linear(h, self.head_weight, self.head_bias)
@@ -389,6 +433,9 @@ class GPT(nn.Module):
     def generate(self, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0,
                  top_k: Optional[int] = None, use_cache: bool = True, generator=None,
                  cuda_graph: bool = False) -> torch.Tensor:
+        if self.parallel is not None and self.parallel.model_parallel:
+            raise ValueError("generate() runs on a dense model: load the consolidated checkpoint "
+                             "(Trainer.save writes one) or parallel.model_parallel.gather_dense_state")
         from ..inference.generate import generate
         return generate(self, idx, max_new_tokens, temperature=temperature, top_k=top_k,
                         use_cache=use_cache, generator=generator, cuda_graph=cuda_graph)

@@ -93,14 +93,20 @@ class ShardedFlatAdamW(FlatAdamW):
         self._inplace_ag = dist.is_initialized() and dist.get_backend(process_group) == "nccl"
 
     # ------------------------------------------------------------------
+    def replicated_grad_ranges(self):
+        """The TP-replicated parameters' owned slices, in ``grad_shard`` coordinates."""
+        ranges = [(o + max(a, fs) - fs, o + min(b, fe) - fs) for fs, fe, o in self.own
+                  for a, b in self._rep_ranges if max(a, fs) < min(b, fe)]
+        return self.grad_shard, ranges
+
     def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
-        if self.use_hip and _ops_mod.get_backend() == "auto":
-            ss = _lib.require().sumsq(self.grad_shard)
-        else:
-            ss = self.grad_shard.float().pow(2).sum()
-        ss = ss.reshape(1).float()
+        ss = self._sumsq(self.grad_shard)
+        if getattr(self, "tp", 1) > 1:
+            ss = self._tp_adjust(ss)
         if self.world > 1:
             dist.all_reduce(ss, op=dist.ReduceOp.SUM, group=self.pg)
+        if getattr(self, "tp", 1) > 1:
+            dist.all_reduce(ss, op=dist.ReduceOp.SUM, group=self.tp_group)
         return ss[0].sqrt() * grad_scale
 
     def _update_part(self, fs, fe, o, grad_scale, clip):

@@ -175,12 +175,39 @@ class FlatAdamW:
     def _sync_lr(self):
         self.lr = self.param_groups[0]["lr"]
 
-    def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
+    def _sumsq(self, buf: torch.Tensor) -> torch.Tensor:
         if self.use_hip and _ops_mod.get_backend() == "auto":
-            ss = _lib.require().sumsq(self.flat_grad)
-        else:
-            ss = self.flat_grad.float().pow(2).sum()
-        return ss.sqrt() * grad_scale
+            return _lib.require().sumsq(buf).reshape(1).float()
+        return buf.float().pow(2).sum().reshape(1)
+
+    def set_tensor_parallel(self, group, tp: int):
+        """Tensor parallelism (parallel/model_parallel.py): the global gradient norm sums the
+        sharded parameters over the TP group and counts the replicated ones (norms, embeddings,
+        LM head, row-parallel biases -- identical on every TP rank) once."""
+        self.tp_group, self.tp = group, tp
+        self._rep_ranges = [(self.offsets[i], self.offsets[i] + p.numel()) for i, p in enumerate(self.params)
+                            if not getattr(p, "_pllm_tp_sharded", False)]
+
+    def replicated_grad_ranges(self):
+        """(buffer the optimizer step reads, [(start, end)] of the TP-replicated parameters in it)."""
+        return self.flat_grad, self._rep_ranges
+
+    def _tp_adjust(self, ss: torch.Tensor) -> torch.Tensor:
+        """ss (this rank's local sum of squares of its gradient buffer) -> this rank's share of the
+        global one: replicated ranges weighted 1/tp, so a SUM over the TP group counts them once."""
+        buf, ranges = self.replicated_grad_ranges()
+        if ranges:
+            rep = self._sumsq(torch.cat([buf[a:b] for a, b in ranges]))
+            ss = ss - rep * (1.0 - 1.0 / self.tp)
+        return ss
+
+    def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
+        ss = self._sumsq(self.flat_grad)
+        if getattr(self, "tp", 1) > 1:
+            import torch.distributed as dist
+            ss = self._tp_adjust(ss)
+            dist.all_reduce(ss, op=dist.ReduceOp.SUM, group=self.tp_group)
+        return ss[0].sqrt() * grad_scale
 
     @torch.no_grad()
     def prepare_graph_step(self, lr: float):

@@ -31,6 +31,8 @@ from .. import ops
 from ..data import TokenLoader, ensure_synthetic_shard
 from ..models import GPT, ModelConfig, get_preset
 from ..parallel.dp import DataParallelEngine, all_reduce_mean
+from ..parallel.model_parallel import (gather_dense_state, init_parallel_groups, parallelize_gpt,
+                                       sync_replicated_grads)
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from ..utils.dist import DistInfo, init_distributed
 from ..utils.metrics import MetricsLogger, mfu, peak_memory_gb
@@ -87,6 +89,12 @@ class Trainer:
         else:
             self.dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}[dtype_name]
         self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
+        # model parallelism (parallel/model_parallel.py): a dp x cp x tp mesh; the model is built
+        # dense from the shared seed, then sharded, so every layout starts from the same weights
+        tp, cp = int(self.cfg.get("tp_size", 1)), int(self.cfg.get("cp_size", 1))
+        self.pg = init_parallel_groups(tp, cp, bool(self.cfg.get("sequence_parallel", False)))
+        if self.pg.model_parallel:
+            parallelize_gpt(self.model, self.pg)
         decay_filter = None if self.cfg.get("weight_decay_all", True) else no_decay_1d
         okw = dict(lr=self.cfg["t_lr"], betas=tuple(self.cfg.get("betas", (0.9, 0.999))),
                    eps=self.cfg.get("eps", 1e-8), weight_decay=self.cfg.get("weight_decay", 0.01),
@@ -95,11 +103,14 @@ class Trainer:
         if int(self.cfg.get("zero_stage", 0)) >= 1:
             # ZeRO-1: fp32 master + moments sharded over the DP ranks (parallel/zero.py)
             from ..parallel.zero import ShardedFlatAdamW, ZeroDataParallelEngine
-            self.opt = ShardedFlatAdamW(self.model, **okw, **bkw)
+            self.opt = ShardedFlatAdamW(self.model, process_group=self.pg.grad_group, **okw, **bkw)
             self.engine = ZeroDataParallelEngine(self.opt)
         else:
             self.opt = FlatAdamW(self.model, **okw)
-            self.engine = DataParallelEngine(self.opt, **bkw)
+            # gradients are averaged over the ranks that hold the same shard: dp x cp
+            self.engine = DataParallelEngine(self.opt, process_group=self.pg.grad_group, **bkw)
+        if self.pg.tp > 1:
+            self.opt.set_tensor_parallel(self.pg.tp_group, self.pg.tp)  # global grad norm over TP shards
         self.accum = int(self.cfg.get("grad_accum_steps", 1))
         self.step = 0
         # TORCH_COMPILE (reference: torch.compile(model) when the env var is "1",
@@ -116,7 +127,8 @@ class Trainer:
         self.fwd = self.model
         if self.compile and self.device.type == "cuda":
             why = ("grad_accum_steps > 1" if self.accum > 1 else "ZeRO-1 (collectives inside the optimizer step)"
-                   if int(self.cfg.get("zero_stage", 0)) >= 1 else None)
+                   if int(self.cfg.get("zero_stage", 0)) >= 1 else "tensor / context parallelism"
+                   if self.pg.model_parallel else None)
             if why is None:
                 self.use_graph = True
             elif self.di.is_master:
@@ -147,8 +159,9 @@ class Trainer:
                                        stream=stream, fast=None if kind == "auto" else kind == "fast")
             if dist.is_initialized():
                 dist.barrier()
-        return TokenLoader(path, self.cfg["t_batch_size"], self.seq_len, self.di.rank,
-                           self.di.world_size, seed=seed, start_batch=start, device=self.device)
+        # every rank of a TP / CP group reads the same batch: shard the data over dp only
+        return TokenLoader(path, self.cfg["t_batch_size"], self.seq_len, self.pg.dp_rank,
+                           self.pg.dp, seed=seed, start_batch=start, device=self.device)
 
     def lr(self, step: int) -> float:
         return lr_at(step, self.cfg)
@@ -169,6 +182,12 @@ class Trainer:
                 loss.backward()
             total += loss.detach().float()
         scale = self.engine.finish_grad_sync()
+        if self.pg.sequence_parallel:
+            # each TP rank's loss is the mean over its T/tp tokens: replicated parameters hold
+            # partial gradients (summed over the TP group here) and every gradient is tp x the
+            # gradient of the global mean
+            sync_replicated_grads(self.opt, self.pg)
+            scale /= self.pg.tp
         self.opt.step(grad_scale=scale / self.accum)
         self.opt.zero_grad()
         self.step += 1
@@ -301,6 +320,8 @@ class Trainer:
     def save(self, path: str):
         data_state = {"train_batches": self.train_loader.batches_consumed,
                       "val_batches": self.val_loader.batches_consumed if self.val_loader else 0}
+        if self.pg.tp > 1:
+            return self._save_tp(path, data_state)
         # a sharded optimizer consolidates its state collectively (every rank), rank 0 writes it
         osd = self.opt.state_dict() if getattr(self.opt, "collective_state", False) else None
         if self.di.is_master:
@@ -310,11 +331,39 @@ class Trainer:
         if dist.is_initialized():
             dist.barrier()
 
+    def _save_tp(self, path: str, data_state: dict):
+        """Tensor parallelism: each TP rank of replica (dp 0, cp 0) writes its shard with its optimizer
+        state to ``path.tp{r}`` (what ``resume`` reads back), and global rank 0 writes the
+        consolidated dense fp32 checkpoint in the reference format to ``path`` (generate_text.py
+        loads it as usual).  Collective over the TP group of that replica."""
+        pg = self.pg
+        osd = self.opt.state_dict()  # collective for ZeRO (over the dp x cp group)
+        writer = pg.dp_rank == 0 and pg.cp_rank == 0
+        if writer:
+            save_checkpoint(f"{path}.tp{pg.tp_rank}", self.model, optimizer_state=osd, params=self.opt.params,
+                            step=self.step, config=self.cfg, data_state=data_state,
+                            extra={"tp_rank": pg.tp_rank, "tp_size": pg.tp})
+            masters = None
+            if not getattr(self.opt, "collective_state", False):
+                masters = {id(p): self.opt.master[self.opt.offsets[i]:self.opt.offsets[i] + p.numel()].view(p.shape)
+                           for i, p in enumerate(self.opt.params)}
+            dense = GPT(self.mcfg).to(device=self.device, dtype=torch.float32)
+            gather_dense_state(self.model, dense, pg, masters)
+            if self.di.is_master:
+                save_checkpoint(path, dense, step=self.step, config=self.cfg, data_state=data_state,
+                                extra={"tp_size": pg.tp, "tp_shards": [f"{path}.tp{r}" for r in range(pg.tp)]})
+                self.log(f"saved checkpoint to {path} (+{pg.tp} tensor-parallel shards, step {self.step})")
+            del dense
+        if dist.is_initialized():
+            dist.barrier()
+
     def resume(self, path: str):
         if path == "auto":
             path = self._ckpt_path(periodic=True)
             if not os.path.exists(path):
                 return
+        if self.pg.tp > 1:
+            path = f"{path}.tp{self.pg.tp_rank}"  # this rank's shard (and its optimizer state)
         ck = load_checkpoint(path, map_location="cpu")
         missing, unexpected = self.model.load_state_dict(ck["model_state_dict"], strict=False)
         missing = [k for k in missing if not k.endswith("pos_idxs")]
