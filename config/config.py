@@ -53,7 +53,10 @@ default_config = {
 
     # --- keys the reference scripts read but never defined ---------------
     'ddp_backend': 'nccl',            # = RCCL on ROCm (train_transformer.py:17)
-    'dtype': 'bfloat16',              # compute dtype (train_transformer.py:41)
+    'dtype': 'bfloat16',              # bfloat16 (HIP kernels) | float16 (fp16 autocast + loss scaling) | float32 (train/amp.py)
+    'loss_scaling': None,             # dynamic loss scaling (GradScaler semantics); None = on iff dtype == 'float16'
+    'loss_scale_init': 65536.0,
+    'loss_scale_growth_interval': 2000,
     'val_path': DEV_PATH,             # alias of dev_path (train_transformer.py:134)
     'dataset_name': 'openwebtext',    # scripts/data_preprocess.py:12, data_download.py:12
     'tokenizer_name': 'gpt2',         # scripts/data_preprocess.py:15

@@ -114,7 +114,7 @@ def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[
     if top_k is not None and top_k < logits.shape[-1] and temperature != 0.0:
         v, _ = torch.topk(logits, top_k)
         logits = logits.masked_fill(logits < v[:, [-1]], float("-inf"))
-    if ops._hip(logits):
+    if logits.is_cuda and ops.get_backend() == "auto":  # fp32 logits of any model dtype
         seed = 0
         if temperature != 0.0:
             gdev = generator.device if generator is not None else "cpu"

@@ -5,8 +5,12 @@ The extension is built by ``pretraining_llm_amd/build.py`` with ``hipcc
 registers its ops under ``torch.ops.pllm``.
 
 Policy (no silent fallback on a GPU):
-* CUDA(HIP) tensors always go to the HIP kernels.  If the extension is
-  missing when a GPU op is requested, ``require()`` raises.
+* bf16 CUDA(HIP) tensors always go to the HIP kernels (the hand-written kernels
+  are bf16: the training compute dtype).  If the extension is missing when a GPU
+  op is requested, ``require()`` raises.
+* fp32 / fp16 CUDA tensors -- only the explicitly selected ``dtype='float32'`` and
+  ``dtype='float16'`` (fp16 autocast + dynamic loss scaling) training modes make
+  them -- run the PyTorch implementation of the op (hipBLASLt GEMMs through torch).
 * CPU tensors use the pure-PyTorch reference implementation of the same op
   (which is also the numerics oracle for the tests).
 """
@@ -60,11 +64,15 @@ def require():
 
 
 def use_hip(*tensors) -> bool:
-    """True when the op must run on the HIP kernels (any CUDA/HIP tensor)."""
+    """True when the op must run on the HIP kernels: a CUDA/HIP tensor whose first
+    floating-point CUDA operand is bf16 (integer-only operands: any CUDA tensor)."""
+    cuda = False
     for t in tensors:
         if isinstance(t, torch.Tensor) and t.is_cuda:
-            return True
-    return False
+            if t.is_floating_point():
+                return t.dtype == torch.bfloat16
+            cuda = True
+    return cuda
 
 
 def error() -> str | None:

@@ -34,6 +34,7 @@ from ..parallel.dp import DataParallelEngine, all_reduce_mean
 from ..parallel.model_parallel import (gather_dense_state, init_parallel_groups, parallelize_gpt,
                                        sync_replicated_grads)
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
+from .amp import DynamicLossScaler, autocast_ctx, precision_mode
 from ..utils.dist import DistInfo, init_distributed
 from ..utils.metrics import MetricsLogger, mfu, peak_memory_gb
 from .optim import FlatAdamW, no_decay_1d
@@ -83,11 +84,14 @@ class Trainer:
             torch.use_deterministic_algorithms(True, warn_only=True)
         self.mcfg = model_config_from(self.cfg)
         self.seq_len = int(self.cfg.get("seq_len") or self.mcfg.context_length)
+        # precision (train/amp.py): bf16 on the HIP kernels; float16 = fp32 weights + fp16 autocast
+        # + dynamic loss scaling; float32 = fp32 through torch
         dtype_name = self.cfg.get("dtype", "bfloat16")
-        if self.device.type == "cpu" and not self.cfg.get("cpu_bf16", False):
-            self.dtype = torch.float32
-        else:
-            self.dtype = {"bfloat16": torch.bfloat16, "float32": torch.float32, "float16": torch.float16}[dtype_name]
+        self.dtype, self.autocast_dtype = precision_mode(dtype_name, self.device, bool(self.cfg.get("cpu_bf16", False)))
+        ls = self.cfg.get("loss_scaling")
+        self.scaler = DynamicLossScaler(init_scale=float(self.cfg.get("loss_scale_init", 2.0 ** 16)),
+                                        growth_interval=int(self.cfg.get("loss_scale_growth_interval", 2000)),
+                                        enabled=(dtype_name == "float16") if ls is None else bool(ls))
         self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
         # model parallelism (parallel/model_parallel.py): a dp x cp x tp mesh; the model is built
         # dense from the shared seed, then sharded, so every layout starts from the same weights
@@ -128,7 +132,9 @@ class Trainer:
         if self.compile and self.device.type == "cuda":
             why = ("grad_accum_steps > 1" if self.accum > 1 else "ZeRO-1 (collectives inside the optimizer step)"
                    if int(self.cfg.get("zero_stage", 0)) >= 1 else "tensor / context parallelism"
-                   if self.pg.model_parallel else None)
+                   if self.pg.model_parallel else "loss scaling (host-side skip decision)" if self.scaler.enabled
+                   else f"dtype={dtype_name} (the graphed step runs the bf16 HIP kernels)"
+                   if self.dtype != torch.bfloat16 else None)
             if why is None:
                 self.use_graph = True
             elif self.di.is_master:
@@ -178,8 +184,9 @@ class Trainer:
             x, y = self.train_loader.next()
             ctx = self.engine.no_sync() if micro < self.accum - 1 else contextlib.nullcontext()
             with ctx:
-                _, loss = self.fwd(x, y, return_logits=False)
-                loss.backward()
+                with autocast_ctx(self.device, self.autocast_dtype):
+                    _, loss = self.fwd(x, y, return_logits=False)
+                self.scaler.scale_loss(loss).backward()
             total += loss.detach().float()
         scale = self.engine.finish_grad_sync()
         if self.pg.sequence_parallel:
@@ -188,6 +195,17 @@ class Trainer:
             # gradient of the global mean
             sync_replicated_grads(self.opt, self.pg)
             scale /= self.pg.tp
+        if self.scaler.enabled:
+            # GradScaler.step/update: an inf/nan gradient skips the optimizer step and backs the
+            # scale off; otherwise the unscale rides on the AdamW kernel's grad_scale
+            used = self.scaler.scale  # the scale this step's backward ran with
+            inf = self.scaler.found_inf(self.opt)
+            self.scaler.update(inf)
+            if inf:
+                self.opt.zero_grad()
+                self.step += 1
+                return total / self.accum
+            scale /= used
         self.opt.step(grad_scale=scale / self.accum)
         self.opt.zero_grad()
         self.step += 1
@@ -216,7 +234,8 @@ class Trainer:
         acc = torch.zeros((), device=self.device, dtype=torch.float32)
         for _ in range(iters):
             x, y = self.val_loader.next()
-            _, loss = self.fwd(x, y, return_logits=False)
+            with autocast_ctx(self.device, self.autocast_dtype):
+                _, loss = self.fwd(x, y, return_logits=False)
             acc += loss.float()
         self.model.train()
         return float(all_reduce_mean(acc / iters))
@@ -326,10 +345,15 @@ class Trainer:
         osd = self.opt.state_dict() if getattr(self.opt, "collective_state", False) else None
         if self.di.is_master:
             save_checkpoint(path, self.model, self.opt if osd is None else None, step=self.step, config=self.cfg,
-                            data_state=data_state, optimizer_state=osd, params=self.opt.params)
+                            data_state=data_state, optimizer_state=osd, params=self.opt.params,
+                            extra=self._scaler_extra())
             self.log(f"saved checkpoint to {path} (step {self.step})")
         if dist.is_initialized():
             dist.barrier()
+
+    def _scaler_extra(self) -> dict:
+        # reference key name for a GradScaler's state; only written when loss scaling is on
+        return {"scaler_state_dict": self.scaler.state_dict()} if self.scaler.enabled else {}
 
     def _save_tp(self, path: str, data_state: dict):
         """Tensor parallelism: each TP rank of replica (dp 0, cp 0) writes its shard with its optimizer
@@ -342,7 +366,7 @@ class Trainer:
         if writer:
             save_checkpoint(f"{path}.tp{pg.tp_rank}", self.model, optimizer_state=osd, params=self.opt.params,
                             step=self.step, config=self.cfg, data_state=data_state,
-                            extra={"tp_rank": pg.tp_rank, "tp_size": pg.tp})
+                            extra={"tp_rank": pg.tp_rank, "tp_size": pg.tp, **self._scaler_extra()})
             masters = None
             if not getattr(self.opt, "collective_state", False):
                 masters = {id(p): self.opt.master[self.opt.offsets[i]:self.opt.offsets[i] + p.numel()].view(p.shape)
@@ -373,6 +397,8 @@ class Trainer:
         if "optimizer_state_dict" in ck:
             self.opt.load_state_dict(ck["optimizer_state_dict"])
         self.step = int(ck.get("step", 0))
+        if "scaler_state_dict" in ck:
+            self.scaler.load_state_dict(ck["scaler_state_dict"])
         ds = ck.get("data_state", {})
         seed = int(self.cfg.get("seed", 1337))
         self.train_loader.close()
