@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="gpt2", choices=["gpt2", "llama"])
+    ap.add_argument("--variants", default="32,8", help="wgrad_set_mfma values to compare (32: two-stage, 8: phased)")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
@@ -50,17 +51,18 @@ def main():
         rel = ((r.float() - ref).norm() / ref.norm()).item()
         flops = 2.0 * M * P * Q
         res = {"P": P, "Q": Q, "M": M, "rel_err": rel}
-        for mf in (32, 1056):  # split-K slices summed by the separate reduce pass (default) / (+1024) in-kernel
+        variants = [int(v) for v in args.variants.split(",")]
+        for mf in variants:
             torch.ops.pllm.wgrad_set_mfma(mf)
             r = torch.ops.pllm.wgrad(dy[:4096], x[:4096])
             res[f"rel_err{mf}"] = ((r.float() - ref).norm() / ref.norm()).item()
         for _ in range(args.rounds):
-            for mf in (32, 1056):
+            for mf in variants:
                 torch.ops.pllm.wgrad_set_mfma(mf)
                 res.setdefault(f"hip{mf}_us", []).append(1e6 * timeit(lambda: torch.ops.pllm.wgrad(dy, x, tgt)))
             res.setdefault("blas_us", []).append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
         torch.ops.pllm.wgrad_set_mfma(32)
-        for k in ("hip32", "hip1056", "blas"):
+        for k in [f"hip{v}" for v in variants] + ["blas"]:
             res[f"{k}_tflops"] = flops / (min(res[f"{k}_us"]) * 1e-6) / 1e12
         print(json.dumps(res), flush=True)
         out.append(res)

@@ -25,6 +25,13 @@
 //    slice order by wgrad_reduce_kernel (deterministic).  Measured and dropped in round 1: a
 //    4/5-slot staging ring (4-15 % slower, profiles/r1_wgrad_ring_ab.jsonl) and an in-kernel
 //    last-arriver reduction (1.0-3.2x slower, profiles/r1_wgrad_fused_reduce_negative.jsonl).
+//    Round 2: a phased variant after the 256² 8-phase GEMM template (4 quadrant phases per K-tile,
+//    counted vmcnt(6) with 3 half-tile images in flight, raw barriers, setprio, wave stagger;
+//    16x16x32 and 32x32x16) measured 3-10 % SLOWER than this kernel on every GPT-2 / Llama shape
+//    (profiles/r2_wgrad_phased_negative_*.jsonl).  PMC (profiles/r2_pmc_wgrad_*head.md): both run
+//    the LM-head shape at the same MFMA cycles, 77 % L2 hit rate, 8.4 TB/s L2->LDS, and the
+//    wave-cycle count puts the shader clock near 1.7 GHz under this load: ~60 % MFMA-busy at the
+//    clock the chip holds.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include <type_traits>
 
