@@ -185,6 +185,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) qf[j][ks] = as_frag(raw[ks]);
   }
+  vm_wait_all();  // Q fragments ready before the tile loop (see common.h)
 
   int kv_end = a.S;
   if (a.causal) kv_end = min(a.S, q0 + BM + off);
@@ -487,6 +488,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     }
   }
 
+  vm_wait_all();  // K/V fragments and the K image ready before the query loop (see common.h)
   f32x16 dk[KH][NDB], dv[KH][NDB];
 #pragma unroll
   for (int kh = 0; kh < KH; ++kh)
@@ -525,10 +527,14 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       }
     }
     if (tid < 2 * BQ) {
-      const int q = q0 + (tid & (BQ - 1));
-      const int64_t idx = ((int64_t)b * a.H + h) * a.T + q;
-      if (q < a.T) rc = tid < BQ ? -a.lse[idx] * inv_scale : -a.delta[idx];
-      else rc = 0.f;
+      // unconditional load (clamped row) consumed only at the LDS write of the next iteration:
+      // a use here, or a load under a branch, makes hipcc wait vmcnt(0) -- for the Q/dO
+      // prefetch above too
+      // waves [0, BQ/64) load -lse rows, the next BQ/64 waves -delta: a wave-uniform (scalar)
+      // base, so no per-lane 64-bit pointer is kept live (it was spilled at D = 64)
+      const float* base = __builtin_amdgcn_readfirstlane(tid >> 6) < BQ / 64 ? a.lse : a.delta;
+      const int q = min(q0 + (tid & (BQ - 1)), a.T - 1);
+      rc = base[((int64_t)b * a.H + h) * a.T + q];
     }
   };
 
@@ -558,7 +564,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         st16(Ol + I::off(row, (col + CPR2) * 8), dor[i + 1]);
       }
     }
-    if (tid < 2 * BQ) rowc[tid] = rc;
+    if (tid < 2 * BQ) {
+      const bool live = q0 + (tid & (BQ - 1)) < a.T;
+      rowc[tid] = live ? (tid < BQ ? -rc * inv_scale : -rc) : 0.f;  // -lse/scale, -delta
+    }
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 

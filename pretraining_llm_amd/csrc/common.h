@@ -166,6 +166,13 @@ PLLM_DEV int xcd_remap(int orig, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (orig >> 3);
 }
 
+// Retire every outstanding vector-memory load (s_waitcnt vmcnt(0); gfx9 encoding: expcnt 7,
+// lgkmcnt 15).  A real S_WAITCNT the compiler's waitcnt pass understands -- unlike inline asm --
+// so registers loaded before a loop (Q fragments, K/V rows) count as ready inside it.  Without
+// it the pass merges the loop's pending prefetch with those loads and emits vmcnt(0) in front
+// of the first MFMA of EVERY iteration, which serialises the prefetch it was meant to overlap.
+PLLM_DEV void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+
 #define PLLM_CHECK_LAUNCH() (void)hipGetLastError()
 
 // Debug builds (python -m pretraining_llm_amd.build --debug): report a violated device-side
