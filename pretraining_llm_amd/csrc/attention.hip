@@ -147,9 +147,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
 
   const int nqb = (a.T + BM - 1) / BM;
+  // heaviest (last) query blocks of every head first.  A head-local order (a head's blocks
+  // adjacent inside one XCD's range, for L2 reuse of its K/V) measured 0-38 % slower
+  // (profiles/r2_attn_order_ab.txt)
   const int BH = a.B * a.H;
   const int id = blockIdx.x;
-  const int qb = nqb - 1 - id / BH;  // heaviest (last) query blocks first
+  const int qb = nqb - 1 - id / BH;
   const int bh = id % BH;
   const int b = bh / a.H, h = bh % a.H, hk = h / (a.H / a.Hkv);
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
@@ -196,14 +199,18 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   constexpr int CPR2 = CPR / 2;
   constexpr int NPAIR = (BN * CPR2 + 255) / 256;
   u32x4 kr[2 * NPAIR], vr[2 * NPAIR];
+  // K / V rows by buffer loads through a per-tile descriptor (scalar base = the tile's first
+  // row): rows past S read as zeros (range check), per-lane offsets loop-invariant
   auto gload = [&](int t) {
     const int kv0 = t * BN;
+    const auto krs = rows_rsrc(kp + (int64_t)kv0 * a.k_st, a.S - kv0, a.k_st, D);
+    const auto vrs = rows_rsrc(vp + (int64_t)kv0 * a.v_st, a.S - kv0, a.v_st, D);
 #pragma unroll
     for (int i = 0; i < 2 * NPAIR; ++i) {
-      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2, key = kv0 + row;
-      if (c < BN * CPR2 && key < a.S) {
-        kr[i] = ld16(kp + (int64_t)key * a.k_st + col * 8);
-        vr[i] = ld16(vp + (int64_t)key * a.v_st + col * 8);
+      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
+      if (c < BN * CPR2) {
+        kr[i] = buf_ld16(krs, (uint32_t)(row * (int)a.k_st + col * 8) * 2u);
+        vr[i] = buf_ld16(vrs, (uint32_t)(row * (int)a.v_st + col * 8) * 2u);
       } else {
         kr[i] = u32x4{0u, 0u, 0u, 0u};
         vr[i] = u32x4{0u, 0u, 0u, 0u};
@@ -434,9 +441,11 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   uint16_t* Ol = Ql + BQ * D;             // dO tile
   uint16_t* Sl = Ol + BQ * D;             // dS^T image [key][q]
 
+  // lowest key blocks (most query blocks under causal) of every head first; head-local order
+  // measured 14-28 % slower (profiles/r2_attn_order_ab.txt)
   const int BH = a.B * a.Hkv;
   const int id = blockIdx.x;
-  const int kb = a.kb0 + id / BH;         // key block (lowest first: most query blocks under causal)
+  const int kb = a.kb0 + id / BH;
   const int bh = id % BH;
   const int b = bh / a.Hkv, hk = bh % a.Hkv;
   const int G = a.H / a.Hkv;
@@ -513,14 +522,20 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   auto gload = [&](int it) {
     const int h = hk * G + it / per_head;
     const int q0 = (qb_start + it % per_head) * BQ;
-    const uint16_t* qp = a.q + b * a.q_sb + (int64_t)h * a.q_sh;
-    const uint16_t* dop = a.dO + b * a.do_sb + (int64_t)h * a.do_sh;
+    // Q / dO rows of head h by buffer loads through a per-tile descriptor (scalar base = row
+    // q0): rows past T read as zeros (range check), per-lane offsets loop-invariant
+    const auto qrs = rows_rsrc(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st, a.T - q0, a.q_st, D);
+    const auto ors = rows_rsrc(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st, a.T - q0, a.do_st, D);
+    // per-lane offsets recomputed per iteration (a few VALU): hoisted out of the loop they are
+    // spilled at D = 64's register pressure, and each reload's vmcnt(0) serialises the loads
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
 #pragma unroll
     for (int i = 0; i < 2 * QPAIR; ++i) {
-      const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2, q = q0 + row;
-      if (c < BQ * CPR2 && q < a.T) {
-        qr[i] = ld16(qp + (int64_t)q * a.q_st + col * 8);
-        dor[i] = ld16(dop + (int64_t)q * a.do_st + col * 8);
+      const int c = tl + NT * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
+      if (c < BQ * CPR2) {
+        qr[i] = buf_ld16(qrs, (uint32_t)(row * (int)a.q_st + col * 8) * 2u);
+        dor[i] = buf_ld16(ors, (uint32_t)(row * (int)a.do_st + col * 8) * 2u);
       } else {
         qr[i] = u32x4{0u, 0u, 0u, 0u};
         dor[i] = u32x4{0u, 0u, 0u, 0u};

@@ -607,6 +607,14 @@ void check_head_view(const Tensor& t, const char* name, int64_t D) {
   check_aligned16(t, name);
 }
 
+// the attention kernels read a head's rows through a buffer descriptor with 32-bit byte offsets
+// (common.h rows_rsrc): the last row must start below 2 GiB of that head's slice
+void check_rows_span(const Tensor& t, const char* name) {
+  const int64_t D = t.size(3), rows = t.size(1);
+  TORCH_CHECK(rows == 0 || ((rows - 1) * t.stride(1) + D) * 2 < (int64_t(1) << 31), "attention: ", name,
+              " spans >= 2 GiB within one head (sequence x row stride too large for 32-bit offsets)");
+}
+
 // fused RoPE tables: fp32 contiguous [>= S, D/2] on the device (both or neither)
 void check_rope(const std::optional<Tensor>& c, const std::optional<Tensor>& sn, int64_t S, int64_t D) {
   TORCH_CHECK(c.has_value() == sn.has_value(), "attention: rope_cos and rope_sin go together");
@@ -631,6 +639,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   TORCH_CHECK(H % Hkv == 0, "H % Hkv");
   TORCH_CHECK(!causal || S >= T, "causal attention needs S >= T");
   check_rope(rope_cos, rope_sin, S, D);
+  check_rows_span(k, "k");
+  check_rows_span(v, "v");
   Tensor o = at::empty({B, T, H, D}, q.options());
   Tensor lse = at::empty({B, H, T}, q.options().dtype(at::kFloat));
   AttnFwdArgs a{};
@@ -728,6 +738,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   // PLLM_ATTN_BWD_WS_MB (default 4096 MiB: one pass for every shipped config -- passes split the
   // causal work unevenly, 2 passes cost llama-1.3B +20 %) however long the sequence, plus one fp32 running
   // sum when more than one pass is needed
+  check_rows_span(q, "q");
+  check_rows_span(dout, "dout");
   const int64_t kbk = pllm::attn_bwd_key_block((int)D);
   const int64_t nkb = (S + kbk - 1) / kbk;
   const int64_t slab_bytes = B * T * H * D * 2;

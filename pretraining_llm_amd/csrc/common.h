@@ -173,6 +173,18 @@ PLLM_DEV int xcd_remap(int orig, int nwg) {
 // of the first MFMA of EVERY iteration, which serialises the prefetch it was meant to overlap.
 PLLM_DEV void vm_wait_all() { __builtin_amdgcn_s_waitcnt(0x0F70); }
 
+// Buffer loads over the rows [0, rows) of one (batch, head) slice of a row-strided bf16 matrix
+// (cdna_hip_programming.md T8/T20): a wave-uniform descriptor plus a 32-bit per-lane byte offset
+// replaces per-load 64-bit address arithmetic, and the hardware range check returns zeros for
+// rows >= rows (no per-load branch).  Requires (rows - 1) * stride + width < 2^31 elements.
+PLLM_DEV __amdgpu_buffer_rsrc_t rows_rsrc(const uint16_t* base, int rows, int64_t stride, int width) {
+  const int bytes = rows > 0 ? (int)(((int64_t)(rows - 1) * stride + width) * 2) : 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, bytes, 0x00020000);
+}
+PLLM_DEV u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0u, 0));
+}
+
 #define PLLM_CHECK_LAUNCH() (void)hipGetLastError()
 
 // Debug builds (python -m pretraining_llm_amd.build --debug): report a violated device-side

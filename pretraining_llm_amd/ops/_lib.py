@@ -22,7 +22,7 @@ import threading
 import torch
 
 _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SO_PATH = os.path.join(_HERE, "_C.so")
+SO_PATH = os.environ.get("PLLM_SO") or os.path.join(_HERE, "_C.so")  # PLLM_SO: A/B builds
 
 _lock = threading.Lock()
 _loaded = False
