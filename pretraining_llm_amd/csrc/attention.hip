@@ -703,8 +703,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
         acc = mfma32(A, Bf, acc);
       }
-      const int64_t slab = (int64_t)a.B * a.T * a.H * D;
-      uint16_t* dq = a.dq_acc + (kb - a.kb0) * slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
+      uint16_t* dq = a.dq_acc + (kb - a.kb0) * a.slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int q = qt0 + acc_row(i, hh);
@@ -750,14 +749,309 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   }
 }
 
+// ---------------------------------------------------------------------------
+// Role-split backward ("RS"): one workgroup = 8 waves = 128 keys of one (batch, kv-head) as 4
+// key groups of 32, each group served by a PAIR of waves on one SIMD (w and w + 4):
+//   wave A (w < 4): S = Q K^T -> P (the keys' K rows in registers), dV^T += dO^T P;
+//   wave B (w >= 4): dP = dO V^T (V rows in registers), dS = P (dP - delta) with P handed over
+//   through LDS in the accumulator's own layout (element-wise, fp32), dK^T += Q^T dS, dS^T image.
+// Each wave keeps ONE operand matrix and ONE gradient accumulator (half the registers of the
+// fused-role kernel: two waves per SIMD at D = 128 instead of one, no AGPR shuffling), the two
+// waves of a SIMD overlap one's exp / pack VALU with the other's MFMAs, and the MFMA work per
+// wave is balanced (S + dV vs dP + dK).  dQ as before: per-key-block bf16 slabs, one task per wave.
+template <int D>
+struct RsCfg {
+  static constexpr int NW = 8, NT = 512, NG = 4;  // waves, threads, key groups (wave pairs)
+  static constexpr int BK = 32 * NG;               // 128 keys per workgroup
+  static constexpr int BQ = 64, NQB = BQ / 32;     // 64 queries per iteration, 2 sub-blocks
+  static constexpr int CPR = D / 8;
+  static constexpr int PX = 2 * NG * 16 * 64;      // P hand-off: [sub-block][group][q4][lane] f32x4
+  static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;  // bf16: K, Q, dO, dS^T images
+};
+
+template <int D, bool ROPE>
+__global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
+  using C = RsCfg<D>;
+  using I = Img<D>;
+  using IS = Img<C::BQ>;
+  constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
+  constexpr int NKS = D / 16, NDB = D / 32;
+  __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
+  __shared__ __attribute__((aligned(16))) float px[C::PX];
+  __shared__ __attribute__((aligned(16))) float rowc[2 * BQ];  // -lse/scale, -delta
+  uint16_t* Kl = smem;
+  uint16_t* Ql = smem + BK * D;
+  uint16_t* Ol = Ql + BQ * D;
+  uint16_t* Sl = Ol + BQ * D;
+
+  const int BH = a.B * a.Hkv;
+  const int id = blockIdx.x;
+  const int kb = a.kb0 + id / BH;
+  const int bh = id % BH;
+  const int b = bh / a.Hkv, hk = bh % a.Hkv;
+  const int G = a.H / a.Hkv;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const bool roleA = w < C::NG;  // wave-uniform
+  const int grp = w & (C::NG - 1);
+  const int k0 = kb * BK;
+  const int kw0 = k0 + grp * 32;
+  const int off = a.S - a.T;
+  const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
+  const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
+
+  // this lane's key row of K (wave A, rotated with RoPE) or V (wave B) as B-operand fragments
+  bf16x8 kvf[NKS];
+  {
+    const int key = kw0 + r;
+    u32x4 raw[NKS];
+    const uint16_t* src = roleA ? kp + (int64_t)key * a.k_st : vp + (int64_t)key * a.v_st;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) raw[ks] = key < a.S ? ld16(src + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
+    if (ROPE && roleA && key < a.S) {
+      const int64_t tab = (int64_t)key * (D / 2);
+#pragma unroll
+      for (int ks = 0; ks < NKS / 2; ++ks)
+        rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
+              1.f);
+    }
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) kvf[ks] = as_frag(raw[ks]);
+  }
+  // whole (rotated) K block into LDS for the dQ product
+  constexpr int CPR2 = CPR / 2;
+#pragma unroll
+  for (int i = 0; i < (BK * CPR2 + NT - 1) / NT; ++i) {
+    const int c = tid + NT * i, row = c / CPR2, col = c % CPR2, kk = k0 + row;
+    if (c < BK * CPR2) {
+      u32x4 lo = u32x4{0u, 0u, 0u, 0u}, hi = lo;
+      if (kk < a.S) {
+        lo = ld16(kp + (int64_t)kk * a.k_st + col * 8);
+        hi = ld16(kp + (int64_t)kk * a.k_st + (col + CPR2) * 8);
+        if (ROPE) {
+          const int64_t tab = (int64_t)kk * (D / 2) + col * 8;
+          rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
+        }
+      }
+      st16(Kl + I::off(row, col * 8), lo);
+      st16(Kl + I::off(row, (col + CPR2) * 8), hi);
+    }
+  }
+  vm_wait_all();
+
+  f32x16 acc[NDB];  // dV^T (wave A) or dK^T (wave B) of the group's 32 keys
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) acc[db] = zero16();
+  const float inv_scale = 1.f / a.scale, c2 = a.scale_log2;
+  const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  const int nqb = (a.T + BQ - 1) / BQ;
+  int qb_start = 0;
+  if (a.causal) qb_start = max(0, k0 - off) / BQ;
+  const int per_head = nqb - qb_start;
+  const int total = per_head * G;
+
+  constexpr int QPAIR = (BQ * CPR2 + NT - 1) / NT;
+  u32x4 qr[2 * QPAIR], dor[2 * QPAIR];
+  float rc = 0.f;
+  auto gload = [&](int it) {
+    const int h = hk * G + it / per_head;
+    const int q0 = (qb_start + it % per_head) * BQ;
+    const auto qrs = rows_rsrc(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st, a.T - q0, a.q_st, D);
+    const auto ors = rows_rsrc(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st, a.T - q0, a.do_st, D);
+    int tl = tid;
+    asm volatile("" : "+v"(tl));
+#pragma unroll
+    for (int i = 0; i < 2 * QPAIR; ++i) {
+      const int c = tl + NT * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
+      if (c < BQ * CPR2) {
+        qr[i] = buf_ld16(qrs, (uint32_t)(row * (int)a.q_st + col * 8) * 2u);
+        dor[i] = buf_ld16(ors, (uint32_t)(row * (int)a.do_st + col * 8) * 2u);
+      } else {
+        qr[i] = u32x4{0u, 0u, 0u, 0u};
+        dor[i] = u32x4{0u, 0u, 0u, 0u};
+      }
+    }
+    if (tid < 2 * BQ) {
+      const float* base = __builtin_amdgcn_readfirstlane(tid >> 6) < BQ / 64 ? a.lse : a.delta;
+      const int q = min(q0 + (tid & (BQ - 1)), a.T - 1);
+      rc = base[((int64_t)b * a.H + h) * a.T + q];
+    }
+  };
+
+  constexpr int NTASK = NQB * NDB;
+  if (total > 0) gload(0);
+  for (int it = 0; it < total; ++it) {
+    const int h = hk * G + it / per_head;
+    const int q0 = (qb_start + it % per_head) * BQ;
+    __syncthreads();  // previous iteration's readers of Q / dO / dS^T are done
+#pragma unroll
+    for (int i = 0; i < 2 * QPAIR; i += 2) {
+      const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
+      if (c < BQ * CPR2) {
+        if (ROPE && q0 + row < a.T) {
+          const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
+          rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
+        }
+        st16(Ql + I::off(row, col * 8), qr[i]);
+        st16(Ql + I::off(row, (col + CPR2) * 8), qr[i + 1]);
+        st16(Ol + I::off(row, col * 8), dor[i]);
+        st16(Ol + I::off(row, (col + CPR2) * 8), dor[i + 1]);
+      }
+    }
+    if (tid < 2 * BQ) {
+      const bool live = q0 + (tid & (BQ - 1)) < a.T;
+      rowc[tid] = live ? (tid < BQ ? -rc * inv_scale : -rc) : 0.f;
+    }
+    __syncthreads();
+    if (it + 1 < total) gload(it + 1);
+
+    const bool need_mask = (q0 + BQ > a.T) || (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
+#pragma unroll
+    for (int j = 0; j < NQB; ++j) {
+      const int qj0 = q0 + 32 * j;
+      // causal: the group's keys all after every query of the sub-block -> P = dS = 0
+      const bool live = !a.causal || kw0 <= qj0 + 31 + off;
+      f32x16 x;
+      bf16x8 f0, f1;
+      float* pxj = px + (j * C::NG + grp) * 16 * 64;  // [q4][lane] f32x4 of this group
+      if (live) {
+        // S' = Q K^T - lse/scale (wave A) or dP' = dO V^T - delta (wave B), key on the lane
+        const int rbase = roleA ? 0 : BQ;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[rbase + 32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) x[4 * g + e] = rs[e];
+        }
+        const uint16_t* Al = roleA ? Ql : Ol;
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) x = mfma32(as_frag(ld16(Al + I::off(32 * j + r, 16 * ks + 8 * hh))), kvf[ks], x);
+        if (roleA) {
+          const int key = kw0 + r;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float p = fast_exp2(c2 * x[i]);
+            if (need_mask) {
+              const int q = qj0 + acc_row(i, hh);
+              if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+            }
+            x[i] = p;
+          }
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4)
+            *reinterpret_cast<f32x4*>(pxj + (q4 * 64 + lane) * 4) =
+                f32x4{x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]};
+          f0 = pack_frag(x, 0);
+          f1 = pack_frag(x, 1);
+        }
+      } else if (!roleA) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<u32x2*>(Sl + IS::off(grp * 32 + r, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
+      }
+      __syncthreads();  // P of sub-block j handed over
+      if (live) {
+        if (!roleA) {
+          // dS = P * dP' (unscaled); P read back in the same accumulator layout
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            const f32x4 p4 = *reinterpret_cast<const f32x4*>(pxj + (q4 * 64 + lane) * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[4 * q4 + e] *= p4[e];
+          }
+          f0 = pack_frag(x, 0);
+          f1 = pack_frag(x, 1);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            u32x2 v2;
+            v2[0] = pack_bf16x2(x[4 * g], x[4 * g + 1]);
+            v2[1] = pack_bf16x2(x[4 * g + 2], x[4 * g + 3]);
+            *reinterpret_cast<u32x2*>(Sl + IS::off(grp * 32 + r, 32 * j + 8 * g + 4 * hh)) = v2;
+          }
+        }
+        // dV^T += dO^T P (A) / dK^T += Q^T dS (B): A operands by transposed reads
+        const uint16_t* Tl = roleA ? Ol : Ql;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
+            const bf16x8 tA = cat_tr(ds_tr(Tl + I::off(rowq, col)), ds_tr(Tl + I::off(rowq + 8, col)));
+            acc[db] = mfma32(tA, st == 0 ? f0 : f1, acc[db]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // dQ partial of this key block: one (query sub-block, d-block) task per wave
+    for (int task = w; task < NTASK; task += C::NW) {
+      const int tq_blk = task / NDB, tdb = task % NDB;
+      const int qt0 = q0 + 32 * tq_blk;
+      int ks_end = BK / 16;
+      if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
+      // dQ^T tile = K^T dS^T: the accumulator has the QUERY on the lane and 16 head-dim values
+      // per lane, dumped as one contiguous 2-KiB fragment-order block (two 16-B stores per lane,
+      // coalesced) that attn_dq_reduce_frag_kernel reads back by (query, head-dim) position
+      f32x16 dqa = zero16();
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        if (ks >= ks_end) break;
+        const int kr0 = ks * 16 + 8 * hh + tq;
+        const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
+        const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
+        const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
+        dqa = mfma32(Bf, A, dqa);
+      }
+      uint16_t* blk = a.dq_acc + (kb - a.kb0) * a.slab +
+                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
+      float lo[8], hi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        lo[e] = dqa[e];
+        hi[e] = dqa[8 + e];
+      }
+      st16(blk, pack8(lo));
+      st16(blk + 8, pack8(hi));
+    }
+  }
+  // dV (wave A) / dK scaled and rotated back (wave B) for this lane's key
+  const int key = kw0 + r;
+  if (key >= a.S) return;
+  if (!roleA && ROPE) {
+    const float* cr = a.rope_cos + (int64_t)key * (D / 2);
+    const float* sr = a.rope_sin + (int64_t)key * (D / 2);
+#pragma unroll
+    for (int db = 0; db < NDB / 2; ++db)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int d = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+        const float c = cr[d], sn = sr[d];
+        const float x0 = acc[db][i], y0 = acc[db + NDB / 2][i];
+        acc[db][i] = x0 * c + y0 * sn;
+        acc[db + NDB / 2][i] = y0 * c - x0 * sn;
+      }
+  }
+  const float sc = roleA ? 1.f : a.scale;
+  uint16_t* dst = roleA ? a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh
+                        : a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh;
+#pragma unroll
+  for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      u32x2 v2;
+      v2[0] = pack_bf16x2(acc[db][4 * g] * sc, acc[db][4 * g + 1] * sc);
+      v2[1] = pack_bf16x2(acc[db][4 * g + 2] * sc, acc[db][4 * g + 3] * sc);
+      *reinterpret_cast<u32x2*>(dst + db * 32 + 8 * g + 4 * hh) = v2;
+    }
+  }
+}
+
 // Sum this pass's fp32 dQ slabs [nkb_pass][B,T,H,D] in key-block order (deterministic); under
 // the causal mask row t only reads blocks kb <= (t+off)/BK (the others were never written for
 // it).  Not the last pass: the sum goes on into the fp32 running sum ``dq_sum``; the last pass
 // adds the running sum (if any) and writes dq (bf16, strided) = scale * total.
-template <int D, int V, bool ROPE>
+template <int D, int BK, bool ROPE>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   constexpr int CPR = D / 8;
-  constexpr int BK = BwdCfg<D, V>::BK;
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t row = gid / CPR;
   const int c = (int)(gid % CPR);
@@ -770,7 +1064,6 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   const int nkb = (a.S + BK - 1) / BK;
   int kmax = min(nkb - 1, a.kb0 + a.nkb_pass - 1);
   if (a.causal) kmax = min(kmax, (t + a.S - a.T) / BK);
-  const int64_t slab = nrows * D;
   float f[8];
   if (a.kb0 > 0) {
     const f32x4* p = reinterpret_cast<const f32x4*>(a.dq_sum + row * D + c * 8);
@@ -787,7 +1080,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   const uint16_t* src = a.dq_acc + row * D + c * 8;
   for (int kb = a.kb0; kb <= kmax; ++kb) {
     float x[8];
-    unpack8(ld16(src + (kb - a.kb0) * slab), x);
+    unpack8(ld16(src + (kb - a.kb0) * a.slab), x);
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] += x[j];
   }
@@ -815,20 +1108,120 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   st16(a.dq + b * a.dq_sb + (int64_t)t * a.dq_st + (int64_t)h * a.dq_sh + c * 8, pack8(f));
 }
 
+
+// Reduce of the role-split kernel's fragment-order slabs: a thread owns 8 head-dim values of one
+// query in d-block tdb < D/64 AND their RoPE partners (the same positions of block tdb + D/64),
+// i.e. 16 contiguous bytes of each of the two blocks per slab (1-KiB coalesced wave reads); lane
+// l of a block holds query l%32, head dims acc_row(i, l/32) at elements i.  Sums the pass's slabs
+// in key-block order (deterministic) into the fp32 running sum (kept in the same fragment order)
+// or, on the last pass, writes dq = scale * total, rotated back with RoPE.
+template <int D, int BK, bool ROPE>
+__global__ __launch_bounds__(256) void attn_dq_reduce_frag_kernel(AttnBwdArgs a) {
+  constexpr int NDB = D / 32, ND2 = NDB / 2;
+  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int half = (int)(gid & 1), lane = (int)((gid >> 1) & 63);
+  const int64_t rest = gid >> 7;  // (b, h, qt, tdb2)
+  const int tdb2 = (int)(rest % ND2);
+  const int64_t bhq = rest / ND2;
+  const int qt = (int)(bhq % a.nqt);
+  const int64_t bh = bhq / a.nqt;
+  if (bh >= (int64_t)a.B * a.H) return;
+  const int h = (int)(bh % a.H), b = (int)(bh / a.H);
+  const int q = qt * 32 + (lane & 31), hh = lane >> 5;
+  if (q >= a.T) return;
+  const int nkb = (a.S + BK - 1) / BK;
+  int kmax = min(nkb - 1, a.kb0 + a.nkb_pass - 1);
+  if (a.causal) kmax = min(kmax, (q + a.S - a.T) / BK);
+  const int64_t blk0 = (bhq * NDB + tdb2) * 1024 + lane * 16 + 8 * half;  // element of the first block
+  const int64_t blk1 = blk0 + (int64_t)ND2 * 1024;                      // its RoPE partner block
+  float f[8], g[8];
+  if (a.kb0 > 0) {
+    float* s0 = a.dq_sum + blk0;
+    float* s1 = a.dq_sum + blk1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] = s0[e];
+      g[e] = s1[e];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = g[e] = 0.f;
+  }
+  for (int kb = a.kb0; kb <= kmax; ++kb) {
+    float x[8], y[8];
+    unpack8(ld16(a.dq_acc + (kb - a.kb0) * a.slab + blk0), x);
+    unpack8(ld16(a.dq_acc + (kb - a.kb0) * a.slab + blk1), y);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      f[e] += x[e];
+      g[e] += y[e];
+    }
+  }
+  if (a.kb0 + a.nkb_pass < nkb) {  // more passes follow: running sum in fragment order
+    float* s0 = a.dq_sum + blk0;
+    float* s1 = a.dq_sum + blk1;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      s0[e] = f[e];
+      s1[e] = g[e];
+    }
+    return;
+  }
+  // element e = 8*half + e' holds head dim tdb2*32 + acc_row(8*half + e', hh): two runs of 4
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    f[e] *= a.scale;
+    g[e] *= a.scale;
+  }
+  uint16_t* dq = a.dq + b * a.dq_sb + (int64_t)q * a.dq_st + (int64_t)h * a.dq_sh;
+#pragma unroll
+  for (int run = 0; run < 2; ++run) {
+    const int d = tdb2 * 32 + acc_row(8 * half + 4 * run, hh);  // first of 4 consecutive dims
+    float lo[4], hi[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      lo[e] = f[4 * run + e];
+      hi[e] = g[4 * run + e];
+    }
+    if (ROPE) {  // R^T: (x, y) at dims (d, d + D/2) -> (x c + y s, y c - x s)
+      const int64_t tab = (int64_t)(q + a.S - a.T) * (D / 2) + d;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float cs = a.rope_cos[tab + e], sn = a.rope_sin[tab + e];
+        const float x0 = lo[e], y0 = hi[e];
+        lo[e] = x0 * cs + y0 * sn;
+        hi[e] = y0 * cs - x0 * sn;
+      }
+    }
+    u32x2 v0, v1;
+    v0[0] = pack_bf16x2(lo[0], lo[1]);
+    v0[1] = pack_bf16x2(lo[2], lo[3]);
+    v1[0] = pack_bf16x2(hi[0], hi[1]);
+    v1[1] = pack_bf16x2(hi[2], hi[3]);
+    *reinterpret_cast<u32x2*>(dq + d) = v0;
+    *reinterpret_cast<u32x2*>(dq + d + D / 2) = v1;
+  }
+}
+
 }  // namespace
 
 namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-// backward tiling variants (BwdCfg): bit 0 = variant for D <= 64 (0 / 1), bit 2 = for D = 128
-// (0 -> V 1, 1 -> V 2)
+// backward variants: bit 0 = BwdCfg variant for D <= 64 (0 / 1), bit 2 = fused-role variant for
+// D = 128 (0 -> V 1, 1 -> V 2) when bit 3 is set, bit 3 = D = 128 runs the fused-role kernel instead
+// of the role-split one, bit 4 = D <= 64 runs the role-split kernel
 static int g_bwd_variant = 0;
-void attn_bwd_set_variant(int v) { g_bwd_variant = v & 5; }
+void attn_bwd_set_variant(int v) { g_bwd_variant = v & 29; }
+// role-split kernel: the default at D = 128 (bit 3 selects the fused-role V 1 / V 2 instead),
+// opt-in at D <= 64 (bit 4)
+static bool vrs(int D) { return D == 128 ? !((g_bwd_variant >> 3) & 1) : (D == 64 && ((g_bwd_variant >> 4) & 1)); }
 static int v64() { return g_bwd_variant & 1; }
 static int v128() { return 1 + ((g_bwd_variant >> 2) & 1); }
 
 int attn_bwd_key_block(int D) {
+  if (vrs(D)) return RsCfg<64>::BK;
   if (D <= 64) return v64() ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
   return BwdCfg<128, 1>::BK;  // 128 keys in every D = 128 variant
 }
@@ -853,7 +1246,7 @@ static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
     a.nkb_pass = min(per, nkb - kb0);
     hipLaunchKernelGGL((attn_bwd_kernel<D, V, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st,
                        a);
-    hipLaunchKernelGGL((attn_dq_reduce_kernel<D, V, ROPE>), dim3(pre_grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_dq_reduce_kernel<D, BwdCfg<D, V>::BK, ROPE>), dim3(pre_grid), dim3(256), 0, st, a);
     a.nkb_pass = per;
   }
 }
@@ -870,7 +1263,36 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
   else attn_fwd_t<128>(a, st);
 }
 
+template <int D, bool ROPE>
+static void attn_bwd_rs_t(AttnBwdArgs a, hipStream_t st) {
+  using C = RsCfg<D>;
+  const int64_t nrows = (int64_t)a.B * a.T * a.H;
+  const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
+  const int nkb = (a.S + C::BK - 1) / C::BK;
+  const int red_grid = (int)(((int64_t)a.B * a.H * a.nqt * (D / 64) * 128 + 255) / 256);
+  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  const int per = a.nkb_pass;
+  for (int kb0 = 0; kb0 < nkb; kb0 += per) {
+    a.kb0 = kb0;
+    a.nkb_pass = min(per, nkb - kb0);
+    hipLaunchKernelGGL((attn_bwd_rs_kernel<D, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(C::NT), 0, st, a);
+    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, C::BK, ROPE>), dim3(red_grid), dim3(256), 0, st, a);
+    a.nkb_pass = per;
+  }
+}
+
+template <int D>
+static void attn_bwd_rs_r(const AttnBwdArgs& a, hipStream_t st) {
+  if (a.rope_cos) attn_bwd_rs_t<D, true>(a, st);
+  else attn_bwd_rs_t<D, false>(a, st);
+}
+
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
+  if (vrs(a.D)) {  // D = 64 / 128 (the fragment-order reduce pairs d-blocks: D >= 64)
+    if (a.D == 64) attn_bwd_rs_r<64>(a, st);
+    else attn_bwd_rs_r<128>(a, st);
+    return;
+  }
   if (a.D == 32) v64() ? attn_bwd_r<32, 1>(a, st) : attn_bwd_r<32, 0>(a, st);
   else if (a.D == 64) v64() ? attn_bwd_r<64, 1>(a, st) : attn_bwd_r<64, 0>(a, st);
   else v128() == 1 ? attn_bwd_r<128, 1>(a, st) : attn_bwd_r<128, 2>(a, st);

@@ -742,11 +742,13 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   check_rows_span(dout, "dout");
   const int64_t kbk = pllm::attn_bwd_key_block((int)D);
   const int64_t nkb = (S + kbk - 1) / kbk;
-  const int64_t slab_bytes = B * T * H * D * 2;
+  const int64_t nqt = (T + 31) / 32;
+  const int64_t slab_elems = B * H * nqt * 32 * D;  // T rounded up to the 32-row fragment tiles
+  const int64_t slab_bytes = slab_elems * 2;
   const int64_t ws_budget = attn_bwd_ws_bytes();
   const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nkb, ws_budget / std::max<int64_t>(1, slab_bytes)));
-  Tensor dq_acc = at::empty({per, B, T, H, D}, q.options());  // bf16 partial slabs
-  Tensor dq_sum = per < nkb ? at::empty({B, T, H, D}, q.options().dtype(at::kFloat)) : Tensor();
+  Tensor dq_acc = at::empty({per, slab_elems}, q.options());  // bf16 partial slabs
+  Tensor dq_sum = per < nkb ? at::empty({slab_elems}, q.options().dtype(at::kFloat)) : Tensor();
   AttnBwdArgs a{};
   a.q = (const uint16_t*)q.data_ptr();
   a.k = (const uint16_t*)k.data_ptr();
@@ -760,6 +762,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.dq_acc = (uint16_t*)dq_acc.data_ptr();
   a.dq_sum = dq_sum.defined() ? dq_sum.data_ptr<float>() : nullptr;
   a.kb0 = 0;
+  a.slab = slab_elems;
+  a.nqt = (int)nqt;
   a.nkb_pass = (int)per;
   a.dq = (uint16_t*)dq.data_ptr();
   a.dk = (uint16_t*)dk.data_ptr();

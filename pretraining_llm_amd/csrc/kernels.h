@@ -38,6 +38,8 @@ struct AttnBwdArgs {
   uint16_t* dq_acc;  // [nkb_pass][B, T, H, D] bf16 per-key-block dQ partial slabs of one pass
   float* dq_sum;  // [B, T, H, D] fp32 running dQ sum across passes (null when one pass)
   int kb0, nkb_pass;  // first key block of the pass / key blocks per pass (set by the host)
+  int64_t slab;       // elements per dQ slab (>= B * ceil32(T) * H * D)
+  int nqt;            // ceil(T / 32): query tiles per head in the fragment-order slab (RS kernel)
   uint16_t *dq, *dk, *dv;
   int B, H, Hkv, T, S, D;
   int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh, do_sb, do_st, do_sh;

@@ -816,8 +816,9 @@ def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
 
 
 def _bwd_variants(D):
-    # attn_bwd_set_variant encoding: bit 0 = D <= 64 variant, bit 2 = D = 128 variant
-    return [0, 1] if D <= 64 else [0, 4]
+    # attn_bwd_set_variant encoding (csrc/attention.hip): D <= 64: 0 = V 0, 1 = V 1, 16 = role split;
+    # D = 128: 0 = role split, 8 = fused-role V 1, 12 = fused-role V 2
+    return [0, 1, 16] if D <= 64 else [0, 8, 12]
 
 
 @pytest.mark.parametrize("D,T,H,Hkv,B", [(32, 1024, 4, 4, 2), (64, 2048, 4, 2, 1), (64, 4096, 2, 2, 1),
@@ -857,9 +858,19 @@ def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
 
 
 @pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1)])
-def test_attention_fused_rope_fwd_bwd(D, Hkv):
+@pytest.mark.parametrize("variant", [0, 8, 16])
+def test_attention_fused_rope_fwd_bwd(D, Hkv, variant):
     """RoPE applied inside the attention kernels (q/k rotated while staged, dq/dk rotated back)
-    == rotate-half RoPE + attention in fp32 torch, gradients w.r.t. the UNROTATED packed qkv."""
+    == rotate-half RoPE + attention in fp32 torch, gradients w.r.t. the UNROTATED packed qkv
+    (default and role-split backward)."""
+    torch.ops.pllm.attn_bwd_set_variant(variant)
+    try:
+        _rope_case(D, Hkv)
+    finally:
+        torch.ops.pllm.attn_bwd_set_variant(0)
+
+
+def _rope_case(D, Hkv):
     from pretraining_llm_amd import ops
     from pretraining_llm_amd.ops import reference as ref
     torch.manual_seed(29 + D)
