@@ -763,7 +763,8 @@ template <int D>
 struct RsCfg {
   static constexpr int NW = 8, NT = 512, NG = 4;  // waves, threads, key groups (wave pairs)
   static constexpr int BK = 32 * NG;               // 128 keys per workgroup
-  static constexpr int BQ = 64, NQB = BQ / 32;     // 64 queries per iteration, 2 sub-blocks
+  static constexpr int BQ = D <= 64 ? 128 : 64;    // queries per iteration (LDS: 112 KiB both)
+  static constexpr int NQB = BQ / 32;              // 32-query sub-blocks
   static constexpr int CPR = D / 8;
   static constexpr int PX = 2 * NG * 16 * 64;      // P hand-off: [sub-block][group][q4][lane] f32x4
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;  // bf16: K, Q, dO, dS^T images
@@ -912,7 +913,9 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       const bool live = !a.causal || kw0 <= qj0 + 31 + off;
       f32x16 x;
       bf16x8 f0, f1;
-      float* pxj = px + (j * C::NG + grp) * 16 * 64;  // [q4][lane] f32x4 of this group
+      // [q4][lane] f32x4 of this group; buffers alternate by sub-block parity (wave B's reads of
+      // sub-block j finish before it reaches barrier j + 1, after which A rewrites the buffer)
+      float* pxj = px + ((j & 1) * C::NG + grp) * 16 * 64;
       if (live) {
         // S' = Q K^T - lse/scale (wave A) or dP' = dO V^T - delta (wave B), key on the lane
         const int rbase = roleA ? 0 : BQ;
