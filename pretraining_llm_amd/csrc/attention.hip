@@ -1112,97 +1112,81 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
 }
 
 
-// Reduce of the role-split kernel's fragment-order slabs: a thread owns 8 head-dim values of one
-// query in d-block tdb < D/64 AND their RoPE partners (the same positions of block tdb + D/64),
-// i.e. 16 contiguous bytes of each of the two blocks per slab (1-KiB coalesced wave reads); lane
-// l of a block holds query l%32, head dims acc_row(i, l/32) at elements i.  Sums the pass's slabs
-// in key-block order (deterministic) into the fp32 running sum (kept in the same fragment order)
-// or, on the last pass, writes dq = scale * total, rotated back with RoPE.
+// Reduce of the role-split kernel's fragment-order slabs.  One workgroup (64 x D/32 threads) per
+// 32-query tile of one (batch, head): thread (d-block blk, lane l) reads its 32 contiguous bytes of
+// the tile's block blk from every slab of the pass (coalesced 2-KiB wave reads; lane l holds query
+// l%32 and head dims blk*32 + acc_row(i, l/32), i < 16), sums them in key-block order
+// (deterministic) into the fp32 running sum (kept in the same fragment order) or, on the last
+// pass, transposes the tile through LDS and writes dq = scale * total as whole 16-B row chunks,
+// rotated back with RoPE (each thread holds a dim chunk and its d + D/2 partner).
 template <int D, int BK, bool ROPE>
 __global__ __launch_bounds__(256) void attn_dq_reduce_frag_kernel(AttnBwdArgs a) {
-  constexpr int NDB = D / 32, ND2 = NDB / 2;
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int half = (int)(gid & 1), lane = (int)((gid >> 1) & 63);
-  const int64_t rest = gid >> 7;  // (b, h, qt, tdb2)
-  const int tdb2 = (int)(rest % ND2);
-  const int64_t bhq = rest / ND2;
+  constexpr int NDB = D / 32, NTH = 64 * NDB, LD = D + 4;  // LD: padded fp32 row of the LDS tile
+  __shared__ float tile[32 * LD];
+  const int tid = threadIdx.x, blk = tid >> 6, lane = tid & 63, hh = lane >> 5;
+  const int64_t bhq = blockIdx.x;  // (b * H + h) * nqt + qt
   const int qt = (int)(bhq % a.nqt);
   const int64_t bh = bhq / a.nqt;
-  if (bh >= (int64_t)a.B * a.H) return;
   const int h = (int)(bh % a.H), b = (int)(bh / a.H);
-  const int q = qt * 32 + (lane & 31), hh = lane >> 5;
-  if (q >= a.T) return;
+  const int q = qt * 32 + (lane & 31);
   const int nkb = (a.S + BK - 1) / BK;
   int kmax = min(nkb - 1, a.kb0 + a.nkb_pass - 1);
-  if (a.causal) kmax = min(kmax, (q + a.S - a.T) / BK);
-  const int64_t blk0 = (bhq * NDB + tdb2) * 1024 + lane * 16 + 8 * half;  // element of the first block
-  const int64_t blk1 = blk0 + (int64_t)ND2 * 1024;                      // its RoPE partner block
-  float f[8], g[8];
+  if (a.causal) kmax = min(kmax, (min(q, a.T - 1) + a.S - a.T) / BK);
+  const int64_t e0 = (bhq * NDB + blk) * 1024 + lane * 16;
+  float f[16];
   if (a.kb0 > 0) {
-    float* s0 = a.dq_sum + blk0;
-    float* s1 = a.dq_sum + blk1;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      f[e] = s0[e];
-      g[e] = s1[e];
-    }
+    for (int i = 0; i < 16; ++i) f[i] = a.dq_sum[e0 + i];
   } else {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) f[e] = g[e] = 0.f;
+    for (int i = 0; i < 16; ++i) f[i] = 0.f;
   }
   for (int kb = a.kb0; kb <= kmax; ++kb) {
+    const uint16_t* p = a.dq_acc + (kb - a.kb0) * a.slab + e0;
     float x[8], y[8];
-    unpack8(ld16(a.dq_acc + (kb - a.kb0) * a.slab + blk0), x);
-    unpack8(ld16(a.dq_acc + (kb - a.kb0) * a.slab + blk1), y);
+    unpack8(ld16(p), x);
+    unpack8(ld16(p + 8), y);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      f[e] += x[e];
-      g[e] += y[e];
+    for (int i = 0; i < 8; ++i) {
+      f[i] += x[i];
+      f[8 + i] += y[i];
     }
   }
   if (a.kb0 + a.nkb_pass < nkb) {  // more passes follow: running sum in fragment order
-    float* s0 = a.dq_sum + blk0;
-    float* s1 = a.dq_sum + blk1;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      s0[e] = f[e];
-      s1[e] = g[e];
-    }
+    for (int i = 0; i < 16; ++i) a.dq_sum[e0 + i] = f[i];
     return;
   }
-  // element e = 8*half + e' holds head dim tdb2*32 + acc_row(8*half + e', hh): two runs of 4
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    f[e] *= a.scale;
-    g[e] *= a.scale;
-  }
-  uint16_t* dq = a.dq + b * a.dq_sb + (int64_t)q * a.dq_st + (int64_t)h * a.dq_sh;
+  for (int i = 0; i < 16; ++i) tile[(lane & 31) * LD + blk * 32 + acc_row(i, hh)] = f[i] * a.scale;
+  __syncthreads();
+  // write-out: 32 rows x D/16 chunk pairs (chunk c and its RoPE partner c + D/16), 8 dims each
+  constexpr int CP = D / 16;
+  for (int it = tid; it < 32 * CP; it += NTH) {
+    const int row = it / CP, c = it % CP, qq = qt * 32 + row;
+    if (qq >= a.T) continue;
+    float lo[8], hi[8];
 #pragma unroll
-  for (int run = 0; run < 2; ++run) {
-    const int d = tdb2 * 32 + acc_row(8 * half + 4 * run, hh);  // first of 4 consecutive dims
-    float lo[4], hi[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      lo[e] = f[4 * run + e];
-      hi[e] = g[4 * run + e];
+    for (int e = 0; e < 8; ++e) {
+      lo[e] = tile[row * LD + 8 * c + e];
+      hi[e] = tile[row * LD + D / 2 + 8 * c + e];
     }
     if (ROPE) {  // R^T: (x, y) at dims (d, d + D/2) -> (x c + y s, y c - x s)
-      const int64_t tab = (int64_t)(q + a.S - a.T) * (D / 2) + d;
+      const int64_t tab = (int64_t)(qq + a.S - a.T) * (D / 2) + 8 * c;
+      const f32x4* cp = reinterpret_cast<const f32x4*>(a.rope_cos + tab);
+      const f32x4* sp = reinterpret_cast<const f32x4*>(a.rope_sin + tab);
+      const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float cs = a.rope_cos[tab + e], sn = a.rope_sin[tab + e];
+      for (int e = 0; e < 8; ++e) {
+        const float cs = e < 4 ? c0[e & 3] : c1[e & 3], sn = e < 4 ? s0[e & 3] : s1[e & 3];
         const float x0 = lo[e], y0 = hi[e];
         lo[e] = x0 * cs + y0 * sn;
         hi[e] = y0 * cs - x0 * sn;
       }
     }
-    u32x2 v0, v1;
-    v0[0] = pack_bf16x2(lo[0], lo[1]);
-    v0[1] = pack_bf16x2(lo[2], lo[3]);
-    v1[0] = pack_bf16x2(hi[0], hi[1]);
-    v1[1] = pack_bf16x2(hi[2], hi[3]);
-    *reinterpret_cast<u32x2*>(dq + d) = v0;
-    *reinterpret_cast<u32x2*>(dq + d + D / 2) = v1;
+    uint16_t* dq = a.dq + b * a.dq_sb + (int64_t)qq * a.dq_st + (int64_t)h * a.dq_sh;
+    st16(dq + 8 * c, pack8(lo));
+    st16(dq + D / 2 + 8 * c, pack8(hi));
   }
 }
 
@@ -1272,14 +1256,14 @@ static void attn_bwd_rs_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
   const int nkb = (a.S + C::BK - 1) / C::BK;
-  const int red_grid = (int)(((int64_t)a.B * a.H * a.nqt * (D / 64) * 128 + 255) / 256);
+  const int red_grid = a.B * a.H * a.nqt;  // one workgroup per 32-query tile
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {
     a.kb0 = kb0;
     a.nkb_pass = min(per, nkb - kb0);
     hipLaunchKernelGGL((attn_bwd_rs_kernel<D, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(C::NT), 0, st, a);
-    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, C::BK, ROPE>), dim3(red_grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, C::BK, ROPE>), dim3(red_grid), dim3(64 * (D / 32)), 0, st, a);
     a.nkb_pass = per;
   }
 }
