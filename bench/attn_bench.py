@@ -34,6 +34,7 @@ def main():
     ap.add_argument("--configs", default="64x12x1024x64,8x16x2048x128,8x16x4096x64")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="", help="fwd|bwd: run only our kernel (for profiling)")
+    ap.add_argument("--rope-ab", action="store_true", help="our fwd/bwd with vs without fused RoPE tables")
     ap.add_argument("--variants", default="", help="comma list of backward tiling variants to A/B (attn_bwd_set_variant)")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
@@ -51,6 +52,30 @@ def main():
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
         ours_f = lambda: torch.ops.pllm.attn_fwd(q, k, v, True, scale)
         ours_b = lambda: torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, True, scale)
+        if args.rope_ab:
+            from pretraining_llm_amd import ops
+            cos, sin = ops.rope_cache(T, D, 10000.0, dev)
+            res = {"cfg": cfg}
+            for tag, rc, rs in (("plain", None, None), ("rope", cos, sin)):
+                o_, l_ = torch.ops.pllm.attn_fwd(q, k, v, True, scale, rc, rs)
+                f_ = lambda: torch.ops.pllm.attn_fwd(q, k, v, True, scale, rc, rs)  # noqa: E731
+                b_ = lambda: torch.ops.pllm.attn_bwd(do, q, k, v, o_, l_, dq, dk, dv, True, scale, rc, rs)  # noqa: E731
+                res[f"{tag}_fwd_us"] = min(1e6 * timeit(f_) for _ in range(args.rounds))
+                res[f"{tag}_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
+            # pre-pass arm: rotate q / k of a packed qkv once (rope_qk), plain forward, backward
+            # rotating only its outputs (the training path, ops._FlashAttnPacked)
+            qkv = torch.cat([q.reshape(B, T, -1), k.reshape(B, T, -1), v.reshape(B, T, -1)], -1)
+            qk = torch.ops.pllm.rope_qk(qkv, cos, sin, 3 * H, 2 * H, T)
+            qr, kr = qk[..., : H * D].view(B, T, H, D), qk[..., H * D:].view(B, T, H, D)
+            o_, l_ = torch.ops.pllm.attn_fwd(qr, kr, v, True, scale)
+            pre = lambda: torch.ops.pllm.rope_qk(qkv, cos, sin, 3 * H, 2 * H, T)  # noqa: E731
+            f_ = lambda: torch.ops.pllm.attn_fwd(qr, kr, v, True, scale)  # noqa: E731
+            b_ = lambda: torch.ops.pllm.attn_bwd(do, qr, kr, v, o_, l_, dq, dk, dv, True, scale, cos, sin, False)  # noqa: E731
+            res["prepass_us"] = min(1e6 * timeit(pre) for _ in range(args.rounds))
+            res["prepass_fwd_us"] = min(1e6 * timeit(f_) for _ in range(args.rounds))
+            res["prepass_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
+            print(json.dumps(res), flush=True)
+            continue
         if args.variants:
             outs, res = {}, {"cfg": cfg}
             for vv in (int(x) for x in args.variants.split(",")):

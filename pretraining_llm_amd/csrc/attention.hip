@@ -427,7 +427,7 @@ struct BwdCfg {
 // bf16 dQ.  fp32 slabs (no partial rounding) measured +12 % (T 1024, D 64) to +34 % (T 4096)
 // on the whole backward: the slab bytes are its second cost after the MFMAs.
 // ROPE: q and k are rotated while staged, dk is rotated back before its store (dq in the reduce).
-template <int D, int V, bool ROPE>
+template <int D, int V, int ROPE>
 __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D, V>;
   using I = Img<D>;
@@ -467,7 +467,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       raw[ks] = key < a.S ? ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
       vf[kh][ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
     }
-    if (ROPE && key < a.S) {
+    if (ROPE == 1 && key < a.S) {
       const int64_t tab = (int64_t)key * (D / 2);
 #pragma unroll
       for (int ks = 0; ks < NKS / 2; ++ks)
@@ -487,7 +487,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       if (kk < a.S) {
         lo = ld16(kp + (int64_t)kk * a.k_st + col * 8);
         hi = ld16(kp + (int64_t)kk * a.k_st + (col + CPR2) * 8);
-        if (ROPE) {
+        if (ROPE == 1) {
           const int64_t tab = (int64_t)kk * (D / 2) + col * 8;
           rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
@@ -569,7 +569,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     for (int i = 0; i < 2 * QPAIR; i += 2) {
       const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
       if (c < BQ * CPR2) {
-        if (ROPE && q0 + row < a.T) {
+        if (ROPE == 1 && q0 + row < a.T) {
           const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
           rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
@@ -717,7 +717,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   for (int kh = 0; kh < KH; ++kh) {
     const int key = kw0 + 32 * kh + r;
     if (key >= a.S) continue;
-    if (ROPE) {
+    if (ROPE != 0) {
       const float* cr = a.rope_cos + (int64_t)key * (D / 2);
       const float* sr = a.rope_sin + (int64_t)key * (D / 2);
 #pragma unroll
@@ -770,7 +770,7 @@ struct RsCfg {
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;  // bf16: K, Q, dO, dS^T images
 };
 
-template <int D, bool ROPE>
+template <int D, int ROPE>
 __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   using C = RsCfg<D>;
   using I = Img<D>;
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     const uint16_t* src = roleA ? kp + (int64_t)key * a.k_st : vp + (int64_t)key * a.v_st;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) raw[ks] = key < a.S ? ld16(src + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
-    if (ROPE && roleA && key < a.S) {
+    if (ROPE == 1 && roleA && key < a.S) {
       const int64_t tab = (int64_t)key * (D / 2);
 #pragma unroll
       for (int ks = 0; ks < NKS / 2; ++ks)
@@ -828,7 +828,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       if (kk < a.S) {
         lo = ld16(kp + (int64_t)kk * a.k_st + col * 8);
         hi = ld16(kp + (int64_t)kk * a.k_st + (col + CPR2) * 8);
-        if (ROPE) {
+        if (ROPE == 1) {
           const int64_t tab = (int64_t)kk * (D / 2) + col * 8;
           rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     for (int i = 0; i < 2 * QPAIR; i += 2) {
       const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
       if (c < BQ * CPR2) {
-        if (ROPE && q0 + row < a.T) {
+        if (ROPE == 1 && q0 + row < a.T) {
           const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
           rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
@@ -1019,7 +1019,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   // dV (wave A) / dK scaled and rotated back (wave B) for this lane's key
   const int key = kw0 + r;
   if (key >= a.S) return;
-  if (!roleA && ROPE) {
+  if (!roleA && ROPE != 0) {
     const float* cr = a.rope_cos + (int64_t)key * (D / 2);
     const float* sr = a.rope_sin + (int64_t)key * (D / 2);
 #pragma unroll
@@ -1052,7 +1052,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
 // the causal mask row t only reads blocks kb <= (t+off)/BK (the others were never written for
 // it).  Not the last pass: the sum goes on into the fp32 running sum ``dq_sum``; the last pass
 // adds the running sum (if any) and writes dq (bf16, strided) = scale * total.
-template <int D, int BK, bool ROPE>
+template <int D, int BK, int ROPE>
 __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   constexpr int CPR = D / 8;
   const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] *= a.scale;
-  if (ROPE) {
+  if (ROPE != 0) {
     // R^T: the partner chunk (c +- CPR/2) of this row is held by lane ^ CPR/2
     const int lo = c < CPR / 2;
     const int64_t tab = (int64_t)(t + a.S - a.T) * (D / 2) + (c % (CPR / 2)) * 8;
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
 // (deterministic) into the fp32 running sum (kept in the same fragment order) or, on the last
 // pass, transposes the tile through LDS and writes dq = scale * total as whole 16-B row chunks,
 // rotated back with RoPE (each thread holds a dim chunk and its d + D/2 partner).
-template <int D, int BK, bool ROPE>
+template <int D, int BK, int ROPE>
 __global__ __launch_bounds__(256) void attn_dq_reduce_frag_kernel(AttnBwdArgs a) {
   constexpr int NDB = D / 32, NTH = 64 * NDB, LD = D + 4;  // LD: padded fp32 row of the LDS tile
   __shared__ float tile[32 * LD];
@@ -1171,7 +1171,7 @@ __global__ __launch_bounds__(256) void attn_dq_reduce_frag_kernel(AttnBwdArgs a)
       lo[e] = tile[row * LD + 8 * c + e];
       hi[e] = tile[row * LD + D / 2 + 8 * c + e];
     }
-    if (ROPE) {  // R^T: (x, y) at dims (d, d + D/2) -> (x c + y s, y c - x s)
+    if (ROPE != 0) {  // R^T: (x, y) at dims (d, d + D/2) -> (x c + y s, y c - x s)
       const int64_t tab = (int64_t)(qq + a.S - a.T) * (D / 2) + 8 * c;
       const f32x4* cp = reinterpret_cast<const f32x4*>(a.rope_cos + tab);
       const f32x4* sp = reinterpret_cast<const f32x4*>(a.rope_sin + tab);
@@ -1220,7 +1220,7 @@ static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
 }
 
-template <int D, int V, bool ROPE>
+template <int D, int V, int ROPE>
 static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
@@ -1238,10 +1238,13 @@ static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
   }
 }
 
+// RoPE mode: 0 none, 1 rotate q / k inputs and dq / dk outputs, 2 inputs already rotated (the
+// caller's pre-pass), rotate the outputs back only
 template <int D, int V>
 static void attn_bwd_r(const AttnBwdArgs& a, hipStream_t st) {
-  if (a.rope_cos) attn_bwd_t<D, V, true>(a, st);
-  else attn_bwd_t<D, V, false>(a, st);
+  if (!a.rope_cos) attn_bwd_t<D, V, 0>(a, st);
+  else if (a.rope_in) attn_bwd_t<D, V, 1>(a, st);
+  else attn_bwd_t<D, V, 2>(a, st);
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
@@ -1250,7 +1253,7 @@ void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
   else attn_fwd_t<128>(a, st);
 }
 
-template <int D, bool ROPE>
+template <int D, int ROPE>
 static void attn_bwd_rs_t(AttnBwdArgs a, hipStream_t st) {
   using C = RsCfg<D>;
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
@@ -1270,8 +1273,9 @@ static void attn_bwd_rs_t(AttnBwdArgs a, hipStream_t st) {
 
 template <int D>
 static void attn_bwd_rs_r(const AttnBwdArgs& a, hipStream_t st) {
-  if (a.rope_cos) attn_bwd_rs_t<D, true>(a, st);
-  else attn_bwd_rs_t<D, false>(a, st);
+  if (!a.rope_cos) attn_bwd_rs_t<D, 0>(a, st);
+  else if (a.rope_in) attn_bwd_rs_t<D, 1>(a, st);
+  else attn_bwd_rs_t<D, 2>(a, st);
 }
 
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {

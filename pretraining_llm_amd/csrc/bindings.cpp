@@ -358,6 +358,29 @@ Tensor swiglu_bwd(const Tensor& dy, const Tensor& gu) {
 }
 
 // packed rows [..., n_heads_total * D]; rotates the first n_rot heads; T = positions per sequence
+// attention pre-pass: the rotated q and k heads of a packed [.., (H + 2 Hkv) D] qkv tensor as one
+// contiguous [.., (H + Hkv) D] buffer (v is not copied)
+Tensor rope_qk(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_heads_total, int64_t n_rot, int64_t T) {
+  check_bf16(x, "x");
+  check_contig(x, "x");
+  TORCH_CHECK(cos.scalar_type() == at::kFloat && sin.scalar_type() == at::kFloat, "rope tables must be fp32");
+  TORCH_CHECK(cos.is_contiguous() && sin.is_contiguous(), "rope tables contiguous");
+  const int64_t W = x.size(-1);
+  TORCH_CHECK(W % n_heads_total == 0 && n_rot > 0 && n_rot <= n_heads_total, "rope_qk: heads");
+  const int64_t D = W / n_heads_total;
+  TORCH_CHECK(D % 16 == 0, "rope_qk: head dim must be a multiple of 16");
+  TORCH_CHECK(cos.size(-1) == D / 2 && cos.size(0) >= T, "rope_qk: table shape");
+  const int64_t rows = x.numel() / W;
+  TORCH_CHECK(rows % T == 0, "rope_qk: rows must be a multiple of T");
+  auto sizes = x.sizes().vec();
+  sizes.back() = n_rot * D;
+  Tensor out = at::empty(sizes, x.options());
+  if (rows)
+    pllm::rope(x.data_ptr(), out.data_ptr(), cos.data_ptr<float>(), sin.data_ptr<float>(), rows, (int)T,
+               (int)n_heads_total, (int)n_rot, (int)D, 0, false, cur_stream(), (int)n_rot);
+  return out;
+}
+
 Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_heads_total, int64_t n_rot, int64_t T,
             int64_t pos_offset, bool inverse) {
   check_bf16(x, "x");
@@ -720,7 +743,7 @@ int64_t attn_bwd_ws_bytes() {
 // dq/dk/dv are written into caller-provided views (e.g. slices of a packed dQKV buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
               Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale, const std::optional<Tensor>& rope_cos,
-              const std::optional<Tensor>& rope_sin) {
+              const std::optional<Tensor>& rope_sin, bool rope_in) {
   const int64_t D = q.size(3);
   TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128");
   for (auto& pr : std::vector<std::pair<const Tensor*, const char*>>{
@@ -762,6 +785,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.dq_acc = (uint16_t*)dq_acc.data_ptr();
   a.dq_sum = dq_sum.defined() ? dq_sum.data_ptr<float>() : nullptr;
   a.kb0 = 0;
+  a.rope_in = rope_in ? 1 : 0;
   a.slab = slab_elems;
   a.nqt = (int)nqt;
   a.nkb_pass = (int)per;
@@ -801,6 +825,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("swiglu_fwd(Tensor gate_up) -> Tensor");
   m.def("swiglu_bwd(Tensor dy, Tensor gate_up) -> Tensor");
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse) -> Tensor");
+  m.def("rope_qk(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
@@ -813,7 +838,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None) -> Tensor[]");
   m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, Tensor? seqlen=None) -> Tensor");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, bool rope_in=True) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
@@ -828,6 +853,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("swiglu_fwd", swiglu_fwd);
   m.impl("swiglu_bwd", swiglu_bwd);
   m.impl("rope", rope);
+  m.impl("rope_qk", rope_qk);
   m.impl("scale_", scale_);
   m.impl("cross_entropy", cross_entropy);
   m.impl("adamw_", adamw_);

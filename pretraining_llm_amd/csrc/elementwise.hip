@@ -146,21 +146,23 @@ __global__ __launch_bounds__(256) void swiglu_bwd_kernel(const uint16_t* __restr
 // (q heads then k heads); the remaining heads (v) are copied when out != in.
 // cos/sin: fp32 [T, D/2]; row r has position (r % T) + pos_offset.
 // dir = +1 forward rotation, -1 inverse (backward).
+// out_heads: heads written per output row (n_heads_total: full copy; n_rot: the rotated q and k
+// heads only, into a [rows, n_rot*D] buffer -- the attention pre-pass)
 __global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                                    const float* __restrict__ cosb, const float* __restrict__ sinb,
                                                    size_t rows, int T, int n_heads_total, int n_rot, int D,
-                                                   int pos_offset, float dir) {
+                                                   int pos_offset, float dir, int out_heads) {
   const int half = D >> 1;
   const int hv = half >> 3;  // 8-element groups per half
-  const size_t W = (size_t)n_heads_total * D;
-  const size_t nwork = rows * n_heads_total * hv;
+  const size_t W = (size_t)n_heads_total * D, WO = (size_t)out_heads * D;
+  const size_t nwork = rows * out_heads * hv;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nwork; i += (size_t)gridDim.x * blockDim.x) {
     const int g = (int)(i % hv);
     const size_t rh = i / hv;
-    const int h = (int)(rh % n_heads_total);
-    const size_t r = rh / n_heads_total;
+    const int h = (int)(rh % out_heads);
+    const size_t r = rh / out_heads;
     const uint16_t* src = in + r * W + (size_t)h * D;
-    uint16_t* dst = out + r * W + (size_t)h * D;
+    uint16_t* dst = out + r * WO + (size_t)h * D;
     u32x4 lo = ld16(src + g * 8), hi = ld16(src + half + g * 8);
     if (h < n_rot) {
       const int t = (int)(r % T) + pos_offset;
@@ -241,10 +243,11 @@ void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, h
 }
 
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
-          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st) {
-  const size_t nwork = rows * n_heads_total * (D / 16);
+          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st, int out_heads) {
+  if (out_heads <= 0) out_heads = n_heads_total;
+  const size_t nwork = rows * out_heads * (D / 16);
   hipLaunchKernelGGL(rope_kernel, dim3(ew_grid(nwork)), dim3(256), 0, st, (const uint16_t*)in, (uint16_t*)out, cosb,
-                     sinb, rows, T, n_heads_total, n_rot, D, pos_offset, inverse ? -1.f : 1.f);
+                     sinb, rows, T, n_heads_total, n_rot, D, pos_offset, inverse ? -1.f : 1.f, out_heads);
 }
 
 void scale_bf16(void* x, const float* s, size_t n, hipStream_t st) {

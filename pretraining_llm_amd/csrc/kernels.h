@@ -38,6 +38,7 @@ struct AttnBwdArgs {
   uint16_t* dq_acc;  // [nkb_pass][B, T, H, D] bf16 per-key-block dQ partial slabs of one pass
   float* dq_sum;  // [B, T, H, D] fp32 running dQ sum across passes (null when one pass)
   int kb0, nkb_pass;  // first key block of the pass / key blocks per pass (set by the host)
+  int rope_in;        // with rope tables: 1 = rotate q / k in-kernel, 0 = already rotated (outputs only)
   int64_t slab;       // elements per dQ slab (>= B * ceil32(T) * H * D)
   int nqt;            // ceil(T / 32): query tiles per head in the fragment-order slab (RS kernel)
   uint16_t *dq, *dk, *dv;
@@ -75,7 +76,7 @@ void act_bwd_bias(int op, const void* dy, const void* xin, void* dx, int N, int 
 void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st);
 void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st);
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
-          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st);
+          int n_rot, int D, int pos_offset, bool inverse, hipStream_t st, int out_heads = 0);
 void scale_bf16(void* x, const float* s, size_t n, hipStream_t st);
 
 // cross_entropy.hip

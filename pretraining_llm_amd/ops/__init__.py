@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import contextlib
 import math
+import os
 from typing import Optional
 
 import torch
@@ -381,30 +382,48 @@ def _split_qkv(qkv, H, Hkv, D):
 
 
 class _FlashAttnPacked(torch.autograd.Function):
-    """Attention over the packed QKV projection; with ``cos``/``sin`` the q and k heads are
-    rotated (RoPE) inside the kernels -- forward and backward -- and the gradient comes back
-    for the unrotated packed tensor (no separate RoPE launches, csrc/attention.hip)."""
+    """Attention over the packed QKV projection.  With ``cos``/``sin`` (RoPE) one pre-pass
+    writes the rotated q and k heads to a [B, T, (H + Hkv) D] buffer that both the forward and
+    the backward kernels read (kept for the backward: 2/3 of qkv for MHA); the backward kernels
+    rotate dq / dk back while storing them, so the gradient comes back for the unrotated packed
+    tensor.  Rotating inside the tile loops instead (rope_pre=False: tables read per tile)
+    measured +22 % forward / +25 % backward at the llama shape (profiles/r2_rope_prepass_ab.txt)."""
 
     @staticmethod
     def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin):
         B, T, W = qkv.shape
         D = W // (H + 2 * Hkv)
         q, k, v = _split_qkv(qkv, H, Hkv, D)
-        o, lse = _ops().attn_fwd(q, k, v, causal, scale, cos, sin)
-        ctx.save_for_backward(qkv, o, lse, cos, sin)
+        qk = None
+        if cos is not None and _ROPE_PREPASS:
+            qk = _ops().rope_qk(qkv, cos, sin, H + 2 * Hkv, H + Hkv, T)
+            q = qk[..., : H * D].view(B, T, H, D)
+            k = qk[..., H * D:].view(B, T, Hkv, D)
+            o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+        else:
+            o, lse = _ops().attn_fwd(q, k, v, causal, scale, cos, sin)
+        ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
         ctx.cfg = (H, Hkv, D, causal, scale)
         return o.view(B, T, H * D)
 
     @staticmethod
     def backward(ctx, do):
-        qkv, o, lse, cos, sin = ctx.saved_tensors
+        qkv, qk, o, lse, cos, sin = ctx.saved_tensors
         H, Hkv, D, causal, scale = ctx.cfg
         B, T, _ = qkv.shape
         q, k, v = _split_qkv(qkv, H, Hkv, D)
+        if qk is not None:
+            q = qk[..., : H * D].view(B, T, H, D)
+            k = qk[..., H * D:].view(B, T, Hkv, D)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = _split_qkv(dqkv, H, Hkv, D)
-        _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin)
+        _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin,
+                        qk is None)
         return dqkv, None, None, None, None, None, None
+
+
+# RoPE for the HIP attention: pre-pass rotation (default) or rotation inside the kernels' tile loops
+_ROPE_PREPASS = os.environ.get("PLLM_ROPE_PREPASS", "1") == "1"
 
 
 class _RopePackedFn(torch.autograd.Function):

@@ -78,6 +78,10 @@ def register() -> None:
     def _(x, cos, sin, n_heads_total, n_rot, T, pos_offset, inverse):
         return torch.empty_like(x)
 
+    @_reg("rope_qk")
+    def _(x, cos, sin, n_heads_total, n_rot, T):
+        return x.new_empty((*x.shape[:-1], x.shape[-1] // n_heads_total * n_rot))
+
     @_reg("scale_")
     def _(x, s):
         return None
@@ -129,7 +133,7 @@ def register() -> None:
         return q.new_empty(q.shape)
 
     @_reg("attn_bwd")
-    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, rope_cos=None, rope_sin=None):
+    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, rope_cos=None, rope_sin=None, rope_in=True):
         return None
 
     @_reg("gemv")

@@ -859,15 +859,20 @@ def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
 
 @pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1)])
 @pytest.mark.parametrize("variant", [0, 8, 16])
-def test_attention_fused_rope_fwd_bwd(D, Hkv, variant):
-    """RoPE applied inside the attention kernels (q/k rotated while staged, dq/dk rotated back)
-    == rotate-half RoPE + attention in fp32 torch, gradients w.r.t. the UNROTATED packed qkv
-    (default and role-split backward)."""
+@pytest.mark.parametrize("prepass", [True, False])
+def test_attention_fused_rope_fwd_bwd(D, Hkv, variant, prepass):
+    """RoPE with the HIP attention == rotate-half RoPE + attention in fp32 torch, gradients
+    w.r.t. the UNROTATED packed qkv: pre-pass (rope_qk once, backward rotates dq/dk back while
+    storing them) and in-kernel rotation (q/k rotated while staged), every backward variant."""
+    from pretraining_llm_amd import ops
     torch.ops.pllm.attn_bwd_set_variant(variant)
+    old = ops._ROPE_PREPASS
+    ops._ROPE_PREPASS = prepass
     try:
         _rope_case(D, Hkv)
     finally:
         torch.ops.pllm.attn_bwd_set_variant(0)
+        ops._ROPE_PREPASS = old
 
 
 def _rope_case(D, Hkv):
