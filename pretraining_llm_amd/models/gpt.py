@@ -291,7 +291,10 @@ class GPT(nn.Module):
         attention output, MLP pre/post activation) -- within 2 % of the measured difference
         between checkpointed and full runs of GPT-2 medium at 32K tokens (36.9 vs 14.4 GB)."""
         cfg = self.config
-        return 2 * (6 * cfg.n_embed + 2 * cfg.ffn_hidden) * tokens * cfg.n_blocks
+        per = 6 * cfg.n_embed + 2 * cfg.ffn_hidden
+        if cfg.pos == "rope":  # rotated q / k of the attention pre-pass (ops._FlashAttnPacked)
+            per += (cfg.n_head + cfg.n_kv_head) * cfg.head_dim
+        return 2 * per * tokens * cfg.n_blocks
 
     def checkpointed_blocks(self, idx) -> int:
         """How many of the first blocks recompute their forward in backward.
