@@ -89,7 +89,8 @@ default_config = {
     'activation_checkpointing': None,
     'tp_size': 1,                     # tensor parallelism: heads / FFN columns sharded (parallel/model_parallel.py)
     'sequence_parallel': False,       # with tp_size > 1: norm/residual regions sharded along the sequence
-    'cp_size': 1,                     # context parallelism: zigzag sequence shards + ring attention
+    'cp_size': 1,                     # context parallelism: sequence shards over cp_size ranks
+    'cp_mode': 'ring',                # ring (zigzag shards, K/V ring) | ulysses (all-to-all head re-sharding)
     'zero_stage': 0,                  # 1 = shard fp32 master + AdamW moments over DP ranks (parallel/zero.py)
     'profile_dir': None,              # torch.profiler (ROCm activity) chrome traces + kernel table per rank
     'profile_steps': '3:6',           # [start:end) optimizer steps to profile

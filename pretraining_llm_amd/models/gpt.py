@@ -355,17 +355,26 @@ class GPT(nn.Module):
         pg = self.parallel
         if pg is None or pg.cp == 1:
             return None
+        if pg.cp_mode == "ulysses":  # contiguous shard
+            Tl = idx.shape[1]
+            return torch.arange(pg.cp_rank * Tl, (pg.cp_rank + 1) * Tl, device=idx.device)
         from ..parallel.context import zigzag_positions
         return zigzag_positions(idx.shape[1], pg.cp_group, idx.device)
 
     def _shard_inputs(self, idx, targets):
         """Model parallelism: every rank of a TP / CP group receives the same full batch; CP keeps
-        this rank's zigzag sequence shard (sequence parallelism splits after the embedding)."""
+        this rank's sequence shard -- zigzag chunks for ring attention, one contiguous chunk for
+        Ulysses (sequence parallelism splits after the embedding)."""
         pg = self.parallel
         if pg is not None and pg.cp > 1:
-            from ..parallel.context import zigzag_shard
-            idx = zigzag_shard(idx, 1, pg.cp_group)
-            targets = zigzag_shard(targets, 1, pg.cp_group) if targets is not None else None
+            if pg.cp_mode == "ulysses":
+                from ..parallel.tensor import _split_dim
+                idx = _split_dim(idx, 1, pg.cp_group)
+                targets = _split_dim(targets, 1, pg.cp_group) if targets is not None else None
+            else:
+                from ..parallel.context import zigzag_shard
+                idx = zigzag_shard(idx, 1, pg.cp_group)
+                targets = zigzag_shard(targets, 1, pg.cp_group) if targets is not None else None
         return idx, targets
 
     def _trunk(self, idx):

@@ -17,9 +17,10 @@ per-layer all-reduces are the latency-critical traffic):
   per rank; all-gather before each column-parallel GEMM, reduce-scatter after each
   row-parallel one, LM head + CE on the local tokens.  Replicated parameters then carry
   partial gradients, which ``sync_replicated_grads`` sums over the TP group.
-* **CP** (``cp_size``): the sequence is sharded over the CP group in the load-balanced
-  zigzag layout; attention is ring attention over RCCL point-to-point with the flash
-  kernels' LSE merge (``parallel/context.py``); position embeddings / RoPE tables are
+* **CP** (``cp_size``): the sequence is sharded over the CP group.  ``cp_mode="ring"``:
+  load-balanced zigzag layout, ring attention over RCCL point-to-point with the flash kernels'
+  LSE merge (``parallel/context.py``); ``cp_mode="ulysses"``: contiguous shards, all-to-all to
+  head sharding around full-sequence flash attention.  Position embeddings / RoPE tables are
   gathered at the shard's global positions; gradients are averaged over dp x cp.
 
 The model is built dense on every rank (same seed), then ``parallelize_gpt`` slices each
@@ -55,15 +56,19 @@ class ParallelGroups:
     dp_group: object = None
     grad_group: object = None      # ranks that average gradients: dp x cp (same tp rank)
     sequence_parallel: bool = False
+    cp_mode: str = "ring"          # "ring": zigzag shards + ring attention; "ulysses": contiguous + all-to-all
 
     @property
     def model_parallel(self) -> bool:
         return self.tp > 1 or self.cp > 1
 
 
-def init_parallel_groups(tp: int = 1, cp: int = 1, sequence_parallel: bool = False) -> ParallelGroups:
+def init_parallel_groups(tp: int = 1, cp: int = 1, sequence_parallel: bool = False,
+                         cp_mode: str = "ring") -> ParallelGroups:
     """Create the dp / cp / tp / gradient process groups of a ``dp x cp x tp`` mesh (every rank
     must call this, in the same order).  rank = (dp_rank * cp + cp_rank) * tp + tp_rank."""
+    if cp_mode not in ("ring", "ulysses"):
+        raise ValueError(f"cp_mode={cp_mode!r}: expected 'ring' or 'ulysses'")
     init = dist.is_initialized()
     world = dist.get_world_size() if init else 1
     rank = dist.get_rank() if init else 0
@@ -73,7 +78,8 @@ def init_parallel_groups(tp: int = 1, cp: int = 1, sequence_parallel: bool = Fal
         raise ValueError("sequence_parallel needs tp_size > 1")
     dp = world // (tp * cp)
     tp_rank, cp_rank, dp_rank = rank % tp, (rank // tp) % cp, rank // (tp * cp)
-    g = ParallelGroups(world, rank, tp, tp_rank, None, cp, cp_rank, None, dp, dp_rank, None, None, sequence_parallel)
+    g = ParallelGroups(world, rank, tp, tp_rank, None, cp, cp_rank, None, dp, dp_rank, None, None, sequence_parallel,
+                       cp_mode)
     if not init or world == 1:
         return g
 
@@ -237,6 +243,43 @@ class CPAttention(nn.Module):
         return y
 
 
+class UlyssesAttention(nn.Module):
+    """Attention of a contiguous sequence shard by Ulysses re-sharding: the projections run on
+    the local T/cp tokens, one all-to-all turns q / k / v from sequence- to head-sharded (each
+    rank then holds the WHOLE sequence for H/cp query heads and Hkv/cp kv heads), the flash
+    kernels run causal attention over the full sequence, and one all-to-all turns the output
+    back.  Two all-to-alls of the activations per direction instead of the ring's cp - 1 K/V
+    hops; needs n_head and n_kv_head divisible by cp_size.  RoPE is applied on the shard with its
+    own position tables before the exchange."""
+
+    fused_bias_ok = True
+
+    def __init__(self, dense, pg: ParallelGroups):
+        super().__init__()
+        if dense.n_head % pg.cp or dense.n_kv_head % pg.cp:
+            raise ValueError(f"Ulysses: n_head {dense.n_head} and n_kv_head {dense.n_kv_head} must be divisible by "
+                             f"cp_size {pg.cp}")
+        self.pg = pg
+        self.qkv, self.proj = dense.qkv, dense.proj
+        self.n_head, self.n_kv_head, self.head_dim = dense.n_head, dense.n_kv_head, dense.head_dim
+
+    def forward(self, x, rope=None, fuse_out_bias: bool = False):
+        H, Hkv, D, g = self.n_head, self.n_kv_head, self.head_dim, self.pg.cp_group
+        qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
+        if rope is not None:
+            qkv = ops.rope_packed(qkv, rope[0], rope[1], H, Hkv)  # the shard's own position tables
+        B, Tl, _ = qkv.shape
+        q, k, v = ops._split_qkv(qkv, H, Hkv, D)
+        qh, kh, vh = (tpar.seq_to_head_all_to_all(t.contiguous(), g) for t in (q, k, v))  # [B, T, h/cp, D]
+        T, Hl, Hkl = qh.shape[1], qh.shape[2], kh.shape[2]
+        packed = torch.cat([qh, kh, vh], dim=2).reshape(B, T, (Hl + 2 * Hkl) * D)
+        o = ops.attention_packed(packed, Hl, Hkl, causal=True).view(B, T, Hl, D)
+        y = tpar.head_to_seq_all_to_all(o, g).reshape(B, Tl, H * D)
+        if self.proj is not None:
+            y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
+        return y
+
+
 def parallelize_gpt(model, pg: ParallelGroups):
     """Shard a dense ``GPT`` in place for ``pg`` (TP: heads / FFN columns; CP: ring attention)."""
     if pg.tp > 1 and pg.cp > 1:
@@ -247,7 +290,7 @@ def parallelize_gpt(model, pg: ParallelGroups):
             blk.attn = TPAttention(blk.attn, cfg, pg)
             blk.mlp = TPMLP(blk.mlp, cfg, pg)
         elif pg.cp > 1:
-            blk.attn = CPAttention(blk.attn, pg)
+            blk.attn = UlyssesAttention(blk.attn, pg) if pg.cp_mode == "ulysses" else CPAttention(blk.attn, pg)
     model.parallel = pg
     return model
 

@@ -96,7 +96,8 @@ class Trainer:
         # model parallelism (parallel/model_parallel.py): a dp x cp x tp mesh; the model is built
         # dense from the shared seed, then sharded, so every layout starts from the same weights
         tp, cp = int(self.cfg.get("tp_size", 1)), int(self.cfg.get("cp_size", 1))
-        self.pg = init_parallel_groups(tp, cp, bool(self.cfg.get("sequence_parallel", False)))
+        self.pg = init_parallel_groups(tp, cp, bool(self.cfg.get("sequence_parallel", False)),
+                                       self.cfg.get("cp_mode", "ring"))
         if self.pg.model_parallel:
             parallelize_gpt(self.model, self.pg)
         decay_filter = None if self.cfg.get("weight_decay_all", True) else no_decay_1d

@@ -56,7 +56,7 @@ def _batch(dp):
     return data[:, :-1], data[:, 1:]
 
 
-def _worker(rank, world, port, outdir, arch, tp, cp, sp, zero):
+def _worker(rank, world, port, outdir, arch, tp, cp, sp, zero, cp_mode="ring"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -68,7 +68,7 @@ def _worker(rank, world, port, outdir, arch, tp, cp, sp, zero):
     cfg = _cfg(arch)
     torch.manual_seed(0)
     model = GPT(cfg)
-    pg = init_parallel_groups(tp, cp, sp)
+    pg = init_parallel_groups(tp, cp, sp, cp_mode)
     parallelize_gpt(model, pg)
     okw = dict(lr=1e-2, weight_decay=0.1, max_grad_norm=MAX_NORM, eps=EPS)
     if zero:
@@ -134,14 +134,17 @@ CASES = {
     "cp2_llama": (2, "llama", 1, 2, False, False),
     "tp2_sp_dp2_zero_llama": (4, "llama", 2, 1, True, True),
     "cp2_dp2_gpt2": (4, "gpt2", 1, 2, False, False),
+    "ulysses2_gpt2": (2, "gpt2", 1, 2, False, False, "ulysses"),
+    "ulysses2_llama_gqa_rope": (2, "llama", 1, 2, False, False, "ulysses"),
+    "ulysses2_dp2_zero_llama": (4, "llama", 1, 2, False, True, "ulysses"),
 }
 
 
 @pytest.mark.parametrize("case", list(CASES))
 def test_model_parallel_step_matches_dense(case):
-    world, arch, tp, cp, sp, zero = CASES[case]
+    world, arch, tp, cp, sp, zero, *mode = CASES[case]
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, arch, tp, cp, sp, zero), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, arch, tp, cp, sp, zero, *mode), nprocs=world, join=True)
         got = torch.load(os.path.join(d, "out.pt"), weights_only=True)
     ref = _dense(arch, world // (tp * cp))
     assert abs(got["loss"] - ref["loss"]) < 1e-5, (got["loss"], ref["loss"])
@@ -198,7 +201,8 @@ def _trainer_worker(rank, world, port, tmp, kw):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kw", [dict(tp_size=2, sequence_parallel=True), dict(cp_size=2)], ids=["tp2_sp", "cp2"])
+@pytest.mark.parametrize("kw", [dict(tp_size=2, sequence_parallel=True), dict(cp_size=2),
+                                dict(cp_size=2, cp_mode="ulysses")], ids=["tp2_sp", "cp2", "ulysses2"])
 def test_trainer_model_parallel_matches_dense_and_resumes(tmp_path, kw):
     """Trainer with tp_size / cp_size on 2 gloo ranks: the consolidated dense checkpoint after 8
     steps equals a 1-process dense Trainer's weights on the same data, and resuming from the

@@ -50,7 +50,7 @@ def _step(model, opt, x, y, pg=None, eng=None):
     return loss, scale
 
 
-def _worker(rank, world, port, outdir, arch, tp, cp, sp):
+def _worker(rank, world, port, outdir, arch, tp, cp, sp, cp_mode="ring"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -64,7 +64,7 @@ def _worker(rank, world, port, outdir, arch, tp, cp, sp):
     cfg = _cfg(arch)
     torch.manual_seed(0)
     model = GPT(cfg).to(dev, torch.bfloat16)
-    pg = init_parallel_groups(tp, cp, sp)
+    pg = init_parallel_groups(tp, cp, sp, cp_mode)
     parallelize_gpt(model, pg)
     opt = FlatAdamW(model, lr=1e-3, max_grad_norm=1e9)
     eng = DataParallelEngine(opt, process_group=pg.grad_group)
@@ -101,12 +101,12 @@ def _dense(arch):
 
 
 @pytest.mark.parametrize("case", [("gpt2", 2, 1, True), ("llama", 2, 1, True), ("llama", 2, 1, False),
-                                  ("llama", 1, 2, False)], ids=["tp2_sp_gpt2", "tp2_sp_llama", "tp2_llama",
-                                                                 "cp2_llama"])
+                                  ("llama", 1, 2, False), ("llama", 1, 2, False, "ulysses")],
+                         ids=["tp2_sp_gpt2", "tp2_sp_llama", "tp2_llama", "cp2_ring_llama", "cp2_ulysses_llama"])
 def test_model_parallel_step_on_hip_kernels(case):
-    arch, tp, cp, sp = case
+    arch, tp, cp, sp, *mode = case
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(2, _free_port(), d, arch, tp, cp, sp), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), d, arch, tp, cp, sp, *mode), nprocs=2, join=True)
         got = torch.load(os.path.join(d, "out.pt"), weights_only=True)
     ref = _dense(arch)
     assert abs(got["loss"] - ref["loss"]) < 2e-2, (got["loss"], ref["loss"])
