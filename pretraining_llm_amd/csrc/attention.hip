@@ -422,7 +422,7 @@ struct BwdCfg {
 
 // dQ: each key block's partial dQ (summed over its BK keys on chip, rounded once to bf16) goes
 // to a slab of the current PASS: the host runs the key blocks in passes of at most
-// ``nkb_pass`` blocks so the workspace is bounded independently of T; attn_dq_reduce_kernel adds
+// ``nkb_pass`` blocks so the workspace is bounded independently of T; attn_dq_reduce_frag_kernel adds
 // the slabs in fp32 in a fixed order (deterministic, no atomics) into an fp32 running sum / the
 // bf16 dQ.  fp32 slabs (no partial rounding) measured +12 % (T 1024, D 64) to +34 % (T 4096)
 // on the whole backward: the slab bytes are its second cost after the MFMAs.
@@ -690,9 +690,12 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     for (int task = w; task < NTASK; task += C::NW) {
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
+      if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
       // causal: key steps entirely after the task's last query contribute zeros -> skip
       int ks_end = BK / 16;
       if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
+      // dQ^T tile = K^T dS^T (query on the lane), dumped as a coalesced fragment-order block
+      // (attn_dq_reduce_frag_kernel reads it back)
       f32x16 acc = zero16();
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
@@ -701,14 +704,18 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
         const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
         const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
-        acc = mfma32(A, Bf, acc);
+        acc = mfma32(Bf, A, acc);
       }
-      uint16_t* dq = a.dq_acc + (kb - a.kb0) * a.slab + (((int64_t)b * a.T) * a.H + h) * D + tdb * 32 + r;
+      uint16_t* blk = a.dq_acc + (kb - a.kb0) * a.slab +
+                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
+      float lo[8], hi[8];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int q = qt0 + acc_row(i, hh);
-        if (q < a.T) dq[(int64_t)q * a.H * D] = f2bf_bits(acc[i]);
+      for (int e = 0; e < 8; ++e) {
+        lo[e] = acc[e];
+        hi[e] = acc[8 + e];
       }
+      st16(blk, pack8(lo));
+      st16(blk + 8, pack8(hi));
     }
   }
   // write dK (scaled) and dV for this lane's keys; with RoPE, dK is rotated back (R^T): the
@@ -989,6 +996,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     for (int task = w; task < NTASK; task += C::NW) {
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
+      if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
       int ks_end = BK / 16;
       if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
       // dQ^T tile = K^T dS^T: the accumulator has the QUERY on the lane and 16 head-dim values
@@ -1048,71 +1056,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   }
 }
 
-// Sum this pass's fp32 dQ slabs [nkb_pass][B,T,H,D] in key-block order (deterministic); under
-// the causal mask row t only reads blocks kb <= (t+off)/BK (the others were never written for
-// it).  Not the last pass: the sum goes on into the fp32 running sum ``dq_sum``; the last pass
-// adds the running sum (if any) and writes dq (bf16, strided) = scale * total.
-template <int D, int BK, int ROPE>
-__global__ __launch_bounds__(256) void attn_dq_reduce_kernel(AttnBwdArgs a) {
-  constexpr int CPR = D / 8;
-  const int64_t gid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int64_t row = gid / CPR;
-  const int c = (int)(gid % CPR);
-  const int64_t nrows = (int64_t)a.B * a.T * a.H;
-  if (row >= nrows) return;
-  const int h = (int)(row % a.H);
-  const int64_t bt = row / a.H;
-  const int t = (int)(bt % a.T);
-  const int b = (int)(bt / a.T);
-  const int nkb = (a.S + BK - 1) / BK;
-  int kmax = min(nkb - 1, a.kb0 + a.nkb_pass - 1);
-  if (a.causal) kmax = min(kmax, (t + a.S - a.T) / BK);
-  float f[8];
-  if (a.kb0 > 0) {
-    const f32x4* p = reinterpret_cast<const f32x4*>(a.dq_sum + row * D + c * 8);
-    const f32x4 x0 = p[0], x1 = p[1];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      f[j] = x0[j];
-      f[4 + j] = x1[j];
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = 0.f;
-  }
-  const uint16_t* src = a.dq_acc + row * D + c * 8;
-  for (int kb = a.kb0; kb <= kmax; ++kb) {
-    float x[8];
-    unpack8(ld16(src + (kb - a.kb0) * a.slab), x);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] += x[j];
-  }
-  if (a.kb0 + a.nkb_pass < nkb) {  // more passes follow
-    f32x4* p = reinterpret_cast<f32x4*>(a.dq_sum + row * D + c * 8);
-    p[0] = f32x4{f[0], f[1], f[2], f[3]};
-    p[1] = f32x4{f[4], f[5], f[6], f[7]};
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] *= a.scale;
-  if (ROPE != 0) {
-    // R^T: the partner chunk (c +- CPR/2) of this row is held by lane ^ CPR/2
-    const int lo = c < CPR / 2;
-    const int64_t tab = (int64_t)(t + a.S - a.T) * (D / 2) + (c % (CPR / 2)) * 8;
-    float g[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) g[j] = __shfl_xor(f[j], CPR / 2, 64);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float cs = a.rope_cos[tab + j], sn = a.rope_sin[tab + j];
-      f[j] = lo ? f[j] * cs + g[j] * sn : f[j] * cs - g[j] * sn;
-    }
-  }
-  st16(a.dq + b * a.dq_sb + (int64_t)t * a.dq_st + (int64_t)h * a.dq_sh + c * 8, pack8(f));
-}
-
-
-// Reduce of the role-split kernel's fragment-order slabs.  One workgroup (64 x D/32 threads) per
+// Reduce of the backward kernels' fragment-order dQ slabs.  One workgroup (64 x D/32 threads) per
 // 32-query tile of one (batch, head): thread (d-block blk, lane l) reads its 32 contiguous bytes of
 // the tile's block blk from every slab of the pass (coalesced 2-KiB wave reads; lane l holds query
 // l%32 and head dims blk*32 + acc_row(i, l/32), i < 16), sums them in key-block order
@@ -1233,7 +1177,8 @@ static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
     a.nkb_pass = min(per, nkb - kb0);
     hipLaunchKernelGGL((attn_bwd_kernel<D, V, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st,
                        a);
-    hipLaunchKernelGGL((attn_dq_reduce_kernel<D, BwdCfg<D, V>::BK, ROPE>), dim3(pre_grid), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, BwdCfg<D, V>::BK, ROPE>), dim3(a.B * a.H * a.nqt),
+                       dim3(64 * (D / 32)), 0, st, a);
     a.nkb_pass = per;
   }
 }
