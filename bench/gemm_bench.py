@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="gpt2", choices=["gpt2", "llama"])
-    ap.add_argument("--variants", default="32,8", help="wgrad_set_mfma values to compare (32: two-stage, 8: phased)")
+    ap.add_argument("--variants", default="32,16", help="wgrad_set_mfma values to compare (32: 32x32x16 tiles, 16: 16x16x32 tiles)")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
