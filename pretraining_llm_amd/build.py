@@ -56,6 +56,12 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsaf
                 "-Wno-unused-result", "-Wno-unused-variable"]
 
 
+# per-file flags.  attention.hip: no SLP vectorisation -- it packs pairs of independent f32
+# multiplies of the softmax / dS math into v_pk_mul_f32 plus two v_mov each to gather the
+# operands, more vector issue beside the MFMAs than the scalar multiplies
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+
+
 def _needs(obj: str, deps) -> bool:
     if not os.path.exists(obj):
         return True
@@ -95,7 +101,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
     jobs_list = []
     for src in kernel_srcs:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-        cmd = [hipcc, *COMMON_FLAGS, "-c", src, "-o", obj]
+        cmd = [hipcc, *COMMON_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         jobs_list.append((obj, [src, *headers], cmd))
     bobj = os.path.join(BUILD, "bindings.o")
     py_inc = sysconfig.get_paths()["include"]

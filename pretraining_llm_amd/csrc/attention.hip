@@ -407,6 +407,8 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 // KH (32-key halves per wave) is kept as a parameter of the code: 4 waves x 64 keys (KH = 2,
 // one wave per SIMD, every Q/dO fragment feeding two MFMAs) measured 24-33 % SLOWER than V 0
 // at every D = 64 shape (profiles/r2_attn_bwd_variants.jsonl), so every variant uses KH = 1.
+constexpr float kLog2e = 1.4426950408889634f;
+
 template <int D, int V = 0>
 struct BwdCfg {
   static constexpr int KH = 1;
@@ -506,7 +508,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       dk[kh][db] = zero16();
       dv[kh][db] = zero16();
     }
-  const float inv_scale = 1.f / a.scale, c2 = a.scale_log2;
+  const float c2 = a.scale_log2;
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int nqb = (a.T + BQ - 1) / BQ;
   int qb_start = 0;
@@ -556,6 +558,19 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   // dQ task of this wave in each iteration: (query sub-block, d-block)
   constexpr int NTASK = NQB * NDB;
 
+  // Per-lane LDS element offsets with the swizzle applied once.  Every image's f(row) depends
+  // only on row bits 0..3, so row steps of 16 / 32 are plain additions (instruction immediates),
+  // and column-chunk steps are XORs into the chunk bits:
+  //   fragment reads (32 j + r, 16 ks + 8 hh)        = fq ^ (ks << 4) + 32 j D
+  //   transposed reads (32 j + 16 st + 4 hh + tq (+8), 32 db + 16 g1 + 4 tp)
+  //                                                   = ft0 (ft8) ^ (db << 5) + (32 j + 16 st) D
+  //   dS^T stores (key row, 32 j + 8 g + 4 hh)        = fs ^ ((4 j + g) << 3)
+  // Left to itself hipcc hoisted one full address per (j, ks / g / db) out of the loop and spilled
+  // them (scratch reloads with vmcnt(0) inside the sub-blocks, serialising the Q/dO prefetch).
+  const int fq = I::off(r, 8 * hh);
+  const int ft0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
+  const int fs0 = IS::off(w * 32 * KH + r, 4 * hh);
+
   // static priority for the second-dispatched half of an 8-wave workgroup: it loses every
   // VALU arbitration to its older SIMD partner otherwise (MI355X_MICROARCH.md, 'Two waves
   // per SIMD' item 4)
@@ -564,6 +579,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   for (int it = 0; it < total; ++it) {
     const int h = hk * G + it / per_head;
     const int q0 = (qb_start + it % per_head) * BQ;
+    // opaque per iteration: the (j, g) store offsets derived from it are formed next to their
+    // stores instead of being hoisted out of the loop as 16 live registers
+    int fs = fs0;
+    asm volatile("" : "+v"(fs));
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done
 #pragma unroll
     for (int i = 0; i < 2 * QPAIR; i += 2) {
@@ -581,12 +600,13 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     }
     if (tid < 2 * BQ) {
       const bool live = q0 + (tid & (BQ - 1)) < a.T;
-      rowc[tid] = live ? (tid < BQ ? -rc * inv_scale : -rc) : 0.f;  // -lse/scale, -delta
+      rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
     }
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 
-    const bool need_mask = (q0 + BQ > a.T) || (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
+    // rows past T need no mask: their Q / dO rows are zero-filled, their row constants 0
+    const bool need_mask = (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
       const int qj0 = q0 + 32 * j;
@@ -605,49 +625,69 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         if (kh < live) continue;
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<u32x2*>(Sl + IS::off(w * 32 * KH + 32 * kh + r, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
+          *reinterpret_cast<u32x2*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + g) << 3))) = u32x2{0u, 0u};
       }
-      auto body = [&](auto live_c) {
+      // MASKED is a compile-time property of the code path: a uniform run-time test per
+      // element made hipcc emit one basic block per exponential (16 scalar branches per
+      // sub-block), which also kept the exponentials from interleaving with the MFMAs
+      auto body = [&](auto live_c, auto mask_c) {
         constexpr int NL = decltype(live_c)::value;
-        // S' = Q K^T - lse/scale ; dP' = dO V^T - delta   (query rows in registers, key on the lane)
-        // accumulator rows 4g..4g+3 are 4 consecutive queries: one 16-B LDS read each
+        constexpr bool MASKED = decltype(mask_c)::value;
+        // S = Q K^T ; dP = dO V^T   (query rows in registers, key on the lane; zero-initialised
+        // accumulators: the row constants enter in the exponent / the subtraction below)
         f32x16 s[NL], dp[NL];
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
           const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * g + 4 * hh]);
 #pragma unroll
           for (int kh = 0; kh < NL; ++kh)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              s[kh][4 * g + e] = rs[e];
-              dp[kh][4 * g + e] = rd[e];
-            }
+            for (int e = 0; e < 4; ++e) dp[kh][4 * g + e] = rd[e];
         }
 #pragma unroll
+        for (int kh = 0; kh < NL; ++kh) s[kh] = zero16();
+#pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 qa = as_frag(ld16(Ql + I::off(32 * j + r, 16 * ks + 8 * hh)));
-          const bf16x8 oa = as_frag(ld16(Ol + I::off(32 * j + r, 16 * ks + 8 * hh)));
+          const int fo = 32 * j * D + (fq ^ (ks << 4));
+          const bf16x8 qa = as_frag(ld16(Ql + fo));
+          const bf16x8 oa = as_frag(ld16(Ol + fo));
 #pragma unroll
           for (int kh = 0; kh < NL; ++kh) {
             s[kh] = mfma32(qa, kf[kh][ks], s[kh]);
             dp[kh] = mfma32(oa, vf[kh][ks], dp[kh]);
           }
         }
+        // P = exp2(S c2 - lse log2e) ; dS = P (dP - delta)   (unscaled).  Masked paths: the
+        // lane's element i (query qb + acc_row(i)) is dead iff acc_row(i) < lo[kh] (causal:
+        // key > query; keys past S: all).  Query rows past T need no test: their Q / dO rows
+        // are zero-filled and their row constants 0, so P = 1 meets dO = 0 (dV) and dS = 0
+        // (dK, dQ), and no dQ row past T is stored.
+        int lo[NL];
+        if constexpr (MASKED) {
+#pragma unroll
+          for (int kh = 0; kh < NL; ++kh) {
+            const int key = kw0 + 32 * kh + r;
+            lo[kh] = key >= a.S ? 64 : (a.causal ? key - off - (qj0 + 4 * hh) : -64);
+          }
+        }
         bf16x8 pf[NL][2], sf[NL][2];
 #pragma unroll
-        for (int kh = 0; kh < NL; ++kh) {
-          const int key = kw0 + 32 * kh + r;
+        for (int g = 0; g < 4; ++g) {
+          // accumulator rows 4g..4g+3 are 4 consecutive queries: one 16-B LDS read each
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float p = fast_exp2(c2 * s[kh][i]);
-            if (need_mask) {
-              const int q = qj0 + acc_row(i, hh);
-              if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+          for (int kh = 0; kh < NL; ++kh)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * g + e;
+              float p = fast_exp2(__builtin_fmaf(s[kh][i], c2, rs[e]));
+              if constexpr (MASKED) p = acc_row(i, 0) < lo[kh] ? 0.f : p;
+              s[kh][i] = p;               // P
+              dp[kh][i] = p * dp[kh][i];  // dS (unscaled; dP accumulated onto -delta)
             }
-            s[kh][i] = p;               // P
-            dp[kh][i] = p * dp[kh][i];  // dS (unscaled)
-          }
+        }
+#pragma unroll
+        for (int kh = 0; kh < NL; ++kh) {
           pf[kh][0] = pack_frag(s[kh], 0);
           pf[kh][1] = pack_frag(s[kh], 1);
           sf[kh][0] = pack_frag(dp[kh], 0);
@@ -659,9 +699,9 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         for (int db = 0; db < NDB; ++db) {
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
-            const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
-            const bf16x8 oA = cat_tr(ds_tr(Ol + I::off(rowq, col)), ds_tr(Ol + I::off(rowq + 8, col)));
-            const bf16x8 qA = cat_tr(ds_tr(Ql + I::off(rowq, col)), ds_tr(Ql + I::off(rowq + 8, col)));
+            const int rb = (32 * j + 16 * st) * D, o0 = rb + (ft0 ^ (db << 5)), o8 = rb + (ft8 ^ (db << 5));
+            const bf16x8 oA = cat_tr(ds_tr(Ol + o0), ds_tr(Ol + o8));
+            const bf16x8 qA = cat_tr(ds_tr(Ql + o0), ds_tr(Ql + o8));
 #pragma unroll
             for (int kh = 0; kh < NL; ++kh) {
               dv[kh][db] = mfma32(oA, pf[kh][st], dv[kh][db]);
@@ -669,19 +709,31 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
             }
           }
         }
-        // dS^T image: the lane's key rows, 4 consecutive queries per 8-byte store
+        // dS^T image: the lane's key rows, 4 consecutive queries per 8-byte store -- dwords
+        // 2(g&1), 2(g&1)+1 of the packed fragment sf[g/2] (no second conversion)
 #pragma unroll
         for (int kh = 0; kh < NL; ++kh)
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            u32x2 v2;
-            v2[0] = pack_bf16x2(dp[kh][4 * g], dp[kh][4 * g + 1]);
-            v2[1] = pack_bf16x2(dp[kh][4 * g + 2], dp[kh][4 * g + 3]);
-            *reinterpret_cast<u32x2*>(Sl + IS::off(w * 32 * KH + 32 * kh + r, 32 * j + 8 * g + 4 * hh)) = v2;
+            const u32x4 w4 = __builtin_bit_cast(u32x4, sf[kh][g >> 1]);
+            const u32x2 v2 = {w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
+            *reinterpret_cast<u32x2*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + g) << 3))) = v2;
           }
+        // keep the scheduler from overlapping consecutive sub-blocks (their live ranges
+        // together exceed the 256 registers of two waves per SIMD)
+        __builtin_amdgcn_sched_barrier(0);
       };
-      if (live == KH) body(std::integral_constant<int, KH>{});
-      else if (KH > 1 && live == 1) body(std::integral_constant<int, 1>{});
+      using TT = std::true_type;
+      using FF = std::false_type;
+      // per wave and sub-block: only the sub-block whose 32 queries overlap the wave's keys
+      // (the causal diagonal) or a ragged key end needs the masked path
+      const bool mask_j = need_mask && ((kw0 + 32 * KH > a.S) || (a.causal && kw0 + 32 * KH - 1 > qj0 + off));
+      if (live == KH) {
+        if (mask_j) body(std::integral_constant<int, KH>{}, TT{});
+        else body(std::integral_constant<int, KH>{}, FF{});
+      } else if (KH > 1 && live == 1) {
+        body(std::integral_constant<int, 1>{}, TT{});
+      }
     }
     __syncthreads();
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
@@ -697,13 +749,15 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       // dQ^T tile = K^T dS^T (query on the lane), dumped as a coalesced fragment-order block
       // (attn_dq_reduce_frag_kernel reads it back)
       f32x16 acc = zero16();
+      // key rows 16 ks + 8 hh + tq (+4): the 16 ks steps are additions (see fq above)
+      const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
+      const int sa0 = IS::off(8 * hh + tq, qc), sa4 = IS::off(8 * hh + tq + 4, qc);
+      const int ka0 = I::off(8 * hh + tq, dc), ka4 = I::off(8 * hh + tq + 4, dc);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         if (ks >= ks_end) break;
-        const int kr0 = ks * 16 + 8 * hh + tq;
-        const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
-        const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
-        const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
+        const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
+        const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
       }
       uint16_t* blk = a.dq_acc + (kb - a.kb0) * a.slab +
@@ -849,7 +903,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   f32x16 acc[NDB];  // dV^T (wave A) or dK^T (wave B) of the group's 32 keys
 #pragma unroll
   for (int db = 0; db < NDB; ++db) acc[db] = zero16();
-  const float inv_scale = 1.f / a.scale, c2 = a.scale_log2;
+  const float c2 = a.scale_log2;
   const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
   const int nqb = (a.T + BQ - 1) / BQ;
   int qb_start = 0;
@@ -907,12 +961,13 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     }
     if (tid < 2 * BQ) {
       const bool live = q0 + (tid & (BQ - 1)) < a.T;
-      rowc[tid] = live ? (tid < BQ ? -rc * inv_scale : -rc) : 0.f;
+      rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : rc) : 0.f;  // -lse*log2(e), delta
     }
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 
-    const bool need_mask = (q0 + BQ > a.T) || (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
+    // rows past T need no mask (zero-filled Q / dO rows, row constants 0: see attn_bwd_kernel)
+    const bool need_mask = (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
       const int qj0 = q0 + 32 * j;
@@ -924,28 +979,36 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       // sub-block j finish before it reaches barrier j + 1, after which A rewrites the buffer)
       float* pxj = px + ((j & 1) * C::NG + grp) * 16 * 64;
       if (live) {
-        // S' = Q K^T - lse/scale (wave A) or dP' = dO V^T - delta (wave B), key on the lane
-        const int rbase = roleA ? 0 : BQ;
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[rbase + 32 * j + 8 * g + 4 * hh]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) x[4 * g + e] = rs[e];
-        }
+        // S = Q K^T (wave A) or dP = dO V^T (wave B), key on the lane
+        x = zero16();
         const uint16_t* Al = roleA ? Ql : Ol;
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) x = mfma32(as_frag(ld16(Al + I::off(32 * j + r, 16 * ks + 8 * hh))), kvf[ks], x);
         if (roleA) {
-          const int key = kw0 + r;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            float p = fast_exp2(c2 * x[i]);
-            if (need_mask) {
-              const int q = qj0 + acc_row(i, hh);
-              if (q >= a.T || key >= a.S || (a.causal && key > q + off)) p = 0.f;
+          // P = exp2(S c2 - lse log2e); the mask is a compile-time property of the code path (a
+          // uniform run-time test per element compiles to a branch per exponential)
+          auto expo = [&](auto mask_c) {
+            constexpr bool MASKED = decltype(mask_c)::value;
+            int lo = 0;
+            if constexpr (MASKED) {
+              const int key = kw0 + r;
+              lo = key >= a.S ? 64 : (a.causal ? key - off - (qj0 + 4 * hh) : -64);
             }
-            x[i] = p;
-          }
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+              const f32x4 rs = *reinterpret_cast<const f32x4*>(&rowc[32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int i = 4 * g + e;
+                float p = fast_exp2(__builtin_fmaf(x[i], c2, rs[e]));
+                if constexpr (MASKED) p = acc_row(i, 0) < lo ? 0.f : p;
+                x[i] = p;
+              }
+            }
+          };
+          // only the group's diagonal sub-block (or a ragged key end) needs the masked path
+          if (need_mask && ((kw0 + 32 > a.S) || (a.causal && kw0 + 31 > qj0 + off))) expo(std::true_type{});
+          else expo(std::false_type{});
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4)
             *reinterpret_cast<f32x4*>(pxj + (q4 * 64 + lane) * 4) =
@@ -961,20 +1024,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       __syncthreads();  // P of sub-block j handed over
       if (live) {
         if (!roleA) {
-          // dS = P * dP' (unscaled); P read back in the same accumulator layout
+          // dS = P (dP - delta) (unscaled); P read back in the same accumulator layout
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
             const f32x4 p4 = *reinterpret_cast<const f32x4*>(pxj + (q4 * 64 + lane) * 4);
+            const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * q4 + 4 * hh]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) x[4 * q4 + e] *= p4[e];
+            for (int e = 0; e < 4; ++e) x[4 * q4 + e] = (x[4 * q4 + e] - rd[e]) * p4[e];
           }
           f0 = pack_frag(x, 0);
           f1 = pack_frag(x, 1);
+          // dS^T image from the packed fragments (dwords 2(g&1), 2(g&1)+1 of f[g/2])
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
-            u32x2 v2;
-            v2[0] = pack_bf16x2(x[4 * g], x[4 * g + 1]);
-            v2[1] = pack_bf16x2(x[4 * g + 2], x[4 * g + 3]);
+            const u32x4 w4 = __builtin_bit_cast(u32x4, g < 2 ? f0 : f1);
+            const u32x2 v2 = {w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
             *reinterpret_cast<u32x2*>(Sl + IS::off(grp * 32 + r, 32 * j + 8 * g + 4 * hh)) = v2;
           }
         }
