@@ -95,6 +95,33 @@ PLLM_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, 
   hi = pack8(o2);
 }
 
+// Row-per-lane epilogue of 32x32 accumulator tiles (guide T21): acc[db] holds, for the lane's
+// row, columns db*32 + 8g + 4hh + e (e < 4), the two half-waves sharing each row.  Packs to
+// bf16 (times sc), swaps group pairs (k, k+1) across the half-waves with v_permlane32_swap and
+// stores one contiguous 16-B chunk per pair: 2*NDB dwordx4 stores instead of 4*NDB dwordx2 (the
+// store tail is issue-bound, per instruction).  row: 16-B aligned.
+template <int NDB>
+PLLM_DEV void store_row_bf16(uint16_t* row, const f32x16 (&acc)[NDB], float sc, int hh) {
+  u32x2 pk[4 * NDB];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      pk[4 * db + g][0] = pack_bf16x2(acc[db][4 * g] * sc, acc[db][4 * g + 1] * sc);
+      pk[4 * db + g][1] = pack_bf16x2(acc[db][4 * g + 2] * sc, acc[db][4 * g + 3] * sc);
+    }
+#pragma unroll
+  for (int k = 0; k < 4 * NDB; k += 2) {
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][d], pk[k + 1][d], false, false);
+      pk[k][d] = sw[0];
+      pk[k + 1][d] = sw[1];
+    }
+    *reinterpret_cast<u32x4*>(row + 8 * k + 8 * hh) = u32x4{pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]};
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Swizzled LDS image of a [rows][W] bf16 tile (W = 32, 64 or 128 elements).
 // Chunk ch (16 B) of row r lives at chunk position ch ^ f(r):
@@ -353,17 +380,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     const float lt = l[j] + __shfl_xor(l[j], 32, 64);
     if (qi < a.T) {
       const float inv = lt > 0.f ? 1.f / lt : 0.f;
-      uint16_t* op = a.o + b * a.o_sb + (int64_t)qi * a.o_st + (int64_t)h * a.o_sh;
-#pragma unroll
-      for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          u32x2 v2;
-          v2[0] = pack_bf16x2(o[j][db][4 * g] * inv, o[j][db][4 * g + 1] * inv);
-          v2[1] = pack_bf16x2(o[j][db][4 * g + 2] * inv, o[j][db][4 * g + 3] * inv);
-          *reinterpret_cast<u32x2*>(op + db * 32 + 8 * g + 4 * hh) = v2;
-        }
-      }
+      store_row_bf16<NDB>(a.o + b * a.o_sb + (int64_t)qi * a.o_st + (int64_t)h * a.o_sh, o[j], inv, hh);
       if (hh == 0 && a.lse)
         a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m[j] * c2 + log2f(lt)) * 0.69314718055994531f;
     }
@@ -558,6 +575,26 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   // dQ task of this wave in each iteration: (query sub-block, d-block)
   constexpr int NTASK = NQB * NDB;
 
+  // dQ fragment blocks of an iteration are STORED one iteration late, right after the next
+  // iteration's Q/dO staging: vmcnt counts stores too (gfx9 has no separate store counter), so
+  // stores issued at the end of an iteration would make the next iteration's first wait (for the
+  // prefetched Q/dO) wait out their latency as well (same-box A/B: neutral at the GPT-2 / llama
+  // shapes, where that latency was already covered).
+  constexpr int NTPW = (NTASK + C::NW - 1) / C::NW;
+  u32x4 dqv[NTPW][2];
+  uint16_t* dqp[NTPW];
+#pragma unroll
+  for (int i = 0; i < NTPW; ++i) dqp[i] = nullptr;
+  auto flush_dq = [&]() {
+#pragma unroll
+    for (int i = 0; i < NTPW; ++i)
+      if (dqp[i] != nullptr) {
+        st16(dqp[i], dqv[i][0]);
+        st16(dqp[i] + 8, dqv[i][1]);
+        dqp[i] = nullptr;
+      }
+  };
+
   // Per-lane LDS element offsets with the swizzle applied once.  Every image's f(row) depends
   // only on row bits 0..3, so row steps of 16 / 32 are plain additions (instruction immediates),
   // and column-chunk steps are XORs into the chunk bits:
@@ -583,6 +620,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     // stores instead of being hoisted out of the loop as 16 live registers
     int fs = fs0;
     asm volatile("" : "+v"(fs));
+    // every path waits here for the prefetch (and the previous dQ stores, an iteration old): a
+    // wait left inside the staging branches made hipcc assume loads still in flight at the
+    // join and wait vmcnt(0) again before the next prefetch -- on the fresh dQ stores
+    vm_wait_all();
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done
 #pragma unroll
     for (int i = 0; i < 2 * QPAIR; i += 2) {
@@ -602,6 +643,7 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
       const bool live = q0 + (tid & (BQ - 1)) < a.T;
       rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
     }
+    flush_dq();
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 
@@ -739,7 +781,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
     // this pass's fp32 slab of the key block.
-    for (int task = w; task < NTASK; task += C::NW) {
+#pragma unroll
+    for (int ti = 0; ti < NTPW; ++ti) {
+      const int task = __builtin_amdgcn_readfirstlane(w) + ti * C::NW;
+      if (task >= NTASK) break;
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
       if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
@@ -760,18 +805,19 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
         const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
       }
-      uint16_t* blk = a.dq_acc + (kb - a.kb0) * a.slab +
-                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
       float lo[8], hi[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         lo[e] = acc[e];
         hi[e] = acc[8 + e];
       }
-      st16(blk, pack8(lo));
-      st16(blk + 8, pack8(hi));
+      dqv[ti][0] = pack8(lo);
+      dqv[ti][1] = pack8(hi);
+      dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
+                ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
     }
   }
+  flush_dq();
   // write dK (scaled) and dV for this lane's keys; with RoPE, dK is rotated back (R^T): the
   // lane's d-blocks db and db + NDB/2 hold the partner elements i and i + D/2
 #pragma unroll
@@ -792,21 +838,8 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
           dk[kh][db + NDB / 2][i] = y * c - x * sn;
         }
     }
-    uint16_t* dkp = a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh;
-    uint16_t* dvp = a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh;
-#pragma unroll
-    for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        u32x2 k2, v2;
-        k2[0] = pack_bf16x2(dk[kh][db][4 * g] * a.scale, dk[kh][db][4 * g + 1] * a.scale);
-        k2[1] = pack_bf16x2(dk[kh][db][4 * g + 2] * a.scale, dk[kh][db][4 * g + 3] * a.scale);
-        v2[0] = pack_bf16x2(dv[kh][db][4 * g], dv[kh][db][4 * g + 1]);
-        v2[1] = pack_bf16x2(dv[kh][db][4 * g + 2], dv[kh][db][4 * g + 3]);
-        *reinterpret_cast<u32x2*>(dkp + db * 32 + 8 * g + 4 * hh) = k2;
-        *reinterpret_cast<u32x2*>(dvp + db * 32 + 8 * g + 4 * hh) = v2;
-      }
-    }
+    store_row_bf16<NDB>(a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh, dk[kh], a.scale, hh);
+    store_row_bf16<NDB>(a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh, dv[kh], 1.f, hh);
   }
 }
 
@@ -940,10 +973,31 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   };
 
   constexpr int NTASK = NQB * NDB;
+
+  // dQ fragment blocks of an iteration are STORED one iteration late, right after the next
+  // iteration's Q/dO staging: vmcnt counts stores too (gfx9 has no separate store counter), so
+  // stores issued at the end of an iteration would make the next iteration's first wait (for the
+  // prefetched Q/dO) wait out their latency as well (same-box A/B: neutral at the GPT-2 / llama
+  // shapes, where that latency was already covered).
+  constexpr int NTPW = (NTASK + C::NW - 1) / C::NW;
+  u32x4 dqv[NTPW][2];
+  uint16_t* dqp[NTPW];
+#pragma unroll
+  for (int i = 0; i < NTPW; ++i) dqp[i] = nullptr;
+  auto flush_dq = [&]() {
+#pragma unroll
+    for (int i = 0; i < NTPW; ++i)
+      if (dqp[i] != nullptr) {
+        st16(dqp[i], dqv[i][0]);
+        st16(dqp[i] + 8, dqv[i][1]);
+        dqp[i] = nullptr;
+      }
+  };
   if (total > 0) gload(0);
   for (int it = 0; it < total; ++it) {
     const int h = hk * G + it / per_head;
     const int q0 = (qb_start + it % per_head) * BQ;
+    vm_wait_all();  // prefetch landed on every path (see attn_bwd_kernel)
     __syncthreads();  // previous iteration's readers of Q / dO / dS^T are done
 #pragma unroll
     for (int i = 0; i < 2 * QPAIR; i += 2) {
@@ -963,6 +1017,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       const bool live = q0 + (tid & (BQ - 1)) < a.T;
       rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : rc) : 0.f;  // -lse*log2(e), delta
     }
+    flush_dq();
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
 
@@ -1057,7 +1112,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     }
     __syncthreads();
     // dQ partial of this key block: one (query sub-block, d-block) task per wave
-    for (int task = w; task < NTASK; task += C::NW) {
+#pragma unroll
+    for (int ti = 0; ti < NTPW; ++ti) {
+      const int task = __builtin_amdgcn_readfirstlane(w) + ti * C::NW;
+      if (task >= NTASK) break;
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
       if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
@@ -1076,18 +1134,19 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
         const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
         dqa = mfma32(Bf, A, dqa);
       }
-      uint16_t* blk = a.dq_acc + (kb - a.kb0) * a.slab +
-                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
       float lo[8], hi[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         lo[e] = dqa[e];
         hi[e] = dqa[8 + e];
       }
-      st16(blk, pack8(lo));
-      st16(blk + 8, pack8(hi));
+      dqv[ti][0] = pack8(lo);
+      dqv[ti][1] = pack8(hi);
+      dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
+                ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
     }
   }
+  flush_dq();
   // dV (wave A) / dK scaled and rotated back (wave B) for this lane's key
   const int key = kw0 + r;
   if (key >= a.S) return;
@@ -1108,16 +1167,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   const float sc = roleA ? 1.f : a.scale;
   uint16_t* dst = roleA ? a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh
                         : a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh;
-#pragma unroll
-  for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      u32x2 v2;
-      v2[0] = pack_bf16x2(acc[db][4 * g] * sc, acc[db][4 * g + 1] * sc);
-      v2[1] = pack_bf16x2(acc[db][4 * g + 2] * sc, acc[db][4 * g + 3] * sc);
-      *reinterpret_cast<u32x2*>(dst + db * 32 + 8 * g + 4 * hh) = v2;
-    }
-  }
+  store_row_bf16<NDB>(dst, acc, sc, hh);
 }
 
 // Reduce of the backward kernels' fragment-order dQ slabs.  One workgroup (64 x D/32 threads) per
