@@ -613,9 +613,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
   // per SIMD' item 4)
   if (C::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(1);
   if (total > 0) gload(0);
-  for (int it = 0; it < total; ++it) {
-    const int h = hk * G + it / per_head;
-    const int q0 = (qb_start + it % per_head) * BQ;
+  // (head, query block) of iteration it, advanced incrementally (no integer division per step)
+  int h = hk * G, qbi = qb_start;
+  for (int it = 0; it < total; ++it, (++qbi == nqb) ? (qbi = qb_start, ++h) : 0) {
+    const int q0 = qbi * BQ;
     // opaque per iteration: the (j, g) store offsets derived from it are formed next to their
     // stores instead of being hoisted out of the loop as 16 live registers
     int fs = fs0;
@@ -973,6 +974,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   };
 
   constexpr int NTASK = NQB * NDB;
+  // per-lane LDS element offsets, swizzle applied once (see attn_bwd_kernel): fragment reads
+  // fq ^ (ks << 4) + 32 j D, transposed reads ft0 / ft8 ^ (db << 5) + (32 j + 16 st) D, dS^T
+  // stores fs ^ ((4 j + g) << 3)
+  const int fq = I::off(r, 8 * hh);
+  const int ft0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
+  const int fs0 = IS::off(grp * 32 + r, 4 * hh);
 
   // dQ fragment blocks of an iteration are STORED one iteration late, right after the next
   // iteration's Q/dO staging: vmcnt counts stores too (gfx9 has no separate store counter), so
@@ -994,9 +1001,12 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       }
   };
   if (total > 0) gload(0);
-  for (int it = 0; it < total; ++it) {
-    const int h = hk * G + it / per_head;
-    const int q0 = (qb_start + it % per_head) * BQ;
+  // (head, query block) of iteration it, advanced incrementally (no integer division per step)
+  int h = hk * G, qbi = qb_start;
+  for (int it = 0; it < total; ++it, (++qbi == nqb) ? (qbi = qb_start, ++h) : 0) {
+    const int q0 = qbi * BQ;
+    int fs = fs0;
+    asm volatile("" : "+v"(fs));
     vm_wait_all();  // prefetch landed on every path (see attn_bwd_kernel)
     __syncthreads();  // previous iteration's readers of Q / dO / dS^T are done
 #pragma unroll
@@ -1035,15 +1045,21 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       float* pxj = px + ((j & 1) * C::NG + grp) * 16 * 64;
       if (live) {
         // S = Q K^T (wave A) or dP = dO V^T (wave B), key on the lane
-        x = zero16();
         const uint16_t* Al = roleA ? Ql : Ol;
+        auto chain = [&]() {
+          x = zero16();
 #pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) x = mfma32(as_frag(ld16(Al + I::off(32 * j + r, 16 * ks + 8 * hh))), kvf[ks], x);
+          for (int ks = 0; ks < NKS; ++ks) x = mfma32(as_frag(ld16(Al + 32 * j * D + (fq ^ (ks << 4)))), kvf[ks], x);
+        };
+        if (!roleA) chain();
         if (roleA) {
           // P = exp2(S c2 - lse log2e); the mask is a compile-time property of the code path (a
-          // uniform run-time test per element compiles to a branch per exponential)
+          // uniform run-time test per element compiles to a branch per exponential) and each
+          // path carries its own MFMA chain (small paths were if-converted into one that always
+          // paid the compare + select)
           auto expo = [&](auto mask_c) {
             constexpr bool MASKED = decltype(mask_c)::value;
+            chain();
             int lo = 0;
             if constexpr (MASKED) {
               const int key = kw0 + r;
@@ -1074,7 +1090,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       } else if (!roleA) {
 #pragma unroll
         for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<u32x2*>(Sl + IS::off(grp * 32 + r, 32 * j + 8 * g + 4 * hh)) = u32x2{0u, 0u};
+          *reinterpret_cast<u32x2*>(Sl + (fs ^ ((4 * j + g) << 3))) = u32x2{0u, 0u};
       }
       __syncthreads();  // P of sub-block j handed over
       if (live) {
@@ -1094,7 +1110,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
           for (int g = 0; g < 4; ++g) {
             const u32x4 w4 = __builtin_bit_cast(u32x4, g < 2 ? f0 : f1);
             const u32x2 v2 = {w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
-            *reinterpret_cast<u32x2*>(Sl + IS::off(grp * 32 + r, 32 * j + 8 * g + 4 * hh)) = v2;
+            *reinterpret_cast<u32x2*>(Sl + (fs ^ ((4 * j + g) << 3))) = v2;
           }
         }
         // dV^T += dO^T P (A) / dK^T += Q^T dS (B): A operands by transposed reads
@@ -1103,8 +1119,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
         for (int db = 0; db < NDB; ++db) {
 #pragma unroll
           for (int st = 0; st < 2; ++st) {
-            const int rowq = 32 * j + st * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
-            const bf16x8 tA = cat_tr(ds_tr(Tl + I::off(rowq, col)), ds_tr(Tl + I::off(rowq + 8, col)));
+            const int rb = (32 * j + 16 * st) * D;
+            const bf16x8 tA = cat_tr(ds_tr(Tl + rb + (ft0 ^ (db << 5))), ds_tr(Tl + rb + (ft8 ^ (db << 5))));
             acc[db] = mfma32(tA, st == 0 ? f0 : f1, acc[db]);
           }
         }
@@ -1125,13 +1141,14 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       // per lane, dumped as one contiguous 2-KiB fragment-order block (two 16-B stores per lane,
       // coalesced) that attn_dq_reduce_frag_kernel reads back by (query, head-dim) position
       f32x16 dqa = zero16();
+      const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
+      const int sa0 = IS::off(8 * hh + tq, qc), sa4 = IS::off(8 * hh + tq + 4, qc);
+      const int ka0 = I::off(8 * hh + tq, dc), ka4 = I::off(8 * hh + tq + 4, dc);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         if (ks >= ks_end) break;
-        const int kr0 = ks * 16 + 8 * hh + tq;
-        const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
-        const bf16x8 A = cat_tr(ds_tr(Sl + IS::off(kr0, qc)), ds_tr(Sl + IS::off(kr0 + 4, qc)));
-        const bf16x8 Bf = cat_tr(ds_tr(Kl + I::off(kr0, dc)), ds_tr(Kl + I::off(kr0 + 4, dc)));
+        const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
+        const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         dqa = mfma32(Bf, A, dqa);
       }
       float lo[8], hi[8];
