@@ -35,7 +35,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--only", default="", help="fwd|bwd: run only our kernel (for profiling)")
     ap.add_argument("--rope-ab", action="store_true", help="our fwd/bwd with vs without fused RoPE tables")
-    ap.add_argument("--variants", default="", help="comma list of backward tiling variants to A/B (attn_bwd_set_variant)")
+    ap.add_argument("--ours", action="store_true", help="time only the HIP kernels (fwd_us / bwd_us), no SDPA")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
@@ -76,19 +76,12 @@ def main():
             res["prepass_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
             print(json.dumps(res), flush=True)
             continue
-        if args.variants:
-            outs, res = {}, {"cfg": cfg}
-            for vv in (int(x) for x in args.variants.split(",")):
-                torch.ops.pllm.attn_bwd_set_variant(vv)
-                ts = [1e6 * timeit(ours_b) for _ in range(args.rounds)]
-                outs[vv] = [t.float().clone() for t in (dq, dk, dv)]
-                res[f"bwd_v{vv}_us"] = ts
-                res[f"bwd_v{vv}_tflops"] = 2.5 * 2 * 2 * B * H * T * T * D / 2 / (min(ts) * 1e-6) / 1e12
-            v0 = min(outs)
-            for vv, o_ in outs.items():
-                res[f"v{vv}_max_rel_diff_vs_v{v0}"] = max(((a - b).norm() / b.norm()).item()
-                                                          for a, b in zip(o_, outs[v0]))
-            torch.ops.pllm.attn_bwd_set_variant(0)  # the default (D<=64: V 0, D=128: V 1)
+        if args.ours:
+            flops_f = 2 * 2 * B * H * T * T * D / 2
+            res = {"cfg": cfg, "fwd_us": [1e6 * timeit(ours_f) for _ in range(args.rounds)],
+                   "bwd_us": [1e6 * timeit(ours_b) for _ in range(args.rounds)]}
+            res["fwd_tflops"] = flops_f / (min(res["fwd_us"]) * 1e-6) / 1e12
+            res["bwd_tflops"] = 2.5 * flops_f / (min(res["bwd_us"]) * 1e-6) / 1e12
             print(json.dumps(res), flush=True)
             continue
         if args.only:

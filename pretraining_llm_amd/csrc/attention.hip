@@ -416,24 +416,25 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
   if (row < nrows && c == 0) a.delta[((int64_t)b * a.H + h) * a.T + t] = acc;
 }
 
-// Backward tiling.  NW waves per workgroup, each owning 32 keys (BK = 32*NW keys per
-// workgroup); BQ query rows per iteration processed as NQB sub-blocks of 32.
-//   D <= 64, V 0: 8 waves, 256 keys, 128 queries per iteration (two waves per SIMD).
-//            V 1: 4 waves, 128 keys, 64 queries: 48 KiB of LDS, two workgroups per CU.
-//   D = 128, V 1 / 2: 4 waves, 128 keys, 64 / 128 queries per iteration (one wave per SIMD).
-// KH (32-key halves per wave) is kept as a parameter of the code: 4 waves x 64 keys (KH = 2,
-// one wave per SIMD, every Q/dO fragment feeding two MFMAs) measured 24-33 % SLOWER than V 0
-// at every D = 64 shape (profiles/r2_attn_bwd_variants.jsonl), so every variant uses KH = 1.
+// Fused-role backward tiling (D = 32 / 64; D = 128 runs the role-split kernel below): 8 waves
+// (two per SIMD), each owning 32 keys (BK = 256 keys per workgroup); BQ = 128 query rows per
+// iteration as NQB = 4 sub-blocks of 32.  KH (32-key halves per wave) stays a parameter of the
+// code.  Measured and removed (same-box A/B, profiles/r2_attn_bwd_removed_variants_ab.jsonl):
+//   * 4 waves x 64 keys (KH = 2, one wave per SIMD): 13-19 % slower at D = 64;
+//   * 4 waves x 128 keys x 64 queries (48 KiB LDS, two workgroups per CU): 7-15 % slower;
+//   * the role-split kernel at D = 64: 28-49 % slower;
+//   * fused-role D = 128 (4 waves, one per SIMD, 64 / 128 queries): 19-26 % slower than role split.
 constexpr float kLog2e = 1.4426950408889634f;
 
-template <int D, int V = 0>
+template <int D>
 struct BwdCfg {
+  static_assert(D == 32 || D == 64, "fused-role backward: D = 32 / 64");
   static constexpr int KH = 1;
-  static constexpr int NW = (D <= 64 && V == 0) ? 8 : 4;
+  static constexpr int NW = 8;
   static constexpr int NT = 64 * NW;
   static constexpr int BK = 32 * KH * NW;
-  static constexpr int BQ = D <= 64 ? (V == 0 ? 128 : 64) : (32 << V);
-  static constexpr int MIN_WAVES = D == 128 ? 1 : 2;
+  static constexpr int BQ = 128;
+  static constexpr int MIN_WAVES = 2;
   static constexpr int NQB = BQ / 32;
   static constexpr int CPR = D / 8;
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;
@@ -446,9 +447,9 @@ struct BwdCfg {
 // bf16 dQ.  fp32 slabs (no partial rounding) measured +12 % (T 1024, D 64) to +34 % (T 4096)
 // on the whole backward: the slab bytes are its second cost after the MFMAs.
 // ROPE: q and k are rotated while staged, dk is rotated back before its store (dq in the reduce).
-template <int D, int V, int ROPE>
-__global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
-  using C = BwdCfg<D, V>;
+template <int D, int ROPE>
+__global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
+  using C = BwdCfg<D>;
   using I = Img<D>;
   using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
   constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR, KH = C::KH;
@@ -828,16 +829,29 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
     if (ROPE != 0) {
       const float* cr = a.rope_cos + (int64_t)key * (D / 2);
       const float* sr = a.rope_sin + (int64_t)key * (D / 2);
+      if constexpr (NDB >= 2) {
 #pragma unroll
-      for (int db = 0; db < NDB / 2; ++db)
+        for (int db = 0; db < NDB / 2; ++db)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int d = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+          for (int i = 0; i < 16; ++i) {
+            const int d = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+            const float c = cr[d], sn = sr[d];
+            const float x = dk[kh][db][i], y = dk[kh][db + NDB / 2][i];
+            dk[kh][db][i] = x * c + y * sn;
+            dk[kh][db + NDB / 2][i] = y * c - x * sn;
+          }
+      } else {
+        // D = 32: one d-block; element i (dim 8(i/4) + 4hh + i%4) pairs with element i + 8
+        // (dim + 16) of the same lane
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int d = 8 * (i >> 2) + 4 * hh + (i & 3);
           const float c = cr[d], sn = sr[d];
-          const float x = dk[kh][db][i], y = dk[kh][db + NDB / 2][i];
-          dk[kh][db][i] = x * c + y * sn;
-          dk[kh][db + NDB / 2][i] = y * c - x * sn;
+          const float x = dk[kh][0][i], y = dk[kh][0][i + 8];
+          dk[kh][0][i] = x * c + y * sn;
+          dk[kh][0][i + 8] = y * c - x * sn;
         }
+      }
     }
     store_row_bf16<NDB>(a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh, dk[kh], a.scale, hh);
     store_row_bf16<NDB>(a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh, dv[kh], 1.f, hh);
@@ -856,9 +870,10 @@ __global__ __launch_bounds__((BwdCfg<D, V>::NT), (BwdCfg<D, V>::MIN_WAVES)) void
 // wave is balanced (S + dV vs dP + dK).  dQ as before: per-key-block bf16 slabs, one task per wave.
 template <int D>
 struct RsCfg {
+  static_assert(D == 128, "role-split backward: D = 128");
   static constexpr int NW = 8, NT = 512, NG = 4;  // waves, threads, key groups (wave pairs)
   static constexpr int BK = 32 * NG;               // 128 keys per workgroup
-  static constexpr int BQ = D <= 64 ? 128 : 64;    // queries per iteration (LDS: 112 KiB both)
+  static constexpr int BQ = 64;                    // queries per iteration (LDS: 112 KiB)
   static constexpr int NQB = BQ / 32;              // 32-query sub-blocks
   static constexpr int CPR = D / 8;
   static constexpr int PX = 2 * NG * 16 * 64;      // P hand-off: [sub-block][group][q4][lane] f32x4
@@ -1271,22 +1286,7 @@ namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-// backward variants: bit 0 = BwdCfg variant for D <= 64 (0 / 1), bit 2 = fused-role variant for
-// D = 128 (0 -> V 1, 1 -> V 2) when bit 3 is set, bit 3 = D = 128 runs the fused-role kernel instead
-// of the role-split one, bit 4 = D <= 64 runs the role-split kernel
-static int g_bwd_variant = 0;
-void attn_bwd_set_variant(int v) { g_bwd_variant = v & 29; }
-// role-split kernel: the default at D = 128 (bit 3 selects the fused-role V 1 / V 2 instead),
-// opt-in at D <= 64 (bit 4)
-static bool vrs(int D) { return D == 128 ? !((g_bwd_variant >> 3) & 1) : (D == 64 && ((g_bwd_variant >> 4) & 1)); }
-static int v64() { return g_bwd_variant & 1; }
-static int v128() { return 1 + ((g_bwd_variant >> 2) & 1); }
-
-int attn_bwd_key_block(int D) {
-  if (vrs(D)) return RsCfg<64>::BK;
-  if (D <= 64) return v64() ? BwdCfg<64, 1>::BK : BwdCfg<64, 0>::BK;
-  return BwdCfg<128, 1>::BK;  // 128 keys in every D = 128 variant
-}
+int attn_bwd_key_block(int D) { return D == 128 ? RsCfg<128>::BK : BwdCfg<64>::BK; }
 
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
@@ -1295,20 +1295,20 @@ static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
 }
 
-template <int D, int V, int ROPE>
+template <int D, int ROPE>
 static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
-  const int nkb = (a.S + BwdCfg<D, V>::BK - 1) / BwdCfg<D, V>::BK;
+  const int nkb = (a.S + BwdCfg<D>::BK - 1) / BwdCfg<D>::BK;
   hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   // key blocks in passes of at most a.nkb_pass (bounded slab workspace)
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {
     a.kb0 = kb0;
     a.nkb_pass = min(per, nkb - kb0);
-    hipLaunchKernelGGL((attn_bwd_kernel<D, V, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(BwdCfg<D, V>::NT), 0, st,
+    hipLaunchKernelGGL((attn_bwd_kernel<D, ROPE>), dim3(a.nkb_pass * a.B * a.Hkv), dim3(BwdCfg<D>::NT), 0, st,
                        a);
-    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, BwdCfg<D, V>::BK, ROPE>), dim3(a.B * a.H * a.nqt),
+    hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, BwdCfg<D>::BK, ROPE>), dim3(a.B * a.H * a.nqt),
                        dim3(64 * (D / 32)), 0, st, a);
     a.nkb_pass = per;
   }
@@ -1316,11 +1316,11 @@ static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
 
 // RoPE mode: 0 none, 1 rotate q / k inputs and dq / dk outputs, 2 inputs already rotated (the
 // caller's pre-pass), rotate the outputs back only
-template <int D, int V>
+template <int D>
 static void attn_bwd_r(const AttnBwdArgs& a, hipStream_t st) {
-  if (!a.rope_cos) attn_bwd_t<D, V, 0>(a, st);
-  else if (a.rope_in) attn_bwd_t<D, V, 1>(a, st);
-  else attn_bwd_t<D, V, 2>(a, st);
+  if (!a.rope_cos) attn_bwd_t<D, 0>(a, st);
+  else if (a.rope_in) attn_bwd_t<D, 1>(a, st);
+  else attn_bwd_t<D, 2>(a, st);
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
@@ -1354,15 +1354,11 @@ static void attn_bwd_rs_r(const AttnBwdArgs& a, hipStream_t st) {
   else attn_bwd_rs_t<D, 2>(a, st);
 }
 
+// D = 32 / 64: fused-role kernel; D = 128: role-split kernel
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
-  if (vrs(a.D)) {  // D = 64 / 128 (the fragment-order reduce pairs d-blocks: D >= 64)
-    if (a.D == 64) attn_bwd_rs_r<64>(a, st);
-    else attn_bwd_rs_r<128>(a, st);
-    return;
-  }
-  if (a.D == 32) v64() ? attn_bwd_r<32, 1>(a, st) : attn_bwd_r<32, 0>(a, st);
-  else if (a.D == 64) v64() ? attn_bwd_r<64, 1>(a, st) : attn_bwd_r<64, 0>(a, st);
-  else v128() == 1 ? attn_bwd_r<128, 1>(a, st) : attn_bwd_r<128, 2>(a, st);
+  if (a.D == 32) attn_bwd_r<32>(a, st);
+  else if (a.D == 64) attn_bwd_r<64>(a, st);
+  else attn_bwd_rs_r<128>(a, st);
 }
 
 }  // namespace pllm

@@ -145,7 +145,6 @@ void gemv(const GemvArgs& a, hipStream_t st);
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
-void attn_bwd_set_variant(int v);
 // attn_decode.hip: split-KV single-query attention over a KV cache
 bool attn_decode_supported(int D, int group);
 int attn_decode_splits(int B, int Hkv, int S_max);

@@ -3,7 +3,7 @@
 R="${GRAFT_REPO_ROOT:-/root/repo}"
 cd "$R"; mkdir -p gpurun_out
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-timeout -k 10 300 python bench/attn_bench.py --variants 0,2 --configs 8x16x2048x128,64x12x1024x64 --rounds 3 > gpurun_out/attn18.log 2>&1 || { echo "attn bench failed"; tail -20 gpurun_out/attn18.log; exit 3; }
+timeout -k 10 300 python bench/attn_bench.py --ours --configs 8x16x2048x128,64x12x1024x64 --rounds 3 > gpurun_out/attn18.log 2>&1 || { echo "attn bench failed"; tail -20 gpurun_out/attn18.log; exit 3; }
 grep -v amdgpu.ids gpurun_out/attn18.log | cut -c1-500
 for sh in gpt2 llama; do
   M=65536; [ $sh = llama ] && M=16384

@@ -815,18 +815,12 @@ def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
     assert _rel(W._pllm_gradbuf.double() - 1, 2 * Wf.grad.double()) < 3e-2
 
 
-def _bwd_variants(D):
-    # attn_bwd_set_variant encoding (csrc/attention.hip): D <= 64: 0 = V 0, 1 = V 1, 16 = role split;
-    # D = 128: 0 = role split, 8 = fused-role V 1, 12 = fused-role V 2
-    return [0, 1, 16] if D <= 64 else [0, 8, 12]
-
-
 @pytest.mark.parametrize("D,T,H,Hkv,B", [(32, 1024, 4, 4, 2), (64, 2048, 4, 2, 1), (64, 4096, 2, 2, 1),
                                          (128, 2048, 4, 1, 1), (128, 4096, 2, 2, 1), (64, 1000, 4, 4, 2)])
-def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
+def test_attention_bwd_long_sequences(D, T, H, Hkv, B):
     """Backward at the shipped sequence lengths (2048 / 4096, several key blocks and dQ slabs),
-    D = 32 / 64 / 128, GQA, ragged T, every tiling variant, vs fp32 torch; a forced multi-pass
-    run (bounded dQ workspace) is bit-identical to the single-pass one."""
+    D = 32 / 64 (fused-role kernel) and 128 (role-split kernel), GQA, ragged T, vs fp32 torch; a
+    forced multi-pass run (bounded dQ workspace) is bit-identical to the single-pass one."""
     torch.manual_seed(T + D)
     q = torch.randn(B, T, H, D, device=DEV).bfloat16()
     k = torch.randn(B, T, Hkv, D, device=DEV).bfloat16()
@@ -838,40 +832,31 @@ def test_attention_bwd_long_sequences_all_variants(D, T, H, Hkv, B):
     of, _ = _attn_ref(qf, kf, vf, True, scale)
     of.backward(do.float())
     try:
-        for var in _bwd_variants(D):
-            torch.ops.pllm.attn_bwd_set_variant(var)
-            dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
-            torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, dq, dk, dv, True, scale)
-            for a, b, n in ((dq, qf.grad, "dq"), (dk, kf.grad, "dk"), (dv, vf.grad, "dv")):
-                assert _rel(a, b) < 2e-2, (var, n, _rel(a, b))
-        torch.ops.pllm.attn_bwd_set_variant(0)
         ref = [torch.empty_like(t) for t in (q, k, v)]
         torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *ref, True, scale)
+        for a, b, n in zip(ref, (qf.grad, kf.grad, vf.grad), ("dq", "dk", "dv")):
+            assert _rel(a, b) < 2e-2, (n, _rel(a, b))
         torch.ops.pllm.attn_bwd_set_workspace_mb(1e-3)  # one key block per pass
         got = [torch.empty_like(t) for t in (q, k, v)]
         torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *got, True, scale)
         for a, b in zip(got, ref):
             assert torch.equal(a, b)
     finally:
-        torch.ops.pllm.attn_bwd_set_variant(0)
         torch.ops.pllm.attn_bwd_set_workspace_mb(4096)
 
 
-@pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1)])
-@pytest.mark.parametrize("variant", [0, 8, 16])
+@pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 2), (64, 1), (32, 2)])
 @pytest.mark.parametrize("prepass", [True, False])
-def test_attention_fused_rope_fwd_bwd(D, Hkv, variant, prepass):
+def test_attention_fused_rope_fwd_bwd(D, Hkv, prepass):
     """RoPE with the HIP attention == rotate-half RoPE + attention in fp32 torch, gradients
     w.r.t. the UNROTATED packed qkv: pre-pass (rope_qk once, backward rotates dq/dk back while
-    storing them) and in-kernel rotation (q/k rotated while staged), every backward variant."""
+    storing them) and in-kernel rotation (q/k rotated while staged)."""
     from pretraining_llm_amd import ops
-    torch.ops.pllm.attn_bwd_set_variant(variant)
     old = ops._ROPE_PREPASS
     ops._ROPE_PREPASS = prepass
     try:
         _rope_case(D, Hkv)
     finally:
-        torch.ops.pllm.attn_bwd_set_variant(0)
         ops._ROPE_PREPASS = old
 
 
