@@ -873,10 +873,10 @@ struct RsCfg {
   static_assert(D == 128, "role-split backward: D = 128");
   static constexpr int NW = 8, NT = 512, NG = 4;  // waves, threads, key groups (wave pairs)
   static constexpr int BK = 32 * NG;               // 128 keys per workgroup
-  static constexpr int BQ = 64;                    // queries per iteration (LDS: 112 KiB)
+  static constexpr int BQ = 128;                   // queries per iteration (LDS: 145 KiB)
   static constexpr int NQB = BQ / 32;              // 32-query sub-blocks
   static constexpr int CPR = D / 8;
-  static constexpr int PX = 2 * NG * 16 * 64;      // P hand-off: [sub-block][group][q4][lane] f32x4
+  static constexpr int PX = 2 * NG * 2 * 64 * 4;   // P hand-off (dwords): [parity][group][half][lane] bf16x8
   static constexpr int LDS_ELEMS = BK * D + 2 * BQ * D + BK * BQ;  // bf16: K, Q, dO, dS^T images
 };
 
@@ -888,7 +888,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
-  __shared__ __attribute__((aligned(16))) float px[C::PX];
+  __shared__ __attribute__((aligned(16))) uint32_t px[C::PX];
   __shared__ __attribute__((aligned(16))) float rowc[2 * BQ];  // -lse/scale, -delta
   uint16_t* Kl = smem;
   uint16_t* Ql = smem + BK * D;
@@ -1055,9 +1055,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       const bool live = !a.causal || kw0 <= qj0 + 31 + off;
       f32x16 x;
       bf16x8 f0, f1;
-      // [q4][lane] f32x4 of this group; buffers alternate by sub-block parity (wave B's reads of
-      // sub-block j finish before it reaches barrier j + 1, after which A rewrites the buffer)
-      float* pxj = px + ((j & 1) * C::NG + grp) * 16 * 64;
+      // the packed bf16 P fragments of this group ([half][lane] 16 B: coalesced b128 accesses);
+      // buffers alternate by sub-block parity (wave B's reads of sub-block j finish before it
+      // reaches barrier j + 1, after which A rewrites the buffer).  B forms dS from this bf16 P,
+      // the same rounding of P that the dV product consumes.
+      uint32_t* pxj = px + ((j & 1) * C::NG + grp) * 2 * 64 * 4;
       if (live) {
         // S = Q K^T (wave A) or dP = dO V^T (wave B), key on the lane
         const uint16_t* Al = roleA ? Ql : Ol;
@@ -1095,12 +1097,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
           // only the group's diagonal sub-block (or a ragged key end) needs the masked path
           if (need_mask && ((kw0 + 32 > a.S) || (a.causal && kw0 + 31 > qj0 + off))) expo(std::true_type{});
           else expo(std::false_type{});
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4)
-            *reinterpret_cast<f32x4*>(pxj + (q4 * 64 + lane) * 4) =
-                f32x4{x[4 * q4], x[4 * q4 + 1], x[4 * q4 + 2], x[4 * q4 + 3]};
           f0 = pack_frag(x, 0);
           f1 = pack_frag(x, 1);
+          *reinterpret_cast<u32x4*>(pxj + lane * 4) = __builtin_bit_cast(u32x4, f0);
+          *reinterpret_cast<u32x4*>(pxj + (64 + lane) * 4) = __builtin_bit_cast(u32x4, f1);
         }
       } else if (!roleA) {
 #pragma unroll
@@ -1111,12 +1111,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       if (live) {
         if (!roleA) {
           // dS = P (dP - delta) (unscaled); P read back in the same accumulator layout
+          const u32x4 pw[2] = {*reinterpret_cast<const u32x4*>(pxj + lane * 4),
+                               *reinterpret_cast<const u32x4*>(pxj + (64 + lane) * 4)};
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
-            const f32x4 p4 = *reinterpret_cast<const f32x4*>(pxj + (q4 * 64 + lane) * 4);
             const f32x4 rd = *reinterpret_cast<const f32x4*>(&rowc[BQ + 32 * j + 8 * q4 + 4 * hh]);
 #pragma unroll
-            for (int e = 0; e < 4; ++e) x[4 * q4 + e] = (x[4 * q4 + e] - rd[e]) * p4[e];
+            for (int e = 0; e < 4; ++e) {
+              const int i = 4 * q4 + e;
+              const uint32_t wd = pw[i >> 3][(i & 7) >> 1];
+              x[i] = (x[i] - rd[e]) * ((i & 1) ? hi_bf(wd) : lo_bf(wd));
+            }
           }
           f0 = pack_frag(x, 0);
           f1 = pack_frag(x, 1);
