@@ -476,28 +476,17 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
-  // this lane's key rows (one per 32-key half) of K and V as B-operand fragments (k = head dim)
+  // this lane's key rows (one per 32-key half) of V as B-operand fragments (k = head dim); the K
+  // fragments are read back from the K image below (K crosses HBM / L2 once per workgroup)
   bf16x8 kf[KH][NKS], vf[KH][NKS];
 #pragma unroll
   for (int kh = 0; kh < KH; ++kh) {
     const int key = kw0 + 32 * kh + r;
-    u32x4 raw[NKS];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      raw[ks] = key < a.S ? ld16(kp + (int64_t)key * a.k_st + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
+    for (int ks = 0; ks < NKS; ++ks)
       vf[kh][ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
-    }
-    if (ROPE == 1 && key < a.S) {
-      const int64_t tab = (int64_t)key * (D / 2);
-#pragma unroll
-      for (int ks = 0; ks < NKS / 2; ++ks)
-        rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
-              1.f);
-    }
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) kf[kh][ks] = as_frag(raw[ks]);
   }
-  // whole (rotated) K block into LDS for the dQ product; a thread stages both RoPE partners
+  // whole (rotated) K block into LDS for the S and dQ products; a thread stages both RoPE partners
   constexpr int CPR2 = CPR / 2;
 #pragma unroll
   for (int i = 0; i < (BK * CPR2 + NT - 1) / NT; ++i) {
@@ -517,7 +506,15 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     }
   }
 
-  vm_wait_all();  // K/V fragments and the K image ready before the query loop (see common.h)
+  vm_wait_all();  // V fragments and the K image ready before the query loop (see common.h)
+  __syncthreads();
+  // K fragments of the lane's key rows from the (rotated) image: rows w*32*KH + 32 kh + r,
+  // the Q-fragment read pattern (fq below)
+#pragma unroll
+  for (int kh = 0; kh < KH; ++kh)
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      kf[kh][ks] = as_frag(ld16(Kl + (w * 32 * KH + 32 * kh) * D + (I::off(r, 8 * hh) ^ (ks << 4))));
   f32x16 dk[KH][NDB], dv[KH][NDB];
 #pragma unroll
   for (int kh = 0; kh < KH; ++kh)
@@ -910,25 +907,16 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
   const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
 
-  // this lane's key row of K (wave A, rotated with RoPE) or V (wave B) as B-operand fragments
+  // this lane's key row of V (wave B) as B-operand fragments; wave A reads its K fragments back
+  // from the (rotated) K image below, so K crosses HBM / L2 once per workgroup
   bf16x8 kvf[NKS];
-  {
+  if (!roleA) {
     const int key = kw0 + r;
-    u32x4 raw[NKS];
-    const uint16_t* src = roleA ? kp + (int64_t)key * a.k_st : vp + (int64_t)key * a.v_st;
+    const uint16_t* src = vp + (int64_t)key * a.v_st;
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) raw[ks] = key < a.S ? ld16(src + 16 * ks + 8 * hh) : u32x4{0u, 0u, 0u, 0u};
-    if (ROPE == 1 && roleA && key < a.S) {
-      const int64_t tab = (int64_t)key * (D / 2);
-#pragma unroll
-      for (int ks = 0; ks < NKS / 2; ++ks)
-        rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
-              1.f);
-    }
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) kvf[ks] = as_frag(raw[ks]);
+    for (int ks = 0; ks < NKS; ++ks) kvf[ks] = key < a.S ? as_frag(ld16(src + 16 * ks + 8 * hh)) : zero_frag();
   }
-  // whole (rotated) K block into LDS for the dQ product
+  // whole (rotated) K block into LDS for the S (wave A) and dQ products
   constexpr int CPR2 = CPR / 2;
 #pragma unroll
   for (int i = 0; i < (BK * CPR2 + NT - 1) / NT; ++i) {
@@ -948,6 +936,11 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     }
   }
   vm_wait_all();
+  __syncthreads();
+  if (roleA) {
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) kvf[ks] = as_frag(ld16(Kl + grp * 32 * D + (I::off(r, 8 * hh) ^ (ks << 4))));
+  }
 
   f32x16 acc[NDB];  // dV^T (wave A) or dK^T (wave B) of the group's 32 keys
 #pragma unroll
