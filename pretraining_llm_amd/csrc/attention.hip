@@ -263,6 +263,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     }
   };
 
+  // per-lane LDS element offsets with the swizzle applied once (see attn_bwd_kernel): K
+  // fragment reads fk ^ (ks << 4) + 32 kb D, V transposed reads fv0 / fv8 ^ (db << 5) + 16 kst D
+  const int g1 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
+  const int fk = I::off(r, 8 * hh);
+  const int fv0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), fv8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
   f32x16 o[QB][NDB];
   float m[QB], l[QB];  // m: running max of RAW scores (scale applied in the exponent)
 #pragma unroll
@@ -273,7 +278,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     l[j] = 0.f;
   }
   const float c2 = a.scale_log2;
-  const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
 
   if (ntiles > 0) {
     gload(0);
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
         for (int ks = 0; ks < NKS; ++ks) {
-          const bf16x8 kf = as_frag(ld16(Kb + I::off(kb * 32 + r, 16 * ks + 8 * hh)));
+          const bf16x8 kf = as_frag(ld16(Kb + kb * 32 * D + (fk ^ (ks << 4))));
 #pragma unroll
           for (int j = 0; j < QB; ++j)
             if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
@@ -311,13 +315,15 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
         const int qi = qw[j] + r;
         const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off);
         if (need_mask) {
+          // element i of key half kb is key kv0 + 32 kb + 4 hh + acc_row(i, 0): dead past S or
+          // after the lane's query -- one compare per element against a per-lane limit (a
+          // per-element condition compiled to scalar-mask branches)
+          const int lim0 = (a.causal ? min(a.S - 1, qi + off) : a.S - 1) - (kv0 + 4 * hh);
 #pragma unroll
           for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int key = kv0 + kb * 32 + acc_row(i, hh);
-              if (key >= a.S || (a.causal && key > qi + off)) s[j][kb][i] = -INFINITY;
-            }
+            for (int i = 0; i < 16; ++i)
+              s[j][kb][i] = acc_row(i, 0) > lim0 - 32 * kb ? -INFINITY : s[j][kb][i];
           }
         }
         // two independent max / sum chains per lane (ILP), then the lane pair (r, r+32)
@@ -359,8 +365,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       for (int kst = 0; kst < 4; ++kst) {
 #pragma unroll
         for (int db = 0; db < NDB; ++db) {
-          const int row = kst * 16 + 4 * hh + tq, col = db * 32 + 16 * g1 + 4 * tp;
-          const bf16x8 va = cat_tr(ds_tr(Vb + I::off(row, col)), ds_tr(Vb + I::off(row + 8, col)));
+          const int rb = kst * 16 * D;
+          const bf16x8 va = cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
 #pragma unroll
           for (int j = 0; j < QB; ++j)
             if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
