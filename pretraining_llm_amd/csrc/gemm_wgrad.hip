@@ -31,7 +31,9 @@
 //    (profiles/r2_wgrad_phased_negative_*.jsonl).  PMC (profiles/r2_pmc_wgrad_*head.md): both run
 //    the LM-head shape at the same MFMA cycles, 77 % L2 hit rate, 8.4 TB/s L2->LDS, and the
 //    wave-cycle count puts the shader clock near 1.7 GHz under this load: ~60 % MFMA-busy at the
-//    clock the chip holds.
+//    clock the chip holds.  Also measured slower (6-10 %): fragments of k-step k+1 read into a second
+//    register set while step k's 8 MFMAs run, fenced by sched_barriers (256 VGPRs;
+//    profiles/r2_wgrad_regpipe_negative.jsonl) -- hipcc's own interleave of 2 reads per 2 MFMAs wins.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include <type_traits>
 
