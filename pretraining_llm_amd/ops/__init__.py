@@ -665,7 +665,10 @@ def embedding(idx, wte, wpe=None, pos_offset: int = 0):
 # (GPT-2 small, 65,536 rows x 50,304, profiles/r2_ce_chunk_sweep.jsonl): 63.4 ms/step unchunked
 # (29.9 GB peak) vs 64.5 / 65.3 / 70.6 / 73.8 ms at 16K / 8K / 4K / 2K rows (24.8-23.1 GB): the
 # backward GEMMs lose efficiency at small M, so the default budget (8 GiB) keeps every shipped
-# config in one chunk and only bounds the workspace when batch x vocab grows past it.
+# config in one chunk and only bounds the workspace when batch x vocab grows past it.  Also
+# measured slower: sub-chunks of 1K / 2K / 4K rows for GEMM -> CE -> dgrad (logits kept in the
+# Infinity Cache between them) with one weight-gradient GEMM over the whole dlogits afterwards:
+# 75.7 / 68.5 / 66.6 ms vs 60.5 ms per step (scripts/gpu/r2_cesub.sh, profiles/r2_ce_subchunk_negative.txt).
 CE_CHUNK_ROWS = int(_os.environ.get("PLLM_CE_CHUNK_ROWS", "0"))
 CE_WORKSPACE_MB = float(_os.environ.get("PLLM_CE_WORKSPACE_MB", "8192"))
 
