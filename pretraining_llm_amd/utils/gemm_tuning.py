@@ -18,7 +18,9 @@ import tempfile
 
 import torch
 
-TUNING_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
+# PLLM_TUNING_DIR: an alternative table directory (A/B of tables)
+TUNING_DIR = os.environ.get("PLLM_TUNING_DIR") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
 
 
 def _merge_tables(dst: str):
@@ -44,8 +46,10 @@ def _merge_tables(dst: str):
     return True
 
 
-def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_dir: str = None) -> bool:
-    """Enable TunableOp with the shipped tables. Returns True if a table was loaded."""
+def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_dir: str = None,
+                       load_tables: bool = True) -> bool:
+    """Enable TunableOp with the shipped tables (``load_tables=False``: start empty, i.e. re-tune
+    every shape). Returns True if a table was loaded."""
     if not torch.cuda.is_available() or os.environ.get("PLLM_TUNABLEOP", "1") == "0":
         return False
     try:
@@ -56,7 +60,7 @@ def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_di
     base = os.path.join(out_dir, "tunableop.csv")
     # TunableOp reads/writes "<stem><device>.csv" per device ordinal
     per_dev = os.path.join(out_dir, f"tunableop{device_index}.csv")
-    loaded = _merge_tables(per_dev)
+    loaded = _merge_tables(per_dev) if load_tables else False
     tunable.enable(True)
     tunable.tuning_enable(bool(tune_missing))
     if tune_missing:

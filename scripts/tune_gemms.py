@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--out", required=True)
     ap.add_argument("--tune-ms", default="30")
+    ap.add_argument("--fresh", action="store_true", help="ignore the shipped tables (re-tune every shape)")
     args = ap.parse_args()
     os.environ["PLLM_TUNE_MS"] = args.tune_ms
     os.environ.setdefault("PLLM_TUNE_ITERS", "20")
@@ -35,7 +36,7 @@ def main():
     from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
     from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
     ops._lib.require()
-    enable_tuned_gemms(0, tune_missing=True)
+    enable_tuned_gemms(0, tune_missing=True, load_tables=not args.fresh)
     dev = torch.device("cuda", 0)
     cfg = get_preset(args.model)
     model = GPT(cfg).to(dev, torch.bfloat16)
