@@ -429,7 +429,10 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //   * 4 waves x 64 keys (KH = 2, one wave per SIMD): 13-19 % slower at D = 64;
 //   * 4 waves x 128 keys x 64 queries (48 KiB LDS, two workgroups per CU): 7-15 % slower;
 //   * the role-split kernel at D = 64: 28-49 % slower;
-//   * fused-role D = 128 (4 waves, one per SIMD, 64 / 128 queries): 19-26 % slower than role split.
+//   * fused-role D = 128 (4 waves, one per SIMD, 64 / 128 queries): 19-26 % slower than role split;
+//   * persistent grid (one workgroup per CU walking the items round-robin, next item's K/V loads
+//     issued before the dK/dV stores, those stores deferred into the next item): 2-4 % slower
+//     (profiles/r2_attn_bwd_persistent_negative.jsonl).
 constexpr float kLog2e = 1.4426950408889634f;
 
 template <int D>
