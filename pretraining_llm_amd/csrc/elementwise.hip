@@ -5,8 +5,10 @@
 // * SwiGLU -- Llama preset, input laid out [gate | up] along the last dim
 // * RoPE   -- rotate-half convention on the q and k heads of a packed qkv row
 //
-// Every kernel moves 16 B (8 x bf16) per lane per access and grid-strides over
-// a grid capped at 256 CUs x 8 blocks (cdna_hip_programming.md Guideline 11/13).
+// Every kernel moves 16 B (8 x bf16) per lane per access over a FULL grid (one 16-B vector per
+// thread; the loops still grid-stride for safety): a grid capped at 2048 blocks with
+// grid-stride loops streamed 5.1 TB/s where the full grid streams 6.0-6.2 TB/s on MI355X
+// (GELU fwd / bwd at 402 MB, bench/hbm_probe.py, profiles/r2_elementwise_grid_ab.txt).
 #include "common.h"
 #include "kernels.h"
 
@@ -16,7 +18,7 @@ PLLM_DEV float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x
 
 inline int ew_grid(size_t n_vec) {
   size_t g = (n_vec + 255) / 256;
-  return (int)(g < 2048 ? (g > 0 ? g : 1) : 2048);
+  return (int)(g < (1u << 30) ? (g > 0 ? g : 1) : (1u << 30));
 }
 
 // op: 0 relu, 1 gelu
