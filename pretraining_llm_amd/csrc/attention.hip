@@ -432,7 +432,9 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //   * fused-role D = 128 (4 waves, one per SIMD, 64 / 128 queries): 19-26 % slower than role split;
 //   * persistent grid (one workgroup per CU walking the items round-robin, next item's K/V loads
 //     issued before the dK/dV stores, those stores deferred into the next item): 2-4 % slower
-//     (profiles/r2_attn_bwd_persistent_negative.jsonl).
+//     (profiles/r2_attn_bwd_persistent_negative.jsonl);
+//   * delta = rowsum(dO O) formed in this kernel from O rows staged beside dO, instead of the
+//     attn_bwd_pre_kernel pass: 3-4 % slower (profiles/r2_attn_delta_fused_negative.txt).
 constexpr float kLog2e = 1.4426950408889634f;
 
 template <int D>
