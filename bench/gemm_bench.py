@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--shapes", default="gpt2", choices=["gpt2", "llama"])
+    ap.add_argument("--f32", action="store_true", help="fp32 gradient target (the training default)")
     ap.add_argument("--variants", default="32,16", help="wgrad_set_mfma values to compare (32: 32x32x16 tiles, 16: 16x16x32 tiles)")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
@@ -44,7 +45,7 @@ def main():
         torch.manual_seed(0)
         dy = (torch.randn(M, P, device=dev) * 0.1).bfloat16()
         x = torch.randn(M, Q, device=dev).bfloat16()
-        tgt = torch.zeros(P, Q, device=dev, dtype=torch.bfloat16)
+        tgt = torch.zeros(P, Q, device=dev, dtype=torch.float32 if args.f32 else torch.bfloat16)
         # correctness on the first 4096 rows
         r = torch.ops.pllm.wgrad(dy[:4096], x[:4096])
         ref = dy[:4096].float().t() @ x[:4096].float()
@@ -60,9 +61,10 @@ def main():
             for mf in variants:
                 torch.ops.pllm.wgrad_set_mfma(mf)
                 res.setdefault(f"hip{mf}_us", []).append(1e6 * timeit(lambda: torch.ops.pllm.wgrad(dy, x, tgt)))
-            res.setdefault("blas_us", []).append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
+            if not args.f32:
+                res.setdefault("blas_us", []).append(1e6 * timeit(lambda: tgt.addmm_(dy.t(), x)))
         torch.ops.pllm.wgrad_set_mfma(32)
-        for k in [f"hip{v}" for v in variants] + ["blas"]:
+        for k in [f"hip{v}" for v in variants] + ([] if args.f32 else ["blas"]):
             res[f"{k}_tflops"] = flops / (min(res[f"{k}_us"]) * 1e-6) / 1e12
         print(json.dumps(res), flush=True)
         out.append(res)

@@ -34,6 +34,9 @@
 //    clock the chip holds.  Also measured slower (6-10 %): fragments of k-step k+1 read into a second
 //    register set while step k's 8 MFMAs run, fenced by sched_barriers (256 VGPRs;
 //    profiles/r2_wgrad_regpipe_negative.jsonl) -- hipcc's own interleave of 2 reads per 2 MFMAs wins.
+//    And 6-14 % slower: 4 waves (one per SIMD) with 128x128 sub-tiles in AGPRs, i.e. 128 instead of
+//    192 KiB of LDS reads per stage (profiles/r2_wgrad_4wave_negative.jsonl) -- LDS read volume is not
+//    the limiter; the second wave per SIMD covering the per-stage barrier / DMA latency is worth more.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
 #include <type_traits>
 

@@ -43,6 +43,9 @@ def load(raise_on_error: bool = False) -> bool:
                 torch.ops.load_library(SO_PATH)
                 from . import fake  # meta implementations for FakeTensor tracing (torch.compile)
                 fake.register()
+                # PLLM_WGRAD_VARIANT: weight-gradient kernel variant for A/B runs (csrc/gemm_wgrad.hip)
+                if os.environ.get("PLLM_WGRAD_VARIANT"):
+                    torch.ops.pllm.wgrad_set_mfma(int(os.environ["PLLM_WGRAD_VARIANT"]))
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box

@@ -519,8 +519,13 @@ def test_wgrad_kernel(M, P, Q):
     assert _rel(acc32.double(), ref3) < 1e-5, _rel(acc32.double(), ref3)
     # the 16x16x32 MFMA variant computes the same product
     try:
-        torch.ops.pllm.wgrad_set_mfma(16)
-        assert _rel(torch.ops.pllm.wgrad(dy, x), ref) < 5e-3
+        for variant in (16,):
+            torch.ops.pllm.wgrad_set_mfma(variant)
+            assert _rel(torch.ops.pllm.wgrad(dy, x), ref) < 5e-3, variant
+            acc32 = torch.randn(P, Q, device=DEV)
+            ref3 = acc32.double() + dy.double().t() @ x.double()
+            torch.ops.pllm.wgrad(dy, x, acc32)
+            assert _rel(acc32.double(), ref3) < 1e-5, (variant, _rel(acc32.double(), ref3))
     finally:
         torch.ops.pllm.wgrad_set_mfma(32)
     # strided (non-contiguous rows) operands, e.g. a column slice of a packed buffer
