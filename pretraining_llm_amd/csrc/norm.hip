@@ -242,6 +242,40 @@ __global__ __launch_bounds__(1024) void col_reduce_kernel(const float* __restric
   }
 }
 
+// Up to three column reductions of the same [G, C] geometry in ONE launch (blockIdx.y picks the
+// slab): a LayerNorm backward's weight, bias and producer-bias gradients.  Three 6.8-us launches
+// of 12 blocks each were 0.66 ms of the GPT-2-small step (profiles/r2_prof6_gpt2small_b64_kernel_stats.md).
+struct ColReduceSet {
+  const float* part[3];
+  void* out[3];
+  int accumulate[3];
+};
+template <bool OF32>
+__global__ __launch_bounds__(1024) void col_reduce_set_kernel(ColReduceSet set, int G, int C) {
+  __shared__ float red[16][64];
+  const int y = blockIdx.y;
+  const float* __restrict__ part = set.part[y];
+  const int lane = threadIdx.x & 63, g0 = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  float a0 = 0.f, a1 = 0.f;
+  if (c < C) {
+    int g = g0;
+    for (; g + 16 < G; g += 32) {
+      a0 += part[(size_t)g * C + c];
+      a1 += part[(size_t)(g + 16) * C + c];
+    }
+    if (g < G) a0 += part[(size_t)g * C + c];
+  }
+  red[g0][lane] = a0 + a1;
+  __syncthreads();
+  if (threadIdx.x < 64 && c < C) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += red[i][lane];
+    stg1<OF32>(set.out[y], c, set.accumulate[y] ? s + ldg1<OF32>(set.out[y], c) : s);
+  }
+}
+
 // per-block column partial sums of a bf16 [N, C] matrix (bias gradient of a linear
 // layer whose output gradient is x).  Block = 256 threads = 4 row lanes x 64 column
 // chunks of 8 -> one 512-column panel; grid = (panels, row groups).
@@ -328,9 +362,15 @@ void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, c
   else if (K <= 4) { if (xbf) L(4, true); else L(4, false); }
   else { if (xbf) L(8, true); else L(8, false); }
 #undef L
-  col_reduce(dw_part, G, C, dw, grad_f32, accumulate, st);
-  if (db_part && db) col_reduce(db_part, G, C, db, grad_f32, accumulate, st);
-  if (xbf && xb) col_reduce(xb_part, G, C, xb, grad_f32, xb_accumulate, st);
+  // the (bit-identical) per-slab reductions of col_reduce, batched into one launch
+  ColReduceSet set{};
+  int n = 0;
+  set.part[n] = dw_part, set.out[n] = dw, set.accumulate[n++] = (int)accumulate;
+  if (db_part && db) set.part[n] = db_part, set.out[n] = db, set.accumulate[n++] = (int)accumulate;
+  if (xbf && xb) set.part[n] = xb_part, set.out[n] = xb, set.accumulate[n++] = (int)xb_accumulate;
+  const dim3 rg((C + 63) / 64, n);
+  if (grad_f32) hipLaunchKernelGGL(col_reduce_set_kernel<true>, rg, dim3(1024), 0, st, set, G, C);
+  else hipLaunchKernelGGL(col_reduce_set_kernel<false>, rg, dim3(1024), 0, st, set, G, C);
 }
 
 int colsum_groups(int N) {
