@@ -27,7 +27,22 @@ class ByteTokenizer:
         return self.encode_ordinary(text)
 
     def decode(self, ids):
-        return bytes(int(i) for i in ids if 0 <= int(i) < 256).decode("utf-8", errors="replace")
+        # runs of byte ids decode as UTF-8; any other id (BPE-range ids a model trained on
+        # synthetic or BPE-tokenized shards emits) is rendered as a visible <|id|> marker instead
+        # of being dropped, so a generation is never silently empty
+        out, run = [], []
+        for i in ids:
+            i = int(i)
+            if 0 <= i < 256:
+                run.append(i)
+                continue
+            if run:
+                out.append(bytes(run).decode("utf-8", errors="replace"))
+                run = []
+            out.append(f"<|{i}|>")
+        if run:
+            out.append(bytes(run).decode("utf-8", errors="replace"))
+        return "".join(out)
 
 
 class _HFWrap:

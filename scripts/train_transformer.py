@@ -4,7 +4,9 @@
 # DDP bootstrap :14-29, Trainer :35-109, main :112-143).  Same launch contract:
 #   python scripts/train_transformer.py                       (single process)
 #   torchrun --nproc_per_node=8 scripts/train_transformer.py  (one rank per GPU, RCCL)
-# plus ``--run <name>`` (config.config.PRESET_RUNS) and ``--key=value`` overrides
+# plus ``--preset=<name>`` (config.config.PRESET_RUNS; ``--run=<name>`` is the same flag, but under
+# torchrun only ``--preset`` works: torchrun's own parser takes ``--run`` for an abbreviation of
+# its ``--run-path``) and ``--key=value`` overrides
 # of any default_config key.  ``TORCH_COMPILE=1`` (the reference's toggle) replays the whole
 # training step as one captured hipGraph on the GPU (the hot ops are already hand-written gfx950
 # kernels; what is left to cut is per-launch host cost) and runs torch.compile on the CPU path.
@@ -29,7 +31,8 @@ def _parse_value(v: str):
 
 def build_config(argv=None) -> dict:
     ap = argparse.ArgumentParser(description=__doc__, allow_abbrev=False)
-    ap.add_argument("--run", default=None, help=f"named run preset: {sorted(PRESET_RUNS)}")
+    ap.add_argument("--preset", "--run", dest="run", default=None,
+                    help=f"named run preset: {sorted(PRESET_RUNS)} (use --preset under torchrun)")
     args, rest = ap.parse_known_args(argv)
     cfg = dict(default_config)
     if args.run:

@@ -166,3 +166,33 @@ def test_bench_self_launches_ranks_cpu():
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
     assert rec["comm"]["world"] == 2 and rec["comm"]["hook_launched_buckets"]
     assert rec["value"] > 0 and abs(rec["value"] - 2 * 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) / rec["value"] < 0.01
+
+
+def test_train_cli_under_torchrun_preset(tmp_path):
+    """The reference launch contract ``torchrun --nproc_per_node=N scripts/train_transformer.py``
+    with a named preset: ``--preset=`` survives torchrun's own argument parser (which takes
+    ``--run`` as an abbreviation of its ``--run-path``), 2 gloo ranks train, eval and save."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = tmp_path / "tiny.pt"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(root, "scripts", "train_transformer.py"), "--preset=gpt2-tiny-cpu",
+                        "--ddp_backend=gloo", "--t_train_steps=4", "--t_eval_steps=2", "--t_eval_iters=1",
+                        "--log_interval=2", "--t_batch_size=2", "--seq_len=64", f"--synthetic_dir={tmp_path}",
+                        "--synthetic_tokens=50000", f"--t_out_path={out}"],
+                       capture_output=True, text=True, timeout=300, cwd="/tmp",
+                       env={**os.environ, "OMP_NUM_THREADS": "2"})
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "world=2" in r.stdout and "Step 2" in r.stdout, r.stdout[-2000:]
+    assert out.exists()
+
+
+def test_byte_tokenizer_renders_non_byte_ids():
+    """The offline byte-level fallback keeps ids outside 0..255 visible in decoded text."""
+    from pretraining_llm_amd.data.tokenizer import ByteTokenizer
+    t = ByteTokenizer()
+    ids = t.encode("héllo") + [1234, 50256] + t.encode("!")
+    assert t.decode(ids) == "héllo<|1234|><|50256|>!"
+    assert t.decode(t.encode("plain")) == "plain"
