@@ -87,6 +87,8 @@ default_config = {
     'bucket_mb': 64.0,                # DP all-reduce bucket size (xGMI-sized, see parallel/dp.py)
     'first_bucket_mb': 4.0,
     'activation_checkpointing': None,
+    'override_preset_dims': False,    # with model_preset: the dims above (n_embed, n_head, n_blocks, ...) override the preset's
+    'tuned_gemms': True,              # GPU: load the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/)
     'tp_size': 1,                     # tensor parallelism: heads / FFN columns sharded (parallel/model_parallel.py)
     'sequence_parallel': False,       # with tp_size > 1: norm/residual regions sharded along the sequence
     'cp_size': 1,                     # context parallelism: sequence shards over cp_size ranks

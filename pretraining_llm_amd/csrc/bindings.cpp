@@ -544,9 +544,11 @@ std::vector<Tensor> embedding_bwd(const Tensor& dx, const Tensor& idx, int64_t V
   Tensor sorted = std::get<0>(sr).contiguous(), perm = std::get<1>(sr).to(at::kInt).contiguous();
   Tensor dwte = acc ? *dwte_acc : at::zeros({V, C}, dx.options());
   Tensor dwpe = has_wpe ? (acc ? *dwpe_acc : at::zeros({n_pos, C}, dx.options())) : Tensor();
+  Tensor part = at::empty({2 * pllm::embedding_bwd_chunks(Bn * T) * C}, dx.options().dtype(at::kFloat));
   if (Bn * T)
     pllm::embedding_bwd(dx.data_ptr(), sorted.data_ptr<int32_t>(), perm.data_ptr<int32_t>(), dwte.data_ptr(),
-                        has_wpe ? dwpe.data_ptr() : nullptr, gf32, Bn * T, (int)Bn, (int)T, (int)C, V, cur_stream());
+                        has_wpe ? dwpe.data_ptr() : nullptr, gf32, part.data_ptr<float>(), Bn * T, (int)Bn, (int)T,
+                        (int)C, V, cur_stream());
   if (acc) return {};
   if (!has_wpe) return {dwte};
   return {dwte, dwpe};

@@ -94,8 +94,9 @@ void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t N, int T, int C,
                    int pos_offset, int64_t V, hipStream_t st);
+int64_t embedding_bwd_chunks(int64_t N);  // fp32 workspace: 2 * chunks * C floats
 void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, bool grad_f32,
-                   int64_t N, int Bn, int T, int C, int64_t V, hipStream_t st);
+                   float* part, int64_t N, int Bn, int T, int C, int64_t V, hipStream_t st);
 
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);

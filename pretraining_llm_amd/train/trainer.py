@@ -92,6 +92,11 @@ class Trainer:
         self.scaler = DynamicLossScaler(init_scale=float(self.cfg.get("loss_scale_init", 2.0 ** 16)),
                                         growth_interval=int(self.cfg.get("loss_scale_growth_interval", 2000)),
                                         enabled=(dtype_name == "float16") if ls is None else bool(ls))
+        self.tuned_gemms = False
+        if self.device.type == "cuda" and self.cfg.get("tuned_gemms", True):
+            # the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/), as bench.py uses them
+            from ..utils.gemm_tuning import enable_tuned_gemms
+            self.tuned_gemms = enable_tuned_gemms(self.device.index or 0)
         self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
         # model parallelism (parallel/model_parallel.py): a dp x cp x tp mesh; the model is built
         # dense from the shared seed, then sharded, so every layout starts from the same weights

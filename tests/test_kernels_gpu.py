@@ -183,6 +183,39 @@ def test_embedding(with_pos):
     assert torch.equal(g1, wte.grad)
 
 
+@pytest.mark.parametrize("kind", ["zipf", "boundary_runs", "single_id"])
+def test_embedding_bwd_skewed_ids(kind):
+    """Skewed token distributions (Zipf as in real text, runs of exactly chunk-sized / chunk-crossing
+    lengths, one id everywhere): the chunked two-phase backward matches an fp64 index_add, into
+    fp32 and bf16 gradient targets, and is bitwise reproducible."""
+    torch.manual_seed(11)
+    V, C, B, T = 5000, 768, 8, 1024
+    N = B * T
+    if kind == "zipf":
+        z = torch.distributions.Pareto(1.0, 1.0).sample((N,)).floor().long() - 1
+        idx = (z.clamp_max(V - 1) * 7919 % V).view(B, T).to(DEV)
+    elif kind == "boundary_runs":
+        lens = [64, 128, 1, 63, 65, 127, 129, 2, 191, 64 * 5 + 3]
+        ids, i = [], 0
+        while len(ids) < N:
+            ids += [i % V] * lens[i % len(lens)]
+            i += 1
+        idx = torch.tensor(ids[:N])[torch.randperm(N)].view(B, T).to(DEV)
+    else:
+        idx = torch.full((B, T), 17, device=DEV)
+    dx = torch.randn(B, T, C, device=DEV).bfloat16()
+    ref = torch.zeros(V, C, dtype=torch.float64, device=DEV).index_add_(0, idx.view(-1), dx.view(N, C).double())
+    g32 = torch.randn(V, C, device=DEV)
+    base = g32.double().clone()
+    torch.ops.pllm.embedding_bwd_acc(dx, idx, V, 0, False, g32)
+    assert _rel(g32.double() - base, ref) < 1e-5, _rel(g32.double() - base, ref)
+    g32b = base.float().clone()
+    torch.ops.pllm.embedding_bwd_acc(dx, idx, V, 0, False, g32b)
+    assert torch.equal(g32, g32b)
+    gb, _ = torch.ops.pllm.embedding_bwd(dx, idx, V, 0, False)
+    assert _rel(gb.double(), ref) < 1e-2
+
+
 # ----------------------------------------------------------------- AdamW
 def test_adamw_flat_matches_torch():
     torch.manual_seed(6)
