@@ -51,6 +51,21 @@ def _hip(*ts) -> bool:
     return _BACKEND == "auto" and _lib.use_hip(*ts)
 
 
+# Numerics bisection (diagnostic): PLLM_TORCH_OPS=attn,norm,act,ce,embed,linear runs the named op
+# families through stock PyTorch ops while everything else stays on the HIP kernels
+# (scripts/convergence.py compares the resulting loss curves against fp32).
+_TORCH_OPS = frozenset(x for x in os.environ.get("PLLM_TORCH_OPS", "").split(",") if x)
+
+
+def _hip_op(name: str, *ts) -> bool:
+    return name not in _TORCH_OPS and _hip(*ts)
+
+
+def _stock(name: str) -> bool:
+    """True when op family ``name`` runs on stock torch ops (torch backend, or bisected out)."""
+    return _BACKEND == "torch" or name in _TORCH_OPS
+
+
 def _ops():
     return _lib.require()
 
@@ -200,8 +215,11 @@ def _weight_grad(dy2, x2, tgt):
 
 
 def linear(x, weight, bias=None, bias_grad_external: bool = False):
-    if _hip(x) and torch.is_grad_enabled() and weight.requires_grad:
-        return _LinearFn.apply(x, weight, bias, bias_grad_external and bias is not None)
+    if _hip_op("linear", x) and torch.is_grad_enabled() and weight.requires_grad:
+        # a bias gradient is left to the consumer's kernel only while that consumer (norm / act)
+        # runs on the HIP kernels
+        ext = bias_grad_external and bias is not None and not (_TORCH_OPS & {"norm", "act"})
+        return _LinearFn.apply(x, weight, bias, ext)
     if _hip(x) and not (torch.is_grad_enabled() and x.requires_grad):
         # decode-sized inference projections (<= 8 token rows): weight-streaming skinny GEMM
         # (csrc/gemv.hip) instead of the training-sized library tiles
@@ -334,7 +352,7 @@ class _NormFn(torch.autograd.Function):
 
 def _norm_ref(x, residual, weight, bias, eps, rms):
     s = x if residual is None else x + residual
-    if _BACKEND == "torch":
+    if _stock("norm"):
         if rms:
             y = F.rms_norm(s, (s.shape[-1],), weight, eps)
         else:
@@ -352,7 +370,7 @@ def layer_norm(x, weight, bias, eps: float = 1e-5, residual: Optional[torch.Tens
     """(LayerNorm(x + residual), x + residual).  ``x_bias``: the bias of the linear layer that
     produced ``x`` (created with ``bias_grad_external=True``); its gradient is the column sum of
     dx and is produced by this norm's backward kernel (HIP path)."""
-    if _hip(x):
+    if _hip_op("norm", x):
         return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
                              weight, bias, eps, False, x_bias)
     return _norm_ref(x, residual, weight, bias, eps, False)
@@ -360,7 +378,7 @@ def layer_norm(x, weight, bias, eps: float = 1e-5, residual: Optional[torch.Tens
 
 def rms_norm(x, weight, eps: float = 1e-5, residual: Optional[torch.Tensor] = None,
              x_bias: Optional[torch.Tensor] = None):
-    if _hip(x):
+    if _hip_op("norm", x):
         return _NormFn.apply(x.contiguous(), residual.contiguous() if residual is not None else None,
                              weight, None, eps, True, x_bias)
     return _norm_ref(x, residual, weight, None, eps, True)
@@ -463,13 +481,13 @@ def attention_packed(qkv, n_head: int, n_kv_head: int, causal: bool = True, scal
     B, T, W = qkv.shape
     D = W // (n_head + 2 * n_kv_head)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
-    if _hip(qkv):
+    if _hip_op("attn", qkv):
         # RoPE fused into the attention kernels (q/k rotated while staged, dq/dk rotated back)
         return _FlashAttnPacked.apply(qkv, n_head, n_kv_head, causal, scale, rope_cos, rope_sin)
     if rope_cos is not None:
         qkv = rope_packed(qkv, rope_cos, rope_sin, n_head, n_kv_head)
     q, k, v = _split_qkv(qkv, n_head, n_kv_head, D)
-    if _BACKEND == "torch" and qkv.is_cuda:
+    if _stock("attn") and qkv.is_cuda:
         # stock-PyTorch baseline path (SDPA), used only by the explicit torch backend
         qh, kh, vh = (t.transpose(1, 2) for t in (q, k, v))
         o = F.scaled_dot_product_attention(qh, kh, vh, is_causal=causal, scale=scale,
@@ -591,21 +609,21 @@ class _SwigluFn(torch.autograd.Function):
 
 
 def gelu(x, bias: Optional[torch.Tensor] = None):
-    if _hip(x):
+    if _hip_op("act", x):
         return _GeluFn.apply(x.contiguous(), bias)
-    if _BACKEND == "torch":
+    if _stock("act"):
         return F.gelu(x, approximate="tanh")
     return ref.gelu_tanh(x)
 
 
 def swiglu(gate_up):
-    if _hip(gate_up):
+    if _hip_op("act", gate_up):
         return _SwigluFn.apply(gate_up.contiguous())
     return ref.swiglu(gate_up)
 
 
 def relu(x, bias: Optional[torch.Tensor] = None):
-    if _hip(x):
+    if _hip_op("act", x):
         return _ReluFn.apply(x.contiguous(), bias)
     return ref.relu(x)
 
@@ -643,7 +661,7 @@ class _EmbeddingFn(torch.autograd.Function):
 
 
 def embedding(idx, wte, wpe=None, pos_offset: int = 0):
-    if _hip(wte):
+    if _hip_op("embed", wte):
         if pos_offset:
             return _ops().embedding_fwd(idx.contiguous(), wte, wpe, pos_offset)
         return _EmbeddingFn.apply(idx.contiguous(), wte, wpe)
@@ -752,9 +770,9 @@ def lm_head_cross_entropy(h, weight, bias, targets, ignore_index: int = -100):
     (chunked over rows on the HIP path: no [N, V] buffer in training or evaluation)."""
     targets = targets.reshape(-1)
     h = h.reshape(-1, h.shape[-1])
-    if _hip(h) and torch.is_grad_enabled() and (h.requires_grad or weight.requires_grad):
+    if _hip_op("ce", h) and torch.is_grad_enabled() and (h.requires_grad or weight.requires_grad):
         return _LMHeadCEFn.apply(h, weight, bias, targets, ignore_index)
-    if _hip(h):
+    if _hip_op("ce", h):
         N, V = h.shape[0], weight.shape[0]
         R = _ce_chunk_rows(N, V)
         ws = torch.empty(R, V, dtype=h.dtype, device=h.device)

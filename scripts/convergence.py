@@ -22,7 +22,8 @@ if ROOT not in sys.path:
 
 
 def train_curve(backend: str, model: str, steps: int, batch: int, seq: int, lr: float, log_every: int = 10,
-                tokens: int = 4_000_000, data_dir: str = None, overrides: dict = None, device: str = "auto"):
+                tokens: int = 4_000_000, data_dir: str = None, overrides: dict = None, device: str = "auto",
+                seed: int = 1234):
     """Run ``steps`` optimizer steps; returns [(step, train_loss, val_loss)] every ``log_every``."""
     import torch
     from pretraining_llm_amd import ops
@@ -35,12 +36,15 @@ def train_curve(backend: str, model: str, steps: int, batch: int, seq: int, lr: 
                warmup_steps=max(1, steps // 10), lr_schedule="cosine", weight_decay=0.1, weight_decay_all=False,
                betas=(0.9, 0.95), max_grad_norm=1.0, log_interval=log_every, t_eval_steps=max(log_every, steps // 4),
                t_eval_iters=4, eval_at_start=False, synthetic_data=True, synthetic_tokens=tokens,
-               synthetic_kind="markov", synthetic_dir=data_dir, seed=1234, t_out_path=None, device=device,
+               synthetic_kind="markov", synthetic_dir=data_dir, seed=seed, t_out_path=None, device=device,
                ddp_backend="auto")
     cfg.update(overrides or {})
     recs = []
     tr = Trainer(cfg, log=lambda *_: None)
-    tr.metrics.log = lambda rec: recs.append(rec)  # keep the records in memory
+    def keep(rec):  # keep the records in memory; one progress line per record (long runs stay visibly alive)
+        recs.append(rec)
+        print(f"[convergence] {backend} step {rec['step']} loss {rec['train_loss']:.4f}", file=sys.stderr, flush=True)
+    tr.metrics.log = keep
     t0 = time.perf_counter()
     try:
         tr.train()
@@ -60,24 +64,28 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--lr", type=float, default=6e-4)
-    ap.add_argument("--backends", default="auto,torch")
+    ap.add_argument("--backends", default="auto,torch", help="comma list of backend[:dtype] (auto = HIP kernels)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--seed", type=int, default=1234, help="init / data-order seed (the synthetic shard stays the same)")
     args = ap.parse_args(argv)
     out = open(args.out, "w") if args.out else sys.stdout
     finals = {}
     for be in args.backends.split(","):
-        curve, wall = train_curve(be, args.model, args.steps, args.batch, args.seq, args.lr)
+        # "backend[:dtype]", e.g. torch:float32 = stock ops in fp32 (the numerics ground truth)
+        name, _, dt = be.partition(":")
+        curve, wall = train_curve(name, args.model, args.steps, args.batch, args.seq, args.lr,
+                                  overrides={"dtype": dt} if dt else None, seed=args.seed)
         for step, tl, vl in curve:
             out.write(json.dumps({"backend": be, "model": args.model, "step": step, "train_loss": round(tl, 5),
                                   "val_loss": None if vl != vl else round(vl, 5)}) + "\n")
         finals[be] = curve[-1][1]
         print(f"[convergence] backend={be} final train loss {curve[-1][1]:.4f} ({wall:.1f} s)", file=sys.stderr)
-    if len(finals) == 2:
-        a, b = finals.values()
-        gap = abs(a - b) / b
+    if len(finals) >= 2:
+        a, b = list(finals.values())[:2]
+        gap = (a - b) / b  # signed: > 0 when the first backend ends higher
         out.write(json.dumps({"summary": True, "final_loss": finals, "rel_gap": round(gap, 5),
                               "steps": args.steps, "batch": args.batch, "seq": args.seq}) + "\n")
-        print(f"[convergence] final-loss relative gap {100 * gap:.2f} %", file=sys.stderr)
+        print(f"[convergence] final-loss relative gap (first - second) / second {100 * gap:+.2f} %", file=sys.stderr)
     if out is not sys.stdout:
         out.close()
 
