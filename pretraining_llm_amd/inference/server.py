@@ -1,0 +1,190 @@
+"""Batched generation service (HTTP) over the KV-cache decoder.
+
+The reference serves text only through a one-shot CLI (scripts/generate_text.py:7-61: load,
+generate one prompt, exit).  For serving, the model stays resident and concurrent requests are
+batched: a worker thread drains a request queue, waits up to ``max_wait_ms`` for company, groups
+requests that can share one decode batch -- same prompt length and the same sampling settings,
+since every sequence of a batch advances through the same cache positions -- and runs each group
+as ONE batched ``generate`` (prefill through the flash-attention kernel, then one hipGraph replay
+per token, csrc/attn_decode.hip + csrc/gemv.hip + csrc/sampling.hip on the GPU).  Decode at batch
+64 is ~24x the tokens/s of batch 1 (README, profiles/r1_decode_bench_fused.jsonl), so batching is
+where serving throughput comes from.
+
+``GenerationServer`` is usable in-process (``submit`` -> Future); ``create_app`` wraps it in a
+FastAPI app (POST /generate, GET /health, GET /stats); ``scripts/serve.py`` runs it under uvicorn.
+"""
+
+import queue
+import threading
+import time
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional
+
+import torch
+
+
+@dataclass
+class GenRequest:
+    tokens: List[int]
+    max_new_tokens: int = 64
+    temperature: float = 1.0
+    top_k: Optional[int] = None
+    seed: Optional[int] = None
+    t_submit: float = field(default_factory=time.perf_counter)
+
+    def group_key(self):
+        # sequences decode in lockstep: one prompt length, one number of steps, one sampler
+        return (len(self.tokens), self.max_new_tokens, float(self.temperature), self.top_k, self.seed)
+
+
+@dataclass
+class GenResult:
+    tokens: List[int]          # prompt + generated ids
+    new_tokens: List[int]      # generated ids only
+    batch_size: int            # how many requests shared the decode batch
+    latency_ms: float          # submit -> result
+
+
+class GenerationServer:
+    def __init__(self, model, max_batch: int = 64, max_wait_ms: float = 5.0, cuda_graph: bool = True):
+        self.model = model.eval()
+        self.device = next(model.parameters()).device
+        self.max_batch = int(max_batch)
+        self.max_wait = max_wait_ms / 1e3
+        self.cuda_graph = cuda_graph and self.device.type == "cuda"
+        self._q = queue.Queue()
+        self._stop = threading.Event()
+        self.stats: Dict[str, float] = {"requests": 0, "batches": 0, "generated_tokens": 0, "max_batch_seen": 0}
+        self._worker = threading.Thread(target=self._run, name="pllm-generation", daemon=True)
+        self._worker.start()
+
+    # ------------------------------------------------------------------
+    def submit(self, req: GenRequest) -> Future:
+        ctx = self.model.config.context_length
+        if not req.tokens:
+            raise ValueError("empty prompt")
+        if req.max_new_tokens < 1:
+            raise ValueError("max_new_tokens must be >= 1")
+        if any(t < 0 or t >= self.model.config.vocab_size for t in req.tokens):
+            raise ValueError("token id outside the vocabulary")
+        if self.model.config.pos != "learned" and len(req.tokens) + req.max_new_tokens > 8 * ctx:
+            raise ValueError("prompt + max_new_tokens too long")
+        fut: Future = Future()
+        self._q.put((req, fut))
+        return fut
+
+    def close(self):
+        self._stop.set()
+        self._q.put(None)
+        self._worker.join(timeout=30)
+
+    # ------------------------------------------------------------------
+    def _collect(self):
+        first = self._q.get()
+        if first is None:
+            return None
+        items = [first]
+        deadline = time.perf_counter() + self.max_wait
+        while len(items) < self.max_batch:
+            left = deadline - time.perf_counter()
+            if left <= 0:
+                break
+            try:
+                it = self._q.get(timeout=left)
+            except queue.Empty:
+                break
+            if it is None:
+                self._stop.set()
+                break
+            items.append(it)
+        return items
+
+    def _run(self):
+        while not self._stop.is_set():
+            items = self._collect()
+            if items is None:
+                return
+            groups: Dict[tuple, list] = {}
+            for req, fut in items:
+                groups.setdefault(req.group_key(), []).append((req, fut))
+            for key, members in groups.items():
+                for i in range(0, len(members), self.max_batch):
+                    self._serve(members[i:i + self.max_batch])
+
+    def _serve(self, members):
+        req0 = members[0][0]
+        try:
+            idx = torch.tensor([r.tokens for r, _ in members], dtype=torch.long, device=self.device)
+            gen = None
+            if req0.seed is not None:
+                gen = torch.Generator(device=self.device).manual_seed(int(req0.seed))
+            with torch.no_grad():
+                out = self.model.generate(idx, max_new_tokens=req0.max_new_tokens, temperature=req0.temperature,
+                                          top_k=req0.top_k, generator=gen, cuda_graph=self.cuda_graph)
+            out = out.tolist()
+        except Exception as e:  # deliver the failure to every waiter of the batch
+            for _, fut in members:
+                fut.set_exception(e)
+            return
+        now = time.perf_counter()
+        n = len(members)
+        self.stats["requests"] += n
+        self.stats["batches"] += 1
+        self.stats["generated_tokens"] += n * req0.max_new_tokens
+        self.stats["max_batch_seen"] = max(self.stats["max_batch_seen"], n)
+        for (r, fut), seq in zip(members, out):
+            fut.set_result(GenResult(tokens=seq, new_tokens=seq[len(r.tokens):], batch_size=n,
+                                     latency_ms=1e3 * (now - r.t_submit)))
+
+
+def create_app(server: GenerationServer, tokenizer=None):
+    """FastAPI app: POST /generate {prompt | tokens, max_new_tokens, temperature, top_k, seed},
+    GET /health, GET /stats."""
+    import asyncio
+
+    from fastapi import FastAPI, HTTPException
+    from pydantic import BaseModel
+
+    class GenerateBody(BaseModel):
+        prompt: Optional[str] = None
+        tokens: Optional[List[int]] = None
+        max_new_tokens: int = 64
+        temperature: float = 1.0
+        top_k: Optional[int] = None
+        seed: Optional[int] = None
+
+    app = FastAPI(title="pretraining-llm-amd generation")
+    cfg = server.model.config
+
+    @app.get("/health")
+    def health():
+        return {"status": "ok", "device": str(server.device), "arch": cfg.arch, "n_blocks": cfg.n_blocks,
+                "n_embed": cfg.n_embed, "vocab_size": cfg.vocab_size, "context_length": cfg.context_length}
+
+    @app.get("/stats")
+    def stats():
+        return dict(server.stats)
+
+    @app.post("/generate")
+    async def generate(body: GenerateBody):
+        if body.tokens is None and body.prompt is None:
+            raise HTTPException(400, "give 'prompt' or 'tokens'")
+        if body.tokens is not None:
+            toks = list(body.tokens)
+        else:
+            if tokenizer is None:
+                raise HTTPException(400, "no tokenizer loaded: send 'tokens'")
+            toks = tokenizer.encode_ordinary(body.prompt) or [tokenizer.eot_token % cfg.vocab_size]
+        try:
+            fut = server.submit(GenRequest(toks, body.max_new_tokens, body.temperature, body.top_k, body.seed))
+        except ValueError as e:
+            raise HTTPException(400, str(e))
+        res: GenResult = await asyncio.wrap_future(fut)
+        out = {"tokens": res.new_tokens, "prompt_tokens": len(toks), "batch_size": res.batch_size,
+               "latency_ms": round(res.latency_ms, 3)}
+        if tokenizer is not None:
+            out["text"] = tokenizer.decode(res.tokens)
+        return out
+
+    return app

@@ -1,0 +1,65 @@
+"""Batched generation service (pretraining_llm_amd/inference/server.py) on CPU: concurrent requests
+with one prompt length share a decode batch, greedy outputs equal single-request generate(), the
+HTTP layer (FastAPI TestClient) round-trips tokens and text, bad requests are rejected."""
+import threading
+
+import pytest
+import torch
+
+from pretraining_llm_amd.inference.server import GenerationServer, GenRequest, create_app
+from pretraining_llm_amd.models import GPT, get_preset
+
+
+@pytest.fixture(scope="module")
+def model():
+    torch.manual_seed(0)
+    return GPT(get_preset("gpt2-tiny").replace(context_length=64)).eval()
+
+
+def test_batches_concurrent_requests_and_matches_generate(model):
+    srv = GenerationServer(model, max_batch=8, max_wait_ms=200.0)
+    try:
+        prompts = [[5, 9, 13, 2], [7, 7, 1, 3], [100, 4, 8, 15], [42, 42, 42, 42], [1, 2, 3]]
+        futs = [srv.submit(GenRequest(p, max_new_tokens=6, temperature=0.0)) for p in prompts]
+        res = [f.result(timeout=120) for f in futs]
+        assert [r.batch_size for r in res[:4]] == [4, 4, 4, 4] and res[4].batch_size == 1
+        for p, r in zip(prompts, res):
+            ref = model.generate(torch.tensor([p]), max_new_tokens=6, temperature=0.0)[0].tolist()
+            assert r.tokens == ref and r.new_tokens == ref[len(p):]
+        assert srv.stats["requests"] == 5 and srv.stats["batches"] == 2 and srv.stats["max_batch_seen"] == 4
+        with pytest.raises(ValueError):
+            srv.submit(GenRequest([], max_new_tokens=3))
+        with pytest.raises(ValueError):
+            srv.submit(GenRequest([model.config.vocab_size], max_new_tokens=3))
+    finally:
+        srv.close()
+
+
+def test_http_app(model):
+    pytest.importorskip("httpx")
+    from fastapi.testclient import TestClient
+
+    from pretraining_llm_amd.data.tokenizer import ByteTokenizer
+    srv = GenerationServer(model, max_batch=4, max_wait_ms=100.0)
+    try:
+        client = TestClient(create_app(srv, ByteTokenizer()))
+        h = client.get("/health").json()
+        assert h["status"] == "ok" and h["n_blocks"] == 2
+        out = {}
+
+        def call(i):
+            out[i] = client.post("/generate", json={"tokens": [3, 1, 4, 1 + i], "max_new_tokens": 5,
+                                                    "temperature": 0.0}).json()
+        ts = [threading.Thread(target=call, args=(i,)) for i in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert all(len(out[i]["tokens"]) == 5 and out[i]["prompt_tokens"] == 4 for i in range(3))
+        assert max(out[i]["batch_size"] for i in range(3)) >= 2
+        r = client.post("/generate", json={"prompt": "hi", "max_new_tokens": 3, "temperature": 0.0}).json()
+        assert r["text"].startswith("hi") and len(r["tokens"]) == 3
+        assert client.post("/generate", json={"max_new_tokens": 3}).status_code == 400
+        assert client.get("/stats").json()["requests"] >= 4
+    finally:
+        srv.close()
