@@ -129,8 +129,11 @@ def sample_next(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[
 @torch.no_grad()
 def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0, top_k: Optional[int] = None,
              use_cache: bool = True, generator: Optional[torch.Generator] = None,
-             cuda_graph: bool = False) -> torch.Tensor:
-    """``cuda_graph``: replay each single-token step from one captured hipGraph (GPU only)."""
+             cuda_graph: bool = False, decode_cache: Optional[dict] = None) -> torch.Tensor:
+    """``cuda_graph``: replay each single-token step from one captured hipGraph (GPU only).
+    ``decode_cache``: a dict owned by the caller (e.g. the generation service) that keeps the KV
+    cache and the captured decode graph per (batch, cache length) across calls, so a repeated
+    shape skips the allocation and the capture (the prefill overwrites the rows a call reads)."""
     was_training = model.training
     model.eval()
     cfg = model.config
@@ -147,12 +150,18 @@ def generate(model, idx: torch.Tensor, max_new_tokens: int, temperature: float =
         B = idx.shape[0]
         max_len = min(idx.shape[1] + max_new_tokens, ctx_len) if learned else idx.shape[1] + max_new_tokens
         dtype = model.token_embed.weight.dtype
-        cache = KVCache(cfg.n_blocks, B, max(max_len, 1), cfg.n_kv_head, cfg.head_dim, dtype, idx.device)
+        key = (B, max(max_len, 1), dtype, idx.device)
+        cache, graph = decode_cache.get(key, (None, None)) if decode_cache is not None else (None, None)
+        if cache is None:
+            cache = KVCache(cfg.n_blocks, B, max(max_len, 1), cfg.n_kv_head, cfg.head_dim, dtype, idx.device)
         window = idx[:, -ctx_len:] if learned else idx
-        graph = None
-        if cuda_graph and idx.is_cuda and max_new_tokens > 1:
+        if graph is None and cuda_graph and idx.is_cuda and max_new_tokens > 1:
             # captured before the prefill: its warm-up steps write cache row 0, which the prefill overwrites
             graph = DecodeGraph(model, cache, B, idx.device)
+        if decode_cache is not None:
+            decode_cache[key] = (cache, graph)
+        if not cuda_graph:
+            graph = None
         logits = forward_cached(model, window, cache, 0)
         pos = window.shape[1]
         for step in range(max_new_tokens):

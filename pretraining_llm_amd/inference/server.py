@@ -47,13 +47,16 @@ class GenResult:
 
 
 class GenerationServer:
-    def __init__(self, model, max_batch: int = 64, max_wait_ms: float = 5.0, cuda_graph: bool = True):
+    def __init__(self, model, max_batch: int = 64, max_wait_ms: float = 5.0, cuda_graph: bool = True,
+                 max_cached_shapes: int = 16):
         self.model = model.eval()
         self.device = next(model.parameters()).device
         self.max_batch = int(max_batch)
         self.max_wait = max_wait_ms / 1e3
+        self.max_cached_shapes = int(max_cached_shapes)
         self.cuda_graph = cuda_graph and self.device.type == "cuda"
         self._q = queue.Queue()
+        self._decode_cache = {}  # (batch, cache length) -> KV cache + captured decode graph, reused
         self._stop = threading.Event()
         self.stats: Dict[str, float] = {"requests": 0, "batches": 0, "generated_tokens": 0, "max_batch_seen": 0}
         self._worker = threading.Thread(target=self._run, name="pllm-generation", daemon=True)
@@ -121,8 +124,11 @@ class GenerationServer:
                 gen = torch.Generator(device=self.device).manual_seed(int(req0.seed))
             with torch.no_grad():
                 out = self.model.generate(idx, max_new_tokens=req0.max_new_tokens, temperature=req0.temperature,
-                                          top_k=req0.top_k, generator=gen, cuda_graph=self.cuda_graph)
+                                          top_k=req0.top_k, generator=gen, cuda_graph=self.cuda_graph,
+                                          decode_cache=self._decode_cache)
             out = out.tolist()
+            while len(self._decode_cache) > self.max_cached_shapes:  # oldest shape first
+                self._decode_cache.pop(next(iter(self._decode_cache)))
         except Exception as e:  # deliver the failure to every waiter of the batch
             for _, fut in members:
                 fut.set_exception(e)

@@ -444,10 +444,10 @@ class GPT(nn.Module):
     @torch.no_grad()
     def generate(self, idx: torch.Tensor, max_new_tokens: int, temperature: float = 1.0,
                  top_k: Optional[int] = None, use_cache: bool = True, generator=None,
-                 cuda_graph: bool = False) -> torch.Tensor:
+                 cuda_graph: bool = False, decode_cache: Optional[dict] = None) -> torch.Tensor:
         if self.parallel is not None and self.parallel.model_parallel:
             raise ValueError("generate() runs on a dense model: load the consolidated checkpoint "
                              "(Trainer.save writes one) or parallel.model_parallel.gather_dense_state")
         from ..inference.generate import generate
         return generate(self, idx, max_new_tokens, temperature=temperature, top_k=top_k,
-                        use_cache=use_cache, generator=generator, cuda_graph=cuda_graph)
+                        use_cache=use_cache, generator=generator, cuda_graph=cuda_graph, decode_cache=decode_cache)
