@@ -73,6 +73,8 @@ class GenerationServer:
             raise ValueError("token id outside the vocabulary")
         if self.model.config.pos != "learned" and len(req.tokens) + req.max_new_tokens > 8 * ctx:
             raise ValueError("prompt + max_new_tokens too long")
+        if self._stop.is_set():
+            raise RuntimeError("generation server closed")
         fut: Future = Future()
         self._q.put((req, fut))
         return fut
@@ -81,6 +83,13 @@ class GenerationServer:
         self._stop.set()
         self._q.put(None)
         self._worker.join(timeout=30)
+        while True:  # requests still queued behind the stop marker fail instead of waiting forever
+            try:
+                it = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if it is not None:
+                it[1].set_exception(RuntimeError("generation server closed"))
 
     # ------------------------------------------------------------------
     def _collect(self):
