@@ -18,7 +18,8 @@
 //    the main loop.  Slices merge by shuffles inside a wave, then through LDS;
 //  * splits > 1 write an fp32 partial (o, log2-sum-exp) per split and a combine
 //    kernel merges them (deterministic, fixed order); splits == 1 writes bf16 o.
-//  * the key count can come from a device scalar (`seqlen`), so a decode step
+//  * the key count can come from a device scalar (`seqlen`; or one count per sequence for
+//    continuous batching, where every slot of the batch sits at its own position), so a decode step
 //    can be captured once in a hipGraph and replayed at every position.
 #include "common.h"
 #include "kernels.h"
@@ -34,7 +35,7 @@ __global__ __launch_bounds__(NT) void attn_decode_kernel(DecodeArgs a) {
   const int split = blockIdx.x, hk = blockIdx.y, b = blockIdx.z;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int dp = t % LPR, ks = t / LPR;
-  const int S = a.seqlen ? *a.seqlen : a.S;
+  const int S = a.seqlen ? a.seqlen[a.seqlen_per_row ? b : 0] : a.S;
   const int chunk = (S + a.splits - 1) / a.splits;
   const int k0 = split * chunk, k1 = min(S, k0 + chunk);
 

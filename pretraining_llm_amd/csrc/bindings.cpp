@@ -250,8 +250,9 @@ std::tuple<Tensor, Tensor> gemv(const Tensor& x, const Tensor& w, const std::opt
     kv_ldb = kc->stride(0);
     kv_cols = kc->stride(1);
     TORCH_CHECK(q_cols >= 0 && q_cols + 2 * kv_cols == N, "gemv: q_cols + 2 * kv_cols must equal N");
-    TORCH_CHECK(pos->scalar_type() == at::kLong && pos->numel() == 1 && pos->device() == x.device(),
-                "gemv: pos int64 [1] on the device");
+    TORCH_CHECK(pos->scalar_type() == at::kLong && (pos->numel() == 1 || pos->numel() == M) &&
+                    pos->is_contiguous() && pos->device() == x.device(),
+                "gemv: pos int64 [1] or [M] (one position per row) on the device");
     // the position itself stays on the device (hipGraph replay); the caller bounds it by S_max
   }
   Tensor y = at::empty({M, N}, x.options());
@@ -281,6 +282,7 @@ std::tuple<Tensor, Tensor> gemv(const Tensor& x, const Tensor& w, const std::opt
     a.kc = kc ? (uint16_t*)kc->data_ptr() : nullptr;
     a.vc = kc ? (uint16_t*)vc->data_ptr() : nullptr;
     a.pos = kc ? (const int64_t*)pos->data_ptr() : nullptr;
+    a.pos_per_row = kc && pos->numel() == M && M > 1;
     a.kv_ldb = kv_ldb;
     a.q_cols = (int)q_cols;
     a.kv_cols = (int)kv_cols;
@@ -715,9 +717,11 @@ Tensor attn_decode(const Tensor& q, const Tensor& k, const Tensor& v, double sca
   a.o_sb = o.stride(0); a.o_sh = o.stride(2);
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   if (seqlen.has_value()) {
-    TORCH_CHECK(seqlen->is_cuda() && seqlen->scalar_type() == at::kInt && seqlen->numel() == 1,
-                "attn_decode: seqlen must be a 1-element int32 device tensor");
+    TORCH_CHECK(seqlen->is_cuda() && seqlen->scalar_type() == at::kInt && seqlen->is_contiguous() &&
+                    (seqlen->numel() == 1 || seqlen->numel() == B),
+                "attn_decode: seqlen must be an int32 device tensor of 1 or B elements");
     a.seqlen = seqlen->data_ptr<int>();
+    a.seqlen_per_row = seqlen->numel() == B && B > 1;
   }
   a.splits = pllm::attn_decode_splits((int)B, (int)Hkv, (int)S);
   Tensor part_o, part_lse;

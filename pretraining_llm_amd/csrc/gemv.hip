@@ -241,7 +241,7 @@ __global__ __launch_bounds__(T) void gemv_splitk_kernel(const pllm::GemvArgs a) 
       else if (a.act == 2) v = fmaxf(v, 0.f);
       const uint16_t o = f2bf_bits(v);
       a.y[(int64_t)m * a.ldy + n] = o;
-      const int64_t p = a.kc ? *a.pos : -1;
+      const int64_t p = a.kc ? a.pos[a.pos_per_row ? m : 0] : -1;
       if (a.kc && n >= a.q_cols && p >= 0 && p < a.kv_smax) {  // KV-cache append (no copy kernels)
         const int j = n - a.q_cols;
         const int64_t at = (int64_t)m * a.kv_ldb + p * a.kv_cols;

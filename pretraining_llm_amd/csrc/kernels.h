@@ -25,6 +25,7 @@ struct DecodeArgs {
   uint16_t* o;
   float *part_o, *part_lse;  // [B, H, splits, D] / [B, H, splits] when splits > 1
   const int* seqlen;         // optional device key count (graph capture); else S
+  int seqlen_per_row;        // seqlen holds B counts (one per sequence) instead of one
   int B, H, Hkv, S, D, splits;
   int64_t q_sb, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_sh;
   float scale_log2;
@@ -137,6 +138,7 @@ struct GemvArgs {
   uint16_t* kc;
   uint16_t* vc;
   const int64_t* pos;
+  int pos_per_row;  // pos holds one position per row (continuous batching) instead of one
   int64_t kv_ldb;
   int q_cols, kv_cols, kv_smax;  // positions outside [0, kv_smax) are dropped, never written
 };

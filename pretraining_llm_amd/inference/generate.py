@@ -57,14 +57,14 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
 
 @torch.no_grad()
 def forward_decode(model, tok: torch.Tensor, cache: KVCache, pos_t: torch.Tensor, len_t: torch.Tensor) -> torch.Tensor:
-    """One decode step for tokens ``tok`` [B, 1] at the device position ``pos_t`` (int64 [1]);
-    ``len_t`` = pos_t + 1 as int32.  Every op is position-agnostic on the host (indexing by
+    """One decode step for tokens ``tok`` [B, 1] at the device position ``pos_t`` (int64 [1], or
+    [B]: one position per sequence, continuous batching); ``len_t`` = pos_t + 1 as int32.  Every op is position-agnostic on the host (indexing by
     device tensors, decode kernel reading the key count from ``len_t``), so the whole step
     is hipGraph-capturable.  Returns fp32 logits [B, V]."""
     cfg = model.config
     x = model.token_embed.weight.index_select(0, tok.view(-1)).view(tok.shape[0], 1, -1)
-    if model.position_embed is not None:
-        x = x + model.position_embed.weight.index_select(0, pos_t).view(1, 1, -1)
+    if model.position_embed is not None:  # pos_t: one position, or one per sequence
+        x = x + model.position_embed.weight.index_select(0, pos_t).view(pos_t.numel(), 1, -1)
     rope = model.rope_tables(tok.device, cache.max_len) if cfg.pos == "rope" else None
     res = None
     for i, blk in enumerate(model.attn_blocks):
@@ -81,11 +81,14 @@ class DecodeGraph:
     is launch-bound.  Replaying one graph removes the per-kernel host overhead.  Inputs
     live in static buffers (token ids, device position); outputs in a static logits buffer."""
 
-    def __init__(self, model, cache: KVCache, batch: int, device, warmup: int = 2):
+    def __init__(self, model, cache: KVCache, batch: int, device, warmup: int = 2, per_row: bool = False):
+        """``per_row``: one position per sequence (continuous batching: slots at different
+        positions); ``__call__`` then takes a [batch] position tensor."""
         self.model, self.cache = model, cache
+        n = batch if per_row else 1
         self.tok = torch.zeros(batch, 1, dtype=torch.long, device=device)
-        self.pos_t = torch.zeros(1, dtype=torch.long, device=device)
-        self.len_t = torch.ones(1, dtype=torch.int32, device=device)
+        self.pos_t = torch.zeros(n, dtype=torch.long, device=device)
+        self.len_t = torch.ones(n, dtype=torch.int32, device=device)
         side = torch.cuda.Stream(device)
         side.wait_stream(torch.cuda.current_stream(device))
         with torch.cuda.stream(side):  # warm up (allocator pools, lazy library init) off-graph
@@ -96,10 +99,14 @@ class DecodeGraph:
         with torch.cuda.graph(self.graph):
             self.logits = forward_decode(model, self.tok, cache, self.pos_t, self.len_t)
 
-    def __call__(self, tok: torch.Tensor, pos: int) -> torch.Tensor:
+    def __call__(self, tok: torch.Tensor, pos) -> torch.Tensor:
         self.tok.copy_(tok)
-        self.pos_t.fill_(pos)
-        self.len_t.fill_(pos + 1)
+        if isinstance(pos, torch.Tensor):
+            self.pos_t.copy_(pos)
+            self.len_t.copy_(pos + 1)
+        else:
+            self.pos_t.fill_(pos)
+            self.len_t.fill_(pos + 1)
         self.graph.replay()
         return self.logits
 

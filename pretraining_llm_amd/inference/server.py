@@ -10,8 +10,10 @@ per token, csrc/attn_decode.hip + csrc/gemv.hip + csrc/sampling.hip on the GPU).
 64 is ~24x the tokens/s of batch 1 (README, profiles/r1_decode_bench_fused.jsonl), so batching is
 where serving throughput comes from.
 
-``GenerationServer`` is usable in-process (``submit`` -> Future); ``create_app`` wraps it in a
-FastAPI app (POST /generate, GET /health, GET /stats); ``scripts/serve.py`` runs it under uvicorn.
+``GenerationServer`` (lockstep groups) and ``ContinuousGenerationServer`` (continuous batching:
+decode slots at per-sequence positions, requests join and leave the running batch one token step
+at a time) are usable in-process (``submit`` -> Future); ``create_app`` wraps either in a FastAPI
+app (POST /generate, GET /health, GET /stats); ``scripts/serve.py`` runs it under uvicorn.
 """
 
 import queue
@@ -203,3 +205,195 @@ def create_app(server: GenerationServer, tokenizer=None):
         return out
 
     return app
+
+
+class ContinuousGenerationServer:
+    """Continuous batching: a fixed set of ``max_batch`` decode slots, each sequence at its own
+    position.  A request is prefilled alone into a free slot (flash attention over its prompt)
+    as soon as one frees up, then joins the shared decode step: one step advances every active
+    slot by one token (per-sequence positions and key counts go to the decode kernels as device
+    tensors -- csrc/attn_decode.hip, csrc/gemv.hip -- so the step is one hipGraph replay for the
+    whole slot set), and a finished sequence leaves without waiting for the others.  Unlike the
+    lockstep ``GenerationServer`` no request waits for company of the same prompt length.
+
+    Learned absolute positions (arch ref / gpt2) follow the reference's crop semantics: a slot
+    whose sequence reaches ``context_length`` is re-prefilled on its last ``context_length``
+    tokens for every further token (transformer.py:108), outside the shared step."""
+
+    def __init__(self, model, max_batch: int = 32, max_len: Optional[int] = None, cuda_graph: bool = True):
+        from .generate import DecodeGraph, KVCache
+        cfg = model.config
+        self.model = model.eval()
+        self.device = next(model.parameters()).device
+        self.B = int(max_batch)
+        self.learned = cfg.pos == "learned"
+        self.ctx = cfg.context_length
+        self.max_len = self.ctx if self.learned else int(max_len or self.ctx)
+        dtype = model.token_embed.weight.dtype
+        self.cache = KVCache(cfg.n_blocks, self.B, self.max_len, cfg.n_kv_head, cfg.head_dim, dtype, self.device)
+        self.graph = None
+        if cuda_graph and self.device.type == "cuda":
+            # captured before any prefill: its warm-up steps write cache row 0 of every slot,
+            # which a slot's prefill overwrites before the slot is used
+            self.graph = DecodeGraph(model, self.cache, self.B, self.device, per_row=True)
+        self.slots: List[Optional[dict]] = [None] * self.B
+        self._q = queue.Queue()
+        self._stop = threading.Event()
+        self.stats: Dict[str, float] = {"requests": 0, "decode_steps": 0, "generated_tokens": 0,
+                                        "max_active_slots": 0, "prefills": 0}
+        self._worker = threading.Thread(target=self._run, name="pllm-continuous-batching", daemon=True)
+        self._worker.start()
+
+    # ------------------------------------------------------------------ API (as GenerationServer)
+    def submit(self, req: GenRequest) -> Future:
+        if self._stop.is_set():
+            raise RuntimeError("generation server closed")
+        if not req.tokens:
+            raise ValueError("empty prompt")
+        if req.max_new_tokens < 1:
+            raise ValueError("max_new_tokens must be >= 1")
+        if any(t < 0 or t >= self.model.config.vocab_size for t in req.tokens):
+            raise ValueError("token id outside the vocabulary")
+        if not self.learned and len(req.tokens) + req.max_new_tokens > self.max_len:
+            raise ValueError(f"prompt + max_new_tokens exceeds the server's cache length {self.max_len}")
+        fut: Future = Future()
+        self._q.put((req, fut))
+        return fut
+
+    def close(self):
+        self._stop.set()
+        self._q.put(None)
+        self._worker.join(timeout=60)
+        while True:
+            try:
+                it = self._q.get_nowait()
+            except queue.Empty:
+                break
+            if it is not None:
+                it[1].set_exception(RuntimeError("generation server closed"))
+
+    # ------------------------------------------------------------------ internals
+    def _slot_cache(self, s: int):
+        from .generate import KVCache
+        view = KVCache.__new__(KVCache)
+        view.k = [t[s:s + 1] for t in self.cache.k]
+        view.v = [t[s:s + 1] for t in self.cache.v]
+        view.max_len = self.max_len
+        return view
+
+    def _prefill(self, s: int, tokens: List[int]) -> torch.Tensor:
+        from .generate import forward_cached
+        window = tokens[-self.ctx:] if self.learned else tokens
+        idx = torch.tensor([window], dtype=torch.long, device=self.device)
+        self.stats["prefills"] += 1
+        with torch.no_grad():
+            return forward_cached(self.model, idx, self._slot_cache(s), 0), len(window)
+
+    def _sample(self, rows: List[int], logits: torch.Tensor) -> List[int]:
+        """Next token for each slot in ``rows`` (logits row k belongs to slot rows[k]); slots with the
+        same sampler and no private seed share one fused sampling launch."""
+        from .generate import sample_next
+        out = [0] * len(rows)
+        groups: Dict[tuple, List[int]] = {}
+        for k, s in enumerate(rows):
+            r = self.slots[s]["req"]
+            key = (float(r.temperature), r.top_k, s if r.seed is not None else -1)
+            groups.setdefault(key, []).append(k)
+        for (temp, top_k, private), ks in groups.items():
+            gen = self.slots[rows[ks[0]]]["gen"] if private >= 0 else None
+            sel = logits if len(ks) == logits.shape[0] else logits[ks]
+            nxt = sample_next(sel, temp, top_k, gen).view(-1).tolist()
+            for k, t in zip(ks, nxt):
+                out[k] = int(t)
+        return out
+
+    def _finish_done(self):
+        now = time.perf_counter()
+        for s, sl in enumerate(self.slots):
+            if sl is None:
+                continue
+            r = sl["req"]
+            if len(sl["seq"]) - len(r.tokens) >= r.max_new_tokens:
+                self.stats["requests"] += 1
+                self.stats["generated_tokens"] += r.max_new_tokens
+                sl["fut"].set_result(GenResult(tokens=sl["seq"], new_tokens=sl["seq"][len(r.tokens):],
+                                               batch_size=sl["peak_batch"], latency_ms=1e3 * (now - r.t_submit)))
+                self.slots[s] = None
+
+    def _admit(self, block: bool):
+        while any(sl is None for sl in self.slots):
+            try:
+                it = self._q.get(timeout=0.05) if block else self._q.get_nowait()
+            except queue.Empty:
+                return
+            block = False
+            if it is None:
+                self._stop.set()
+                return
+            req, fut = it
+            s = self.slots.index(None)
+            try:
+                gen = None
+                if req.seed is not None:
+                    gen = torch.Generator(device=self.device).manual_seed(int(req.seed))
+                self.slots[s] = {"req": req, "fut": fut, "seq": list(req.tokens), "pos": 0, "gen": gen,
+                                 "peak_batch": 1}
+                logits, pos = self._prefill(s, req.tokens)
+                self.slots[s]["pos"] = pos
+                self.slots[s]["seq"].append(self._sample([s], logits)[0])
+            except Exception as e:  # a bad request fails alone
+                self.slots[s] = None
+                fut.set_exception(e)
+        self._finish_done()
+
+    def _step(self):
+        from .generate import forward_decode
+        active = [s for s, sl in enumerate(self.slots) if sl is not None]
+        if not active:
+            return
+        self.stats["max_active_slots"] = max(self.stats["max_active_slots"], len(active))
+        for s in active:
+            self.slots[s]["peak_batch"] = max(self.slots[s]["peak_batch"], len(active))
+        shared = []
+        for s in active:
+            sl = self.slots[s]
+            if self.learned and sl["pos"] >= self.ctx:  # crop semantics: re-prefill the last ctx tokens
+                logits, sl["pos"] = self._prefill(s, sl["seq"])
+                sl["seq"].append(self._sample([s], logits)[0])
+            else:
+                shared.append(s)
+        if shared:
+            tok = [0] * self.B
+            pos = [0] * self.B  # idle slots decode a dummy token at row 0 (overwritten by their next prefill)
+            for s in shared:
+                tok[s] = self.slots[s]["seq"][-1]
+                pos[s] = self.slots[s]["pos"]
+            tok_t = torch.tensor(tok, dtype=torch.long).view(self.B, 1).to(self.device, non_blocking=True)
+            pos_t = torch.tensor(pos, dtype=torch.long).to(self.device, non_blocking=True)
+            with torch.no_grad():
+                if self.graph is not None:
+                    logits = self.graph(tok_t, pos_t)
+                else:
+                    logits = forward_decode(self.model, tok_t, self.cache, pos_t, (pos_t + 1).to(torch.int32))
+            rows = torch.tensor(shared, device=logits.device)
+            nxt = self._sample(shared, logits.index_select(0, rows))
+            for s, t in zip(shared, nxt):
+                self.slots[s]["seq"].append(t)
+                self.slots[s]["pos"] += 1
+            self.stats["decode_steps"] += 1
+        self._finish_done()
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                self._admit(block=all(sl is None for sl in self.slots))
+                self._step()
+            except Exception as e:  # fail every in-flight request rather than hang them
+                for s, sl in enumerate(self.slots):
+                    if sl is not None:
+                        sl["fut"].set_exception(e)
+                        self.slots[s] = None
+        for s, sl in enumerate(self.slots):
+            if sl is not None:
+                sl["fut"].set_exception(RuntimeError("generation server closed"))
+                self.slots[s] = None

@@ -111,13 +111,23 @@ class Attention(nn.Module):
         q = qkv[..., : H * D].view(B, 1, H, D)
         k = qkv[..., H * D:(H + Hkv) * D].view(B, 1, Hkv, D)
         v = qkv[..., (H + Hkv) * D:].view(B, 1, Hkv, D)
+        per_row = pos_t.numel() > 1  # continuous batching: every sequence at its own position
         if rope is not None:
             cos, sin = rope[0].index_select(0, pos_t), rope[1].index_select(0, pos_t)
-            q = ops.apply_rope(q, cos, sin, 0)
-            k = ops.apply_rope(k, cos, sin, 0)
+            if per_row:  # one table row per sequence: lay the batch out along the time axis
+                q = ops.apply_rope(q.reshape(1, B, H, D), cos, sin, 0).view(B, 1, H, D)
+                k = ops.apply_rope(k.reshape(1, B, Hkv, D), cos, sin, 0).view(B, 1, Hkv, D)
+            else:
+                q = ops.apply_rope(q, cos, sin, 0)
+                k = ops.apply_rope(k, cos, sin, 0)
         if not kv_written:
-            cache.k[layer_idx].index_copy_(1, pos_t, k)
-            cache.v[layer_idx].index_copy_(1, pos_t, v)
+            if per_row:
+                rows = torch.arange(B, device=pos_t.device)
+                cache.k[layer_idx].index_put_((rows, pos_t), k[:, 0])
+                cache.v[layer_idx].index_put_((rows, pos_t), v[:, 0])
+            else:
+                cache.k[layer_idx].index_copy_(1, pos_t, k)
+                cache.v[layer_idx].index_copy_(1, pos_t, v)
         y = ops.attention_decode(q.contiguous(), cache.k[layer_idx], cache.v[layer_idx], seqlen=len_t)
         y = y.reshape(B, 1, H * D)
         if self.proj is not None:

@@ -286,8 +286,13 @@ def norm_linear(x, residual, norm_weight, norm_bias, eps: float, rms: bool, weig
         kc, vc, pos, q_cols = kv
         B, kvc = kc.shape[0], kc[0, 0].numel()
         y2 = y.reshape(B, -1)
-        kc.index_copy_(1, pos, y2[:, q_cols:q_cols + kvc].reshape(B, 1, *kc.shape[2:]))
-        vc.index_copy_(1, pos, y2[:, q_cols + kvc:].reshape(B, 1, *vc.shape[2:]))
+        if pos.numel() > 1:  # one position per sequence (continuous batching)
+            rows = torch.arange(B, device=pos.device)
+            kc.index_put_((rows, pos), y2[:, q_cols:q_cols + kvc].reshape(B, *kc.shape[2:]))
+            vc.index_put_((rows, pos), y2[:, q_cols + kvc:].reshape(B, *vc.shape[2:]))
+        else:
+            kc.index_copy_(1, pos, y2[:, q_cols:q_cols + kvc].reshape(B, 1, *kc.shape[2:]))
+            vc.index_copy_(1, pos, y2[:, q_cols + kvc:].reshape(B, 1, *vc.shape[2:]))
     return y, s
 
 
@@ -521,6 +526,9 @@ def attention_decode(q, k, v, seqlen: Optional[torch.Tensor] = None, scale: Opti
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if _hip(q):
         return _ops().attn_decode(q, k, v, scale, seqlen)
+    if seqlen is not None and seqlen.numel() > 1:  # one key count per sequence
+        return torch.cat([ref.attention(q[b:b + 1], k[b:b + 1, :int(n)], v[b:b + 1, :int(n)], causal=False,
+                                        scale=scale)[0] for b, n in enumerate(seqlen.tolist())])
     if seqlen is not None:
         n = int(seqlen.item())
         k, v = k[:, :n], v[:, :n]

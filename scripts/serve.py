@@ -26,17 +26,26 @@ def main() -> None:
     ap.add_argument("--max_batch", type=int, default=64)
     ap.add_argument("--max_wait_ms", type=float, default=5.0, help="how long a request waits for batch company")
     ap.add_argument("--no_cuda_graph", action="store_true")
+    ap.add_argument("--mode", default="continuous", choices=["continuous", "lockstep"],
+                    help="continuous: decode slots at per-sequence positions (requests join/leave every token); "
+                         "lockstep: batch only requests with the same prompt length and sampler")
+    ap.add_argument("--max_len", type=int, default=None, help="continuous mode: KV-cache length per slot "
+                    "(default: the model's context length)")
     args = ap.parse_args()
     import uvicorn
 
     from config.config import default_config
     from pretraining_llm_amd.data.tokenizer import get_tokenizer
-    from pretraining_llm_amd.inference.server import GenerationServer, create_app
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer, GenerationServer, create_app
     from scripts.generate_text import load_model
     device = args.device if (not args.device.startswith("cuda") or torch.cuda.is_available()) else "cpu"
     model = load_model(args.model_path, device)
-    server = GenerationServer(model, max_batch=args.max_batch, max_wait_ms=args.max_wait_ms,
-                              cuda_graph=not args.no_cuda_graph)
+    if args.mode == "continuous":
+        server = ContinuousGenerationServer(model, max_batch=args.max_batch, max_len=args.max_len,
+                                            cuda_graph=not args.no_cuda_graph)
+    else:
+        server = GenerationServer(model, max_batch=args.max_batch, max_wait_ms=args.max_wait_ms,
+                                  cuda_graph=not args.no_cuda_graph)
     app = create_app(server, get_tokenizer(default_config.get("tokenizer_name", "gpt2")))
     try:
         uvicorn.run(app, host=args.host, port=args.port, log_level="info")

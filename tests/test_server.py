@@ -63,3 +63,45 @@ def test_http_app(model):
         assert client.get("/stats").json()["requests"] >= 4
     finally:
         srv.close()
+
+
+@pytest.mark.parametrize("preset", ["gpt2-tiny", "llama-tiny"])
+def test_continuous_batching_matches_single_requests(preset):
+    """Mixed prompt lengths share the decode slots (per-sequence positions); slots recycle as
+    requests finish; greedy outputs equal single-request generate(), including a learned-position
+    sequence that runs past context_length (crop semantics) and a one-token request."""
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer
+    torch.manual_seed(1)
+    cfg = get_preset(preset).replace(context_length=64)
+    m = GPT(cfg).eval()
+    V = cfg.vocab_size
+    g = torch.Generator().manual_seed(3)
+    reqs = [(torch.randint(0, V, (n,), generator=g).tolist(), k)
+            for n, k in [(5, 7), (11, 3), (2, 9), (17, 1), (8, 6), (30, 5)]]
+    if cfg.pos == "learned":
+        reqs.append((torch.randint(0, V, (60,), generator=g).tolist(), 10))  # crosses the 64-token context
+    srv = ContinuousGenerationServer(m, max_batch=3, max_len=80)
+    try:
+        futs = [srv.submit(GenRequest(p, max_new_tokens=k, temperature=0.0)) for p, k in reqs]
+        res = [f.result(timeout=300) for f in futs]
+    finally:
+        srv.close()
+    for (p, k), r in zip(reqs, res):
+        ref = m.generate(torch.tensor([p]), max_new_tokens=k, temperature=0.0)[0].tolist()
+        assert r.tokens == ref, (len(p), k)
+    assert srv.stats["requests"] == len(reqs) and srv.stats["max_active_slots"] == 3
+    assert max(r.batch_size for r in res) == 3
+
+
+def test_continuous_batching_rejects_and_closes():
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer
+    m = GPT(get_preset("llama-tiny").replace(context_length=32)).eval()
+    srv = ContinuousGenerationServer(m, max_batch=2, max_len=40)
+    try:
+        with pytest.raises(ValueError):
+            srv.submit(GenRequest([1, 2, 3], max_new_tokens=38))  # beyond the cache length
+        assert len(srv.submit(GenRequest([1, 2, 3], max_new_tokens=4, temperature=0.7, seed=5)).result(60).new_tokens) == 4
+    finally:
+        srv.close()
+    with pytest.raises(RuntimeError):
+        srv.submit(GenRequest([1], max_new_tokens=1))
