@@ -237,6 +237,10 @@ class ContinuousGenerationServer:
             # which a slot's prefill overwrites before the slot is used
             self.graph = DecodeGraph(model, self.cache, self.B, self.device, per_row=True)
         self.slots: List[Optional[dict]] = [None] * self.B
+        # device-resident decode state: the next input token of every slot and each slot's
+        # generated tokens, so a decode step needs no host <-> device round trip
+        self.tok_d = torch.zeros(self.B, 1, dtype=torch.long, device=self.device)
+        self.out_d = torch.zeros(self.B, 256, dtype=torch.long, device=self.device)
         self._q = queue.Queue()
         self._stop = threading.Event()
         self.stats: Dict[str, float] = {"requests": 0, "decode_steps": 0, "generated_tokens": 0,
@@ -289,62 +293,95 @@ class ContinuousGenerationServer:
         with torch.no_grad():
             return forward_cached(self.model, idx, self._slot_cache(s), 0), len(window)
 
-    def _sample(self, rows: List[int], logits: torch.Tensor) -> List[int]:
-        """Next token for each slot in ``rows`` (logits row k belongs to slot rows[k]); slots with the
-        same sampler and no private seed share one fused sampling launch."""
+    def _sample(self, rows: List[int], logits: torch.Tensor) -> torch.Tensor:
+        """Next token for each slot in ``rows`` (logits row k belongs to slot rows[k]) as a device
+        int64 [len(rows)] tensor (no host sync); slots with the same sampler and no private seed
+        share one fused sampling launch."""
         from .generate import sample_next
-        out = [0] * len(rows)
         groups: Dict[tuple, List[int]] = {}
         for k, s in enumerate(rows):
             r = self.slots[s]["req"]
             key = (float(r.temperature), r.top_k, s if r.seed is not None else -1)
             groups.setdefault(key, []).append(k)
+        if len(groups) == 1:
+            (temp, top_k, private), = groups.keys()
+            gen = self.slots[rows[0]]["gen"] if private >= 0 else None
+            return sample_next(logits, temp, top_k, gen).view(-1)
+        out = torch.empty(len(rows), dtype=torch.long, device=logits.device)
         for (temp, top_k, private), ks in groups.items():
             gen = self.slots[rows[ks[0]]]["gen"] if private >= 0 else None
-            sel = logits if len(ks) == logits.shape[0] else logits[ks]
-            nxt = sample_next(sel, temp, top_k, gen).view(-1).tolist()
-            for k, t in zip(ks, nxt):
-                out[k] = int(t)
+            idx = self._dev_index(ks)
+            out.index_copy_(0, idx, sample_next(logits.index_select(0, idx), temp, top_k, gen).view(-1))
         return out
+
+    def _dev_index(self, values: List[int]) -> torch.Tensor:
+        # small index lists go through pinned memory with an async copy: no host <-> device sync
+        h = torch.tensor(values, dtype=torch.long).pin_memory() if self.device.type == "cuda" else \
+            torch.tensor(values, dtype=torch.long)
+        return h.to(self.device, non_blocking=True)
+
+    def _record(self, rows: List[int], toks: torch.Tensor):
+        """Append the sampled tokens of ``rows`` on the device: the decode input buffer and each
+        slot's output row (read back to the host once, when the request finishes)."""
+        idx = self._dev_index(rows)
+        cols = self._dev_index([self.slots[s]["n_new"] for s in rows])
+        self.tok_d.index_copy_(0, idx, toks.view(-1, 1))
+        self.out_d.index_put_((idx, cols), toks.view(-1))
+        for s in rows:
+            self.slots[s]["n_new"] += 1
 
     def _finish_done(self):
         now = time.perf_counter()
-        for s, sl in enumerate(self.slots):
-            if sl is None:
-                continue
+        done = [s for s, sl in enumerate(self.slots)
+                if sl is not None and sl["n_new"] >= sl["req"].max_new_tokens]
+        if not done:
+            return
+        outs = self.out_d[self._dev_index(done)].tolist()  # the one host sync per finished batch of requests
+        for s, row in zip(done, outs):
+            sl = self.slots[s]
             r = sl["req"]
-            if len(sl["seq"]) - len(r.tokens) >= r.max_new_tokens:
-                self.stats["requests"] += 1
-                self.stats["generated_tokens"] += r.max_new_tokens
-                sl["fut"].set_result(GenResult(tokens=sl["seq"], new_tokens=sl["seq"][len(r.tokens):],
-                                               batch_size=sl["peak_batch"], latency_ms=1e3 * (now - r.t_submit)))
-                self.slots[s] = None
+            new = row[:r.max_new_tokens]
+            self.stats["requests"] += 1
+            self.stats["generated_tokens"] += r.max_new_tokens
+            sl["fut"].set_result(GenResult(tokens=list(r.tokens) + new, new_tokens=new, batch_size=sl["peak_batch"],
+                                           latency_ms=1e3 * (now - r.t_submit)))
+            self.slots[s] = None
 
     def _admit(self, block: bool):
         while any(sl is None for sl in self.slots):
             try:
                 it = self._q.get(timeout=0.05) if block else self._q.get_nowait()
             except queue.Empty:
-                return
+                break
             block = False
             if it is None:
                 self._stop.set()
-                return
+                break
             req, fut = it
             s = self.slots.index(None)
             try:
                 gen = None
                 if req.seed is not None:
                     gen = torch.Generator(device=self.device).manual_seed(int(req.seed))
-                self.slots[s] = {"req": req, "fut": fut, "seq": list(req.tokens), "pos": 0, "gen": gen,
-                                 "peak_batch": 1}
+                if req.max_new_tokens > self.out_d.shape[1]:
+                    self._grow_out(req.max_new_tokens)
+                self.slots[s] = {"req": req, "fut": fut, "pos": 0, "n_new": 0, "gen": gen, "peak_batch": 1}
                 logits, pos = self._prefill(s, req.tokens)
                 self.slots[s]["pos"] = pos
-                self.slots[s]["seq"].append(self._sample([s], logits)[0])
+                self._record([s], self._sample([s], logits))
             except Exception as e:  # a bad request fails alone
                 self.slots[s] = None
                 fut.set_exception(e)
         self._finish_done()
+
+    def _grow_out(self, n: int):
+        out = torch.zeros(self.B, n, dtype=torch.long, device=self.device)
+        out[:, :self.out_d.shape[1]] = self.out_d
+        self.out_d = out
+
+    def _history(self, s: int) -> List[int]:
+        sl = self.slots[s]
+        return list(sl["req"].tokens) + self.out_d[s, :sl["n_new"]].tolist()
 
     def _step(self):
         from .generate import forward_decode
@@ -358,27 +395,23 @@ class ContinuousGenerationServer:
         for s in active:
             sl = self.slots[s]
             if self.learned and sl["pos"] >= self.ctx:  # crop semantics: re-prefill the last ctx tokens
-                logits, sl["pos"] = self._prefill(s, sl["seq"])
-                sl["seq"].append(self._sample([s], logits)[0])
+                logits, sl["pos"] = self._prefill(s, self._history(s))
+                self._record([s], self._sample([s], logits))
             else:
                 shared.append(s)
         if shared:
-            tok = [0] * self.B
             pos = [0] * self.B  # idle slots decode a dummy token at row 0 (overwritten by their next prefill)
             for s in shared:
-                tok[s] = self.slots[s]["seq"][-1]
                 pos[s] = self.slots[s]["pos"]
-            tok_t = torch.tensor(tok, dtype=torch.long).view(self.B, 1).to(self.device, non_blocking=True)
-            pos_t = torch.tensor(pos, dtype=torch.long).to(self.device, non_blocking=True)
+            pos_t = self._dev_index(pos)
             with torch.no_grad():
                 if self.graph is not None:
-                    logits = self.graph(tok_t, pos_t)
+                    logits = self.graph(self.tok_d, pos_t)
                 else:
-                    logits = forward_decode(self.model, tok_t, self.cache, pos_t, (pos_t + 1).to(torch.int32))
-            rows = torch.tensor(shared, device=logits.device)
-            nxt = self._sample(shared, logits.index_select(0, rows))
-            for s, t in zip(shared, nxt):
-                self.slots[s]["seq"].append(t)
+                    logits = forward_decode(self.model, self.tok_d, self.cache, pos_t, (pos_t + 1).to(torch.int32))
+            sel = logits if len(shared) == self.B else logits.index_select(0, self._dev_index(shared))
+            self._record(shared, self._sample(shared, sel))
+            for s in shared:
                 self.slots[s]["pos"] += 1
             self.stats["decode_steps"] += 1
         self._finish_done()
