@@ -105,3 +105,30 @@ def test_continuous_batching_rejects_and_closes():
         srv.close()
     with pytest.raises(RuntimeError):
         srv.submit(GenRequest([1], max_new_tokens=1))
+
+
+def test_http_app_continuous(model):
+    pytest.importorskip("httpx")
+    from fastapi.testclient import TestClient
+
+    from pretraining_llm_amd.data.tokenizer import ByteTokenizer
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer
+    srv = ContinuousGenerationServer(model, max_batch=4)
+    try:
+        client = TestClient(create_app(srv, ByteTokenizer()))
+        outs = {}
+
+        def call(i):
+            outs[i] = client.post("/generate", json={"tokens": list(range(1, 3 + i)), "max_new_tokens": 4 + i,
+                                                     "temperature": 0.0}).json()
+        ts = [threading.Thread(target=call, args=(i,)) for i in range(4)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        for i in range(4):
+            ref = model.generate(torch.tensor([list(range(1, 3 + i))]), max_new_tokens=4 + i, temperature=0.0)
+            assert outs[i]["tokens"] == ref[0, 2 + i:].tolist()
+        assert client.get("/stats").json()["requests"] == 4
+    finally:
+        srv.close()
