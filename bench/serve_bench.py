@@ -64,7 +64,10 @@ def main():
         t0 = time.perf_counter()
         res = [f.result() for f in [cs.submit(GenRequest(p, max_new_tokens=a.new, temperature=0.8)) for p in mixed]]
         dt = time.perf_counter() - t0
+        assert all(len(r.new_tokens) == a.new for r in res)
+        lat = sorted(r.latency_ms for r in res)
         print(json.dumps({"mode": "continuous_mixed_lengths", "requests": a.requests, "new_tokens": a.new,
+                          "latency_ms_min_max": [round(lat[0], 1), round(lat[-1], 1)],
                           "wall_s": round(dt, 3), "tokens_per_s": round(a.requests * a.new / dt, 1),
                           "max_active_slots": cs.stats["max_active_slots"], "decode_steps": cs.stats["decode_steps"],
                           "p50_latency_ms": round(sorted(r.latency_ms for r in res)[len(res) // 2], 1)}), flush=True)

@@ -40,8 +40,11 @@ class KVCache:
 
 
 @torch.no_grad()
-def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.Tensor:
-    """Run tokens ``idx`` [B, T] at absolute positions pos..pos+T-1; returns logits of the last position."""
+def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int,
+                   last: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Run tokens ``idx`` [B, T] at absolute positions pos..pos+T-1; returns logits of the last position
+    (or, with ``last`` [B] int64, of row b's position last[b]: right-padded prompts of different
+    lengths in one batch -- causal attention keeps every real token blind to the padding after it)."""
     cfg = model.config
     wpe = model.position_embed.weight if model.position_embed is not None else None
     x = ops.embedding(idx, model.token_embed.weight, wpe, pos_offset=pos)
@@ -50,8 +53,13 @@ def forward_cached(model, idx: torch.Tensor, cache: KVCache, pos: int) -> torch.
     for i, blk in enumerate(model.attn_blocks):
         x, res = blk.forward_cached(x, res, cache, i, pos, rope)
     # only the last position's logits are needed: norm + head on that row alone
-    logits, _ = model.layer_norm.linear(x[:, -1:], res[:, -1:] if res is not None else None,
-                                        model.head_weight, model.head_bias)
+    if last is not None:
+        rows = torch.arange(x.shape[0], device=x.device)
+        xl = x[rows, last].unsqueeze(1)
+        rl = res[rows, last].unsqueeze(1) if res is not None else None
+    else:
+        xl, rl = x[:, -1:], (res[:, -1:] if res is not None else None)
+    logits, _ = model.layer_norm.linear(xl, rl, model.head_weight, model.head_bias)
     return logits[:, -1, :].float()
 
 

@@ -285,6 +285,29 @@ class ContinuousGenerationServer:
         view.max_len = self.max_len
         return view
 
+    def _prefill_batch(self, slots: List[int], prompts: List[List[int]]) -> torch.Tensor:
+        """Prefill several requests in ONE forward: prompts right-padded to the longest (causal
+        attention keeps real tokens blind to the padding behind them; the padded K/V rows sit past
+        each slot's key count and are overwritten by its decode steps), run into a temporary cache
+        and scattered into the slots' cache rows.  Returns the logits at each prompt's last token."""
+        from .generate import KVCache, forward_cached
+        T = max(len(p) for p in prompts)
+        n = len(prompts)
+        idx = torch.zeros(n, T, dtype=torch.long)
+        for i, p in enumerate(prompts):
+            idx[i, :len(p)] = torch.tensor(p, dtype=torch.long)
+        last = torch.tensor([len(p) - 1 for p in prompts], dtype=torch.long, device=self.device)
+        cfg = self.model.config
+        tmp = KVCache(cfg.n_blocks, n, T, cfg.n_kv_head, cfg.head_dim, self.cache.k[0].dtype, self.device)
+        self.stats["prefills"] += 1
+        with torch.no_grad():
+            logits = forward_cached(self.model, idx.to(self.device), tmp, 0, last=last)
+            sl = torch.tensor(slots, dtype=torch.long, device=self.device)
+            for layer in range(cfg.n_blocks):
+                self.cache.k[layer][sl, :T] = tmp.k[layer]
+                self.cache.v[layer][sl, :T] = tmp.v[layer]
+        return logits
+
     def _prefill(self, s: int, tokens: List[int]) -> torch.Tensor:
         from .generate import forward_cached
         window = tokens[-self.ctx:] if self.learned else tokens
@@ -348,6 +371,7 @@ class ContinuousGenerationServer:
             self.slots[s] = None
 
     def _admit(self, block: bool):
+        admitted = []
         while any(sl is None for sl in self.slots):
             try:
                 it = self._q.get(timeout=0.05) if block else self._q.get_nowait()
@@ -365,14 +389,37 @@ class ContinuousGenerationServer:
                     gen = torch.Generator(device=self.device).manual_seed(int(req.seed))
                 if req.max_new_tokens > self.out_d.shape[1]:
                     self._grow_out(req.max_new_tokens)
-                self.slots[s] = {"req": req, "fut": fut, "pos": 0, "n_new": 0, "gen": gen, "peak_batch": 1}
-                logits, pos = self._prefill(s, req.tokens)
-                self.slots[s]["pos"] = pos
-                self._record([s], self._sample([s], logits))
+                window = req.tokens[-self.ctx:] if self.learned else req.tokens
+                self.slots[s] = {"req": req, "fut": fut, "pos": len(window), "n_new": 0, "gen": gen,
+                                 "peak_batch": 1, "window": window}
+                admitted.append(s)
             except Exception as e:  # a bad request fails alone
                 self.slots[s] = None
                 fut.set_exception(e)
+        # prefill the newly admitted requests together, in batches of similar length (right padding
+        # wastes at most PREFILL_PAD_FRACTION of a batch's tokens)
+        admitted.sort(key=lambda s: len(self.slots[s]["window"]))
+        i = 0
+        while i < len(admitted):
+            j = i + 1
+            while j < len(admitted):
+                L = len(self.slots[admitted[j]]["window"])
+                real = sum(len(self.slots[s]["window"]) for s in admitted[i:j + 1])
+                if real < (1.0 - self.PREFILL_PAD_FRACTION) * L * (j + 1 - i):
+                    break
+                j += 1
+            group = admitted[i:j]
+            try:
+                logits = self._prefill_batch(group, [self.slots[s]["window"] for s in group])
+                self._record(group, self._sample(group, logits))
+            except Exception as e:
+                for s in group:
+                    self.slots[s]["fut"].set_exception(e)
+                    self.slots[s] = None
+            i = j
         self._finish_done()
+
+    PREFILL_PAD_FRACTION = 0.25
 
     def _grow_out(self, n: int):
         out = torch.zeros(self.B, n, dtype=torch.long, device=self.device)
