@@ -23,6 +23,9 @@ TUNING_DIR = os.environ.get("PLLM_TUNING_DIR") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
 
 
+_DEFAULT_DIR = None
+
+
 def _merge_tables(dst: str):
     """Concatenate all shipped tables into one TunableOp CSV (validators once, results deduplicated)."""
     validators, results, seen = [], [], set()
@@ -56,7 +59,13 @@ def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_di
         import torch.cuda.tunable as tunable
     except Exception:
         return False
-    out_dir = out_dir or tempfile.mkdtemp(prefix="pllm_tunableop_")
+    global _DEFAULT_DIR
+    if out_dir is None:  # one scratch dir per process (a Trainer per test / run reuses it)
+        if _DEFAULT_DIR is None:
+            _DEFAULT_DIR = tempfile.mkdtemp(prefix="pllm_tunableop_")
+            import atexit
+            atexit.register(shutil.rmtree, _DEFAULT_DIR, True)
+        out_dir = _DEFAULT_DIR
     base = os.path.join(out_dir, "tunableop.csv")
     # TunableOp reads/writes "<stem><device>.csv" per device ordinal
     per_dev = os.path.join(out_dir, f"tunableop{device_index}.csv")
