@@ -60,11 +60,9 @@ def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_di
     except Exception:
         return False
     global _DEFAULT_DIR
-    if out_dir is None:  # one scratch dir per process (a Trainer per test / run reuses it)
-        if _DEFAULT_DIR is None:
+    if out_dir is None:  # one scratch dir per process (every Trainer / bench of the process reuses it)
+        if _DEFAULT_DIR is None:  # (kept at exit: TunableOp may flush tuned results into it then)
             _DEFAULT_DIR = tempfile.mkdtemp(prefix="pllm_tunableop_")
-            import atexit
-            atexit.register(shutil.rmtree, _DEFAULT_DIR, True)
         out_dir = _DEFAULT_DIR
     base = os.path.join(out_dir, "tunableop.csv")
     # TunableOp reads/writes "<stem><device>.csv" per device ordinal
