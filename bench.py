@@ -71,6 +71,14 @@ def _free_port() -> int:
     return port
 
 
+def _rccl_version():
+    try:
+        import torch
+        return ".".join(str(v) for v in torch.cuda.nccl.version())
+    except Exception:  # informational only: never fail a measured run over it
+        return None
+
+
 def launch_ranks(args, argv) -> int:
     """``--gpus N`` without a torchrun environment: start N ranks (one process per GPU,
     RCCL) through ``torch.distributed.run`` as a CHILD process -- this process never
@@ -213,8 +221,7 @@ def main(argv=None):
             "final_loss": round(final_loss, 4),
             "peak_mem_gb": None if cpu else round(torch.cuda.max_memory_allocated(dev) / 1e9, 2),
             "comm": {"backend": di.backend if world > 1 else None, "world": world,
-                     "rccl_version": (".".join(str(v) for v in torch.cuda.nccl.version())
-                                      if (not cpu and world > 1 and di.backend == "nccl") else None),
+                     "rccl_version": _rccl_version() if (not cpu and world > 1 and di.backend == "nccl") else None,
                      "n_buckets": len(getattr(engine, "buckets", [])),
                      "bucket_mb": [round(b, 2) for b in engine.bucket_sizes_mb()]
                      if hasattr(engine, "bucket_sizes_mb") else None,
