@@ -53,8 +53,8 @@ default_config = {
 
     # --- keys the reference scripts read but never defined ---------------
     'ddp_backend': 'nccl',            # = RCCL on ROCm (train_transformer.py:17)
-    'dtype': 'bfloat16',              # bfloat16 (HIP kernels) | float16 (fp16 autocast + loss scaling) | float32 (train/amp.py)
-    'loss_scaling': None,             # dynamic loss scaling (GradScaler semantics); None = on iff dtype == 'float16'
+    'dtype': 'bfloat16',              # bfloat16 (HIP kernels) | float16 (reference: bf16 compute + loss scaling) | float16_autocast (true fp16, torch ops) | float32 (train/amp.py)
+    'loss_scaling': None,             # dynamic loss scaling (GradScaler semantics); None = on iff dtype is float16 / float16_autocast
     'loss_scale_init': 65536.0,
     'loss_scale_growth_interval': 2000,
     'val_path': DEV_PATH,             # alias of dev_path (train_transformer.py:134)

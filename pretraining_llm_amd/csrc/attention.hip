@@ -143,6 +143,15 @@ struct Img {
   }
   // element offset of (row, col); col's 8-aligned chunk is swizzled, col&7 kept
   static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+  // a row's two RoPE-partner halves (chunks c and c + W/16) stored so that every 8-lane group
+  // of ds_write_b128 (bank = byte address mod 128) covers 128 distinct bytes: at W = 64 rows 2k
+  // and 2k+1 share f, so an odd row stores its upper half first (same image, same reads)
+  static PLLM_DEV void st_pair(uint16_t* base, int r, int c, const u32x4& lo, const u32x4& hi) {
+    constexpr int H = W / 16;
+    const bool sw = W == 64 && (r & 1);
+    st16(base + off(r, (sw ? c + H : c) * 8), sw ? hi : lo);
+    st16(base + off(r, (sw ? c : c + H) * 8), sw ? lo : hi);
+  }
 };
 
 // ============================================================================
@@ -256,10 +265,8 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
         const int64_t tab = (int64_t)min(key, a.S - 1) * (D / 2) + col * 8;
         rope8(kr[i], kr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
       }
-      st16(Kb + I::off(row, col * 8), kr[i]);
-      st16(Kb + I::off(row, (col + CPR2) * 8), kr[i + 1]);
-      st16(Vb + I::off(row, col * 8), vr[i]);
-      st16(Vb + I::off(row, (col + CPR2) * 8), vr[i + 1]);
+      I::st_pair(Kb, row, col, kr[i], kr[i + 1]);
+      I::st_pair(Vb, row, col, vr[i], vr[i + 1]);
     }
   };
 
@@ -512,8 +519,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
           rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
       }
-      st16(Kl + I::off(row, col * 8), lo);
-      st16(Kl + I::off(row, (col + CPR2) * 8), hi);
+      I::st_pair(Kl, row, col, lo, hi);
     }
   }
 
@@ -643,10 +649,8 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
           const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
           rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
-        st16(Ql + I::off(row, col * 8), qr[i]);
-        st16(Ql + I::off(row, (col + CPR2) * 8), qr[i + 1]);
-        st16(Ol + I::off(row, col * 8), dor[i]);
-        st16(Ol + I::off(row, (col + CPR2) * 8), dor[i + 1]);
+        I::st_pair(Ql, row, col, qr[i], qr[i + 1]);
+        I::st_pair(Ol, row, col, dor[i], dor[i + 1]);
       }
     }
     if (tid < 2 * BQ) {
@@ -942,8 +946,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
           rope8(lo, hi, a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
       }
-      st16(Kl + I::off(row, col * 8), lo);
-      st16(Kl + I::off(row, (col + CPR2) * 8), hi);
+      I::st_pair(Kl, row, col, lo, hi);
     }
   }
   vm_wait_all();
@@ -1036,10 +1039,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
           const int64_t tab = (int64_t)(q0 + row + off) * (D / 2) + col * 8;
           rope8(qr[i], qr[i + 1], a.rope_cos + tab, a.rope_sin + tab, 1.f);
         }
-        st16(Ql + I::off(row, col * 8), qr[i]);
-        st16(Ql + I::off(row, (col + CPR2) * 8), qr[i + 1]);
-        st16(Ol + I::off(row, col * 8), dor[i]);
-        st16(Ol + I::off(row, (col + CPR2) * 8), dor[i + 1]);
+        I::st_pair(Ql, row, col, qr[i], qr[i + 1]);
+        I::st_pair(Ol, row, col, dor[i], dor[i + 1]);
       }
     }
     if (tid < 2 * BQ) {

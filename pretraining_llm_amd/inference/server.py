@@ -36,8 +36,11 @@ class GenRequest:
     t_submit: float = field(default_factory=time.perf_counter)
 
     def group_key(self):
-        # sequences decode in lockstep: one prompt length, one number of steps, one sampler
-        return (len(self.tokens), self.max_new_tokens, float(self.temperature), self.top_k, self.seed)
+        # sequences decode in lockstep: one prompt length, one number of steps, one sampler.  A
+        # seeded request is never batched with another: its tokens must not depend on its row or
+        # on its batch-mates, so it decodes alone with its own generator (= single-request generate)
+        private = id(self) if self.seed is not None else None
+        return (len(self.tokens), self.max_new_tokens, float(self.temperature), self.top_k, self.seed, private)
 
 
 @dataclass
@@ -60,6 +63,7 @@ class GenerationServer:
         self._q = queue.Queue()
         self._decode_cache = {}  # (batch, cache length) -> KV cache + captured decode graph, reused
         self._stop = threading.Event()
+        self._submit_lock = threading.Lock()
         self.stats: Dict[str, float] = {"requests": 0, "batches": 0, "generated_tokens": 0, "max_batch_seen": 0}
         self._worker = threading.Thread(target=self._run, name="pllm-generation", daemon=True)
         self._worker.start()
@@ -75,15 +79,17 @@ class GenerationServer:
             raise ValueError("token id outside the vocabulary")
         if self.model.config.pos != "learned" and len(req.tokens) + req.max_new_tokens > 8 * ctx:
             raise ValueError("prompt + max_new_tokens too long")
-        if self._stop.is_set():
-            raise RuntimeError("generation server closed")
         fut: Future = Future()
-        self._q.put((req, fut))
+        with self._submit_lock:  # no request can be queued behind close()'s stop marker
+            if self._stop.is_set():
+                raise RuntimeError("generation server closed")
+            self._q.put((req, fut))
         return fut
 
     def close(self):
-        self._stop.set()
-        self._q.put(None)
+        with self._submit_lock:
+            self._stop.set()
+            self._q.put(None)
         self._worker.join(timeout=30)
         while True:  # requests still queued behind the stop marker fail instead of waiting forever
             try:
@@ -243,6 +249,7 @@ class ContinuousGenerationServer:
         self.out_d = torch.zeros(self.B, 256, dtype=torch.long, device=self.device)
         self._q = queue.Queue()
         self._stop = threading.Event()
+        self._submit_lock = threading.Lock()
         self.stats: Dict[str, float] = {"requests": 0, "decode_steps": 0, "generated_tokens": 0,
                                         "max_active_slots": 0, "prefills": 0}
         self._worker = threading.Thread(target=self._run, name="pllm-continuous-batching", daemon=True)
@@ -250,8 +257,6 @@ class ContinuousGenerationServer:
 
     # ------------------------------------------------------------------ API (as GenerationServer)
     def submit(self, req: GenRequest) -> Future:
-        if self._stop.is_set():
-            raise RuntimeError("generation server closed")
         if not req.tokens:
             raise ValueError("empty prompt")
         if req.max_new_tokens < 1:
@@ -261,12 +266,16 @@ class ContinuousGenerationServer:
         if not self.learned and len(req.tokens) + req.max_new_tokens > self.max_len:
             raise ValueError(f"prompt + max_new_tokens exceeds the server's cache length {self.max_len}")
         fut: Future = Future()
-        self._q.put((req, fut))
+        with self._submit_lock:
+            if self._stop.is_set():
+                raise RuntimeError("generation server closed")
+            self._q.put((req, fut))
         return fut
 
     def close(self):
-        self._stop.set()
-        self._q.put(None)
+        with self._submit_lock:
+            self._stop.set()
+            self._q.put(None)
         self._worker.join(timeout=60)
         while True:
             try:
@@ -354,12 +363,14 @@ class ContinuousGenerationServer:
             self.slots[s]["n_new"] += 1
 
     def _finish_done(self):
-        now = time.perf_counter()
         done = [s for s, sl in enumerate(self.slots)
                 if sl is not None and sl["n_new"] >= sl["req"].max_new_tokens]
         if not done:
             return
         outs = self.out_d[self._dev_index(done)].tolist()  # the one host sync per finished batch of requests
+        # stamped AFTER the read-back: decode steps are enqueued asynchronously, so only the sync
+        # above says the tokens exist (a stamp before it measured host enqueue time)
+        now = time.perf_counter()
         for s, row in zip(done, outs):
             sl = self.slots[s]
             r = sl["req"]

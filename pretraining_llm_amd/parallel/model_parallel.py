@@ -321,43 +321,57 @@ def sync_replicated_grads(optimizer, pg: ParallelGroups):
 @torch.no_grad()
 def gather_dense_state(model, dense_model, pg: ParallelGroups, masters: Optional[dict] = None):
     """COLLECTIVE over the TP group: assemble the dense weights of a TP-sharded ``model`` into
-    ``dense_model`` (same config, built dense); ``masters`` maps local parameter -> fp32 value
-    to gather instead of the compute copy.  Returns ``dense_model``."""
-    src = dict(model.named_parameters())
+    ``dense_model`` (same config, built dense -- on any device, e.g. the CPU); ranks that only
+    contribute their shards pass ``dense_model=None``.  ``masters`` maps local parameter -> fp32
+    value to gather instead of the compute copy.  The gathers run one parameter at a time on the
+    parameters' own device, so no rank holds more than one dense tensor on the GPU.  Returns
+    ``dense_model``."""
+    dst = dict(dense_model.named_parameters()) if dense_model is not None else None
     g = pg.tp_group
 
-    def val(p):
-        return masters.get(id(p), p).float() if masters else p.float()
-
-    def gather(t, dim):
+    def gather(t):
         parts = [torch.empty_like(t) for _ in range(pg.tp)]
         dist.all_gather(parts, t.contiguous(), group=g)
         return parts
 
     cfg = model.config
-    for name, dp_ in dense_model.named_parameters():
-        p = src[name]
-        v = val(p).to(dp_.device)
+    for name, p in model.named_parameters():  # identical order on every TP rank
+        v = (masters.get(id(p), p) if masters else p).to(device=p.device, dtype=torch.float32)
         if not getattr(p, "_pllm_tp_sharded", False):
-            dp_.copy_(v)
-            continue
-        if name.endswith("attn.qkv.weight") or name.endswith("attn.qkv.bias"):
+            full = v
+        elif name.endswith("attn.qkv.weight") or name.endswith("attn.qkv.bias"):
             H, Hkv, D = cfg.n_head, cfg.n_kv_head, cfg.head_dim
             Hl, Hkl = H // pg.tp, Hkv // pg.tp
-            parts = gather(v, 0)
-            qs = [x[:Hl * D] for x in parts]
-            ks = [x[Hl * D:(Hl + Hkl) * D] for x in parts]
-            vs = [x[(Hl + Hkl) * D:] for x in parts]
-            dp_.copy_(torch.cat(qs + ks + vs, 0))
+            parts = gather(v)
+            full = torch.cat([x[:Hl * D] for x in parts] + [x[Hl * D:(Hl + Hkl) * D] for x in parts] +
+                             [x[(Hl + Hkl) * D:] for x in parts], 0)
         elif name.endswith("mlp.hidden.weight") or name.endswith("mlp.hidden.bias"):
-            parts = gather(v, 0)
+            parts = gather(v)
             if cfg.mlp == "swiglu":
                 Fl = cfg.ffn_hidden // pg.tp
-                dp_.copy_(torch.cat([x[:Fl] for x in parts] + [x[Fl:] for x in parts], 0))
+                full = torch.cat([x[:Fl] for x in parts] + [x[Fl:] for x in parts], 0)
             else:
-                dp_.copy_(torch.cat(parts, 0))
+                full = torch.cat(parts, 0)
         elif name.endswith("proj.weight"):  # row-parallel: sharded along the input columns
-            dp_.copy_(torch.cat(gather(v, 1), 1))
+            full = torch.cat(gather(v), 1)
         else:
             raise RuntimeError(f"no unsharding rule for {name}")
+        if dst is not None:
+            dst[name].copy_(full)
+        del full
     return dense_model
+
+
+def build_dense_shell(cfg, device="cpu"):
+    """An uninitialised dense ``GPT`` of ``cfg`` on ``device`` (default: host memory) for a
+    consolidated checkpoint: built on the meta device and materialised with ``to_empty``, so it
+    draws nothing from any RNG stream (a saving rank's RNG stays in step with the others) and
+    costs no GPU memory."""
+    from ..models import GPT
+    with torch.random.fork_rng(devices=[]):
+        with torch.device("meta"):
+            m = GPT(cfg)
+    m = m.to_empty(device=device).float()
+    if getattr(m, "pos_idxs", None) is not None:  # the one persistent buffer (reference layout)
+        m.pos_idxs.copy_(torch.arange(m.pos_idxs.numel()))
+    return m

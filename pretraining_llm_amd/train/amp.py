@@ -9,11 +9,14 @@ Here (``Trainer``):
 
 * ``dtype='bfloat16'`` (default): bf16 weights on the hand-written HIP kernels, fp32 master
   weights and gradients (train/optim.py).  No loss scaling (bf16 has fp32's exponent range).
-* ``dtype='float16'``: fp32 weights, forward under ``torch.autocast(float16)`` (fp16 GEMMs on
-  hipBLASLt through torch; the hand-written kernels are bf16-only) and dynamic loss scaling.
+* ``dtype='float16'``: what the reference's ``float16`` setting does -- bf16 compute (here the
+  bf16 HIP path, as ``'bfloat16'``) WITH dynamic loss scaling.
+* ``dtype='float16_autocast'`` (explicit opt-in, no reference counterpart): true fp16 numerics,
+  fp32 weights, forward under ``torch.autocast(float16)`` (fp16 GEMMs on hipBLASLt through torch;
+  the hand-written kernels are bf16-only, so this mode is much slower) and dynamic loss scaling.
 * ``dtype='float32'``: fp32 weights and compute through torch.
-* ``loss_scaling`` (None = on iff ``dtype='float16'``) switches the scaler on explicitly, e.g.
-  with the bf16 HIP path to reproduce the reference's bf16-compute + GradScaler combination.
+* ``loss_scaling`` (None = on iff ``dtype`` is ``'float16'`` or ``'float16_autocast'``) switches
+  the scaler on or off explicitly.
 
 ``DynamicLossScaler`` has ``GradScaler``'s semantics (scale 2^16, x2 after 2000 clean steps,
 x0.5 and a skipped optimizer step on an inf/nan gradient) but works on the optimizer's flat
@@ -85,16 +88,24 @@ class DynamicLossScaler:
         self.growth_tracker = int(sd.get("_growth_tracker", self.growth_tracker))
 
 
+DTYPES = ("bfloat16", "float16", "float16_autocast", "float32")
+
+
+def loss_scaling_default(dtype_name: str) -> bool:
+    """The reference's ``GradScaler(enabled=dtype == 'float16')`` (train_transformer.py:41)."""
+    return dtype_name in ("float16", "float16_autocast")
+
+
 def precision_mode(dtype_name: str, device: torch.device, cpu_bf16: bool = False):
     """-> (parameter dtype, autocast dtype or None) for a training ``dtype`` setting."""
-    if dtype_name not in ("bfloat16", "float16", "float32"):
-        raise ValueError(f"dtype={dtype_name!r}: expected 'bfloat16', 'float16' or 'float32'")
+    if dtype_name not in DTYPES:
+        raise ValueError(f"dtype={dtype_name!r}: expected one of {DTYPES}")
     if device.type == "cpu":
         # CPU runs are the fp32 numerics reference (cpu_bf16 for bf16 plumbing checks)
-        return (torch.bfloat16 if cpu_bf16 and dtype_name == "bfloat16" else torch.float32), None
-    if dtype_name == "bfloat16":
+        return (torch.bfloat16 if cpu_bf16 and dtype_name in ("bfloat16", "float16") else torch.float32), None
+    if dtype_name in ("bfloat16", "float16"):  # float16 = the reference's bf16 compute + GradScaler
         return torch.bfloat16, None
-    if dtype_name == "float16":
+    if dtype_name == "float16_autocast":
         return torch.float32, torch.float16
     return torch.float32, None
 

@@ -185,8 +185,19 @@ class FlatAdamW:
         sharded parameters over the TP group and counts the replicated ones (norms, embeddings,
         LM head, row-parallel biases -- identical on every TP rank) once."""
         self.tp_group, self.tp = group, tp
-        self._rep_ranges = [(self.offsets[i], self.offsets[i] + p.numel()) for i, p in enumerate(self.params)
-                            if not getattr(p, "_pllm_tp_sharded", False)]
+        # replicated segments rounded up to ALIGN (the padding of the flat gradient is always
+        # zero) and merged where adjacent: every range starts and ends on a 64-element boundary
+        # (the HIP sum of squares needs numel % 8 == 0) and there are few of them
+        runs = []
+        for i, p in enumerate(self.params):
+            if getattr(p, "_pllm_tp_sharded", False):
+                continue
+            a, b = self.offsets[i], self.offsets[i] + _round_up(p.numel(), ALIGN)
+            if runs and runs[-1][1] == a:
+                runs[-1][1] = b
+            else:
+                runs.append([a, b])
+        self._rep_ranges = [(a, b) for a, b in runs]
 
     def replicated_grad_ranges(self):
         """(buffer the optimizer step reads, [(start, end)] of the TP-replicated parameters in it)."""
@@ -197,7 +208,8 @@ class FlatAdamW:
         global one: replicated ranges weighted 1/tp, so a SUM over the TP group counts them once."""
         buf, ranges = self.replicated_grad_ranges()
         if ranges:
-            rep = self._sumsq(torch.cat([buf[a:b] for a, b in ranges]))
+            # one reduction per contiguous run, no concatenated copy of the replicated gradients
+            rep = torch.stack([self._sumsq(buf[a:b]) for a, b in ranges]).sum(0)
             ss = ss - rep * (1.0 - 1.0 / self.tp)
         return ss
 

@@ -31,10 +31,10 @@ from .. import ops
 from ..data import TokenLoader, ensure_synthetic_shard
 from ..models import GPT, ModelConfig, get_preset
 from ..parallel.dp import DataParallelEngine, all_reduce_mean
-from ..parallel.model_parallel import (gather_dense_state, init_parallel_groups, parallelize_gpt,
-                                       sync_replicated_grads)
+from ..parallel.model_parallel import (build_dense_shell, gather_dense_state, init_parallel_groups,
+                                       parallelize_gpt, sync_replicated_grads)
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
-from .amp import DynamicLossScaler, autocast_ctx, precision_mode
+from .amp import DynamicLossScaler, autocast_ctx, loss_scaling_default, precision_mode
 from ..utils.dist import DistInfo, init_distributed
 from ..utils.metrics import MetricsLogger, mfu, peak_memory_gb
 from .optim import FlatAdamW, no_decay_1d
@@ -84,14 +84,15 @@ class Trainer:
             torch.use_deterministic_algorithms(True, warn_only=True)
         self.mcfg = model_config_from(self.cfg)
         self.seq_len = int(self.cfg.get("seq_len") or self.mcfg.context_length)
-        # precision (train/amp.py): bf16 on the HIP kernels; float16 = fp32 weights + fp16 autocast
-        # + dynamic loss scaling; float32 = fp32 through torch
+        # precision (train/amp.py): bf16 on the HIP kernels; float16 = the reference's bf16 compute
+        # + dynamic loss scaling; float16_autocast = fp32 weights + fp16 autocast + loss scaling
+        # (opt-in, torch ops); float32 = fp32 through torch
         dtype_name = self.cfg.get("dtype", "bfloat16")
         self.dtype, self.autocast_dtype = precision_mode(dtype_name, self.device, bool(self.cfg.get("cpu_bf16", False)))
         ls = self.cfg.get("loss_scaling")
         self.scaler = DynamicLossScaler(init_scale=float(self.cfg.get("loss_scale_init", 2.0 ** 16)),
                                         growth_interval=int(self.cfg.get("loss_scale_growth_interval", 2000)),
-                                        enabled=(dtype_name == "float16") if ls is None else bool(ls))
+                                        enabled=loss_scaling_default(dtype_name) if ls is None else bool(ls))
         self.tuned_gemms = False
         if self.device.type == "cuda" and self.cfg.get("tuned_gemms", True):
             # the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/), as bench.py uses them
@@ -373,11 +374,18 @@ class Trainer:
             save_checkpoint(f"{path}.tp{pg.tp_rank}", self.model, optimizer_state=osd, params=self.opt.params,
                             step=self.step, config=self.cfg, data_state=data_state,
                             extra={"tp_rank": pg.tp_rank, "tp_size": pg.tp, **self._scaler_extra()})
-            masters = None
-            if not getattr(self.opt, "collective_state", False):
+            # fp32 masters in the consolidated file on both optimizer paths: FlatAdamW's own
+            # buffer, or (ZeRO) the consolidated state the writer ranks just gathered
+            if getattr(self.opt, "collective_state", False):
+                st = osd.get("state", {})
+                masters = {id(p): st[i]["master"].reshape(p.shape) for i, p in enumerate(self.opt.params)
+                           if i in st and "master" in st[i]}
+            else:
                 masters = {id(p): self.opt.master[self.opt.offsets[i]:self.opt.offsets[i] + p.numel()].view(p.shape)
                            for i, p in enumerate(self.opt.params)}
-            dense = GPT(self.mcfg).to(device=self.device, dtype=torch.float32)
+            # only global rank 0 materialises the dense model, in host memory, from no RNG draw
+            # (parallel/model_parallel.py build_dense_shell); the other writers just contribute
+            dense = build_dense_shell(self.mcfg) if self.di.is_master else None
             gather_dense_state(self.model, dense, pg, masters)
             if self.di.is_master:
                 save_checkpoint(path, dense, step=self.step, config=self.cfg, data_state=data_state,

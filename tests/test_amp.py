@@ -36,7 +36,8 @@ def test_precision_modes():
     from pretraining_llm_amd.train.amp import precision_mode
     cuda, cpu = torch.device("cuda", 0), torch.device("cpu")
     assert precision_mode("bfloat16", cuda) == (torch.bfloat16, None)
-    assert precision_mode("float16", cuda) == (torch.float32, torch.float16)
+    assert precision_mode("float16", cuda) == (torch.bfloat16, None)  # the reference's bf16 + GradScaler
+    assert precision_mode("float16_autocast", cuda) == (torch.float32, torch.float16)
     assert precision_mode("float32", cuda) == (torch.float32, None)
     assert precision_mode("bfloat16", cpu) == (torch.float32, None)
     assert precision_mode("bfloat16", cpu, cpu_bf16=True) == (torch.bfloat16, None)
@@ -105,23 +106,25 @@ def test_overflow_skips_step_and_backs_off(tmp_path):
 
 @pytest.mark.gpu
 def test_fp16_and_fp32_modes_train_on_gpu(tmp_path):
-    """dtype float16 (fp32 weights, fp16 autocast, dynamic loss scaling) and float32 train the
-    GPT-2 tiny config on the GPU and track the bf16 HIP-kernel run."""
+    """dtype float16 (the reference's: bf16 HIP path + dynamic loss scaling), float16_autocast (fp32
+    weights, fp16 autocast, loss scaling) and float32 train the GPT-2 tiny config on the GPU and
+    track the bf16 HIP-kernel run."""
     import json
     from pretraining_llm_amd.train import Trainer
     finals = {}
-    for dt in ("bfloat16", "float16", "float32"):
+    for dt in ("bfloat16", "float16", "float16_autocast", "float32"):
         d = tmp_path / dt
         tr = Trainer(_cfg(d, device="cuda", dtype=dt, t_train_steps=60, t_eval_steps=30, log_interval=10,
                           t_batch_size=8, seq_len=128, metrics_path=str(d / "m.jsonl"), t_out_path=None),
                      log=lambda *_: None)
-        assert tr.scaler.enabled == (dt == "float16")
-        assert next(tr.model.parameters()).dtype == (torch.bfloat16 if dt == "bfloat16" else torch.float32)
+        assert tr.scaler.enabled == dt.startswith("float16")
+        assert next(tr.model.parameters()).dtype == (torch.bfloat16 if dt in ("bfloat16", "float16") else torch.float32)
         tr.train()
         recs = [json.loads(l) for l in open(d / "m.jsonl")]
         assert recs[-1]["train_loss"] < recs[0]["train_loss"] - 1.0, (dt, recs[0], recs[-1])
         finals[dt] = recs[-1]["train_loss"]
-        if dt == "float16":
+        if dt.startswith("float16"):
             assert tr.scaler.scale >= 1.0
-    assert abs(finals["float16"] - finals["float32"]) < 0.05 * finals["float32"], finals
+    for dt in ("float16", "float16_autocast"):
+        assert abs(finals[dt] - finals["float32"]) < 0.05 * finals["float32"], finals
     assert abs(finals["bfloat16"] - finals["float32"]) < 0.05 * finals["float32"], finals

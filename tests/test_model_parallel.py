@@ -201,8 +201,8 @@ def _trainer_worker(rank, world, port, tmp, kw):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kw", [dict(tp_size=2, sequence_parallel=True), dict(cp_size=2),
-                                dict(cp_size=2, cp_mode="ulysses")], ids=["tp2_sp", "cp2", "ulysses2"])
+@pytest.mark.parametrize("kw", [dict(tp_size=2, sequence_parallel=True), dict(tp_size=2, zero_stage=1), dict(cp_size=2),
+                                dict(cp_size=2, cp_mode="ulysses")], ids=["tp2_sp", "tp2_zero1", "cp2", "ulysses2"])
 def test_trainer_model_parallel_matches_dense_and_resumes(tmp_path, kw):
     """Trainer with tp_size / cp_size on 2 gloo ranks: the consolidated dense checkpoint after 8
     steps equals a 1-process dense Trainer's weights on the same data, and resuming from the
@@ -220,3 +220,40 @@ def test_trainer_model_parallel_matches_dense_and_resumes(tmp_path, kw):
     m.load_state_dict(ck["model_state_dict"], strict=True)
     for (n, p), q in zip(dense.model.named_parameters(), m.parameters()):
         assert torch.allclose(p, q, atol=5e-5, rtol=1e-4), (n, (p - q).abs().max())
+
+
+def test_dense_shell_draws_no_rng_and_tp_ranges_aligned():
+    """The consolidated-checkpoint model is built without touching the RNG (a saving rank stays in
+    step with the others), and the TP-replicated gradient ranges are ALIGN-padded runs (the HIP
+    sum of squares needs numel % 8 == 0; an odd-sized replicated parameter must not break it)."""
+    import torch.nn as nn
+    from pretraining_llm_amd.models import GPT, get_preset
+    from pretraining_llm_amd.parallel.model_parallel import build_dense_shell
+    from pretraining_llm_amd.train.optim import ALIGN, FlatAdamW
+    cfg = get_preset("gpt2-tiny")
+    torch.manual_seed(3)
+    before = torch.get_rng_state()
+    m = build_dense_shell(cfg)
+    assert torch.equal(torch.get_rng_state(), before)
+    assert sum(p.numel() for p in m.parameters()) == sum(p.numel() for p in GPT(cfg).parameters())
+
+    class Odd(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Parameter(torch.randn(7))        # replicated, odd size
+            self.w = nn.Parameter(torch.randn(16, 8))    # "sharded"
+            self.b = nn.Parameter(torch.randn(5))        # replicated, odd size
+            self.c = nn.Parameter(torch.randn(3))        # replicated, adjacent to b
+    net = Odd()
+    net.w._pllm_tp_sharded = True
+    opt = FlatAdamW(net)
+    opt.set_tensor_parallel(None, 2)
+    buf, ranges = opt.replicated_grad_ranges()
+    assert all(a % ALIGN == 0 and b % ALIGN == 0 for a, b in ranges) and len(ranges) == 2
+    opt.flat_grad.normal_()
+    for i, p in enumerate(opt.params):  # padding of the flat gradient is zero, as in training
+        o = opt.offsets[i]
+        opt.flat_grad[o + p.numel():o + -(-p.numel() // ALIGN) * ALIGN].zero_()
+    ss = opt._sumsq(opt.flat_grad)
+    rep = sum(opt.grad_view(i).pow(2).sum() for i in (0, 2, 3))
+    assert torch.allclose(opt._tp_adjust(ss), ss - rep * 0.5)

@@ -132,3 +132,56 @@ def test_http_app_continuous(model):
         assert client.get("/stats").json()["requests"] == 4
     finally:
         srv.close()
+
+
+def _latency_matches_observed(srv, reqs):
+    """Submit ``reqs`` at once; every result's latency_ms must sit within 10 % of the wall time the
+    caller observes between its submit and the future completing (stamped after the host read-back,
+    never at enqueue time)."""
+    import time
+    done_at = {}
+    futs = []
+    for i, r in enumerate(reqs):
+        f = srv.submit(r)
+        f.add_done_callback(lambda _f, i=i: done_at.__setitem__(i, time.perf_counter()))
+        futs.append(f)
+    res = [f.result(timeout=300) for f in futs]
+    for i, (r, out) in enumerate(zip(reqs, res)):
+        observed = 1e3 * (done_at[i] - r.t_submit)
+        assert out.latency_ms <= observed + 1e-3 and out.latency_ms >= 0.9 * observed - 1.0, (i, out.latency_ms, observed)
+    return res
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_latency_is_wall_time(model, continuous):
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer
+    srv = ContinuousGenerationServer(model, max_batch=4) if continuous else GenerationServer(model, max_batch=8,
+                                                                                               max_wait_ms=50.0)
+    try:
+        _latency_matches_observed(srv, [GenRequest([3, 1, 4, 1 + i], max_new_tokens=6, temperature=0.0)
+                                        for i in range(6)])
+    finally:
+        srv.close()
+
+
+def test_seeded_requests_reproducible_regardless_of_batch(model):
+    """Two concurrent requests with the same seed get the same tokens as a single-request
+    generate() with that seed: seeded requests are never batched together."""
+    srv = GenerationServer(model, max_batch=8, max_wait_ms=100.0)
+    try:
+        p = [5, 9, 13, 2]
+        futs = [srv.submit(GenRequest(p, max_new_tokens=8, temperature=0.9, seed=11)) for _ in range(2)]
+        res = [f.result(timeout=120) for f in futs]
+    finally:
+        srv.close()
+    g = torch.Generator().manual_seed(11)
+    ref = model.generate(torch.tensor([p]), max_new_tokens=8, temperature=0.9, generator=g)[0].tolist()
+    assert res[0].tokens == ref and res[1].tokens == ref
+    assert all(r.batch_size == 1 for r in res)
+
+
+def test_submit_after_close_fails_fast(model):
+    srv = GenerationServer(model, max_batch=2)
+    srv.close()
+    with pytest.raises(RuntimeError):
+        srv.submit(GenRequest([1, 2], max_new_tokens=2))

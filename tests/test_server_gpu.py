@@ -82,3 +82,27 @@ def test_continuous_batching_gpu_matches_single_requests(preset):
                              cuda_graph=True)[0].tolist()
         assert r.tokens == ref, (len(p), k)
     assert srv.stats["max_active_slots"] == 4
+
+
+@pytest.mark.parametrize("continuous", [False, True])
+def test_server_gpu_latency_is_wall_time(continuous):
+    """Decode is asynchronous on the GPU: latency_ms must include the device work (stamped after the
+    host read-back), i.e. match the caller's own submit -> completion time within 10 %."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_server import _latency_matches_observed
+
+    from pretraining_llm_amd.inference.server import ContinuousGenerationServer, GenerationServer, GenRequest
+    from pretraining_llm_amd.models import GPT, get_preset
+    torch.manual_seed(0)
+    dev = torch.device("cuda", 0)
+    model = GPT(get_preset("gpt2-small").replace(context_length=256)).to(device=dev, dtype=torch.bfloat16).eval()
+    srv = ContinuousGenerationServer(model, max_batch=16, max_len=200) if continuous else \
+        GenerationServer(model, max_batch=16, max_wait_ms=50.0)
+    try:
+        srv.submit(GenRequest([1, 2, 3], max_new_tokens=4, temperature=0.0)).result(timeout=120)  # warm-up
+        _latency_matches_observed(srv, [GenRequest([(5 * i + j) % 1000 for j in range(16)], max_new_tokens=64,
+                                                   temperature=0.8) for i in range(16)])
+    finally:
+        srv.close()
