@@ -49,7 +49,12 @@ def parse(argv=None):
                     help="activation checkpointing on (1) / off (0) / a fraction of the blocks (e.g. 0.5) / "
                          "by HBM budget (auto); default: the preset's")
     ap.add_argument("--backend", default="auto", choices=["auto", "torch"])
-    ap.add_argument("--bucket-mb", type=float, default=64.0)
+    ap.add_argument("--bucket-mb", type=float, default=64.0, help="DP gradient bucket size (MiB)")
+    ap.add_argument("--first-bucket-mb", type=float, default=4.0, help="size of the first (earliest) bucket (MiB)")
+    ap.add_argument("--rccl-channels", type=int, default=None,
+                    help="pin RCCL's channel count (NCCL_MIN/MAX_NCHANNELS) before the communicator is built; "
+                         "default: RCCL's own choice")
+    ap.add_argument("--rccl-env", default="", help="extra RCCL / torch-NCCL settings, 'KEY=VAL,KEY=VAL'")
     ap.add_argument("--zero", type=int, default=0, choices=[0, 1],
                     help="1 = ZeRO-1: reduce-scatter grads, shard fp32 master/moments, all-gather bf16 weights")
     ap.add_argument("--grad-clip", type=float, default=1.0)
@@ -104,9 +109,10 @@ def main(argv=None):
     from pretraining_llm_amd.models import GPT, get_preset
     from pretraining_llm_amd.parallel.dp import DataParallelEngine
     from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
-    from pretraining_llm_amd.utils.dist import init_distributed
+    from pretraining_llm_amd.utils.dist import apply_rccl_env, comm_env, init_distributed, parse_env_list
 
     cpu = args.device == "cpu"
+    apply_rccl_env(args.rccl_channels, parse_env_list(args.rccl_env))  # before the communicator exists
     di = init_distributed("gloo" if cpu else "nccl", args.device)
     world = di.world_size
     if args.gpus != world:
@@ -138,11 +144,14 @@ def main(argv=None):
                max_grad_norm=args.grad_clip)
     if args.zero:
         from pretraining_llm_amd.parallel.zero import ShardedFlatAdamW, ZeroDataParallelEngine
-        opt = ShardedFlatAdamW(model, bucket_mb=args.bucket_mb, **okw)
-        engine = ZeroDataParallelEngine(opt)
+        opt = ShardedFlatAdamW(model, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb, **okw)
+        engine = ZeroDataParallelEngine(opt, timing=world > 1)
     else:
         opt = FlatAdamW(model, **okw)
-        engine = DataParallelEngine(opt, bucket_mb=args.bucket_mb)
+        # world > 1: HIP events around every bucket launch and the end-of-backward wait (where did
+        # the communication time go), reported in the JSON line's "comm" block
+        engine = DataParallelEngine(opt, bucket_mb=args.bucket_mb, first_bucket_mb=args.first_bucket_mb,
+                                    timing=world > 1)
 
     B, T = args.batch, args.seq
     n_tok = max(4_000_000, 4 * B * (T + 1))
@@ -151,6 +160,7 @@ def main(argv=None):
     loader = TokenLoader(shard, B, T, 0, 1, seed=1000 + di.rank, device=dev)
 
     def step():
+        engine.timer.start()
         x, y = loader.next()
         _, loss = model(x, y, return_logits=False)
         loss.backward()
@@ -161,6 +171,7 @@ def main(argv=None):
 
     if args.cuda_graph:
         from pretraining_llm_amd.train.graph import GraphedTrainStep
+        engine.timer.enabled = False  # no event records inside a captured graph
         x0, y0 = loader.next()
         gstep = GraphedTrainStep(model, opt, engine, B, T, dev, warmup=2).capture(x0, y0, 6e-4)
 
@@ -178,6 +189,7 @@ def main(argv=None):
     if dist.is_initialized():
         dist.barrier()
     sync()
+    engine.timer.reset()  # timed steps only
     t0 = time.perf_counter()
     for _ in range(args.steps):
         loss = step()
@@ -186,10 +198,18 @@ def main(argv=None):
         dist.barrier()
     elapsed = time.perf_counter() - t0
     final_loss = float(loss.detach())
+    opt.wait_params()
+    ctime = engine.timer.report()
+    rank_ms = [1000 * elapsed / args.steps]
+    exposed = [ctime.get("exposed_comm_ms") or 0.0]
     if dist.is_initialized():
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        # per-rank step time and exposed communication (the slowest rank sets the pace)
+        t = torch.tensor([elapsed, exposed[0]], device=dev, dtype=torch.float64)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t)
+        rank_ms = [float(p[0]) * 1000 / args.steps for p in parts]
+        exposed = [float(p[1]) for p in parts]
+        elapsed = max(float(p[0]) for p in parts)
     tokens = world * B * T * args.steps
     tps = tokens / elapsed
     flops_tok = mcfg.flops_per_token(T)
@@ -227,7 +247,18 @@ def main(argv=None):
                      if hasattr(engine, "bucket_sizes_mb") else None,
                      # True once the bucket readiness counts were learned: later steps launch each
                      # bucket's collective from the backward hooks (overlapped), not at the end
-                     "hook_launched_buckets": getattr(engine, "_expected", None) is not None},
+                     "hook_launched_buckets": getattr(engine, "_expected", None) is not None,
+                     "first_bucket_mb": args.first_bucket_mb,
+                     # compute-stream stall on RCCL after the backward (ms/step, HIP events), mean
+                     # over timed steps; rank 0's and the worst rank's
+                     "exposed_comm_ms": ctime.get("exposed_comm_ms"),
+                     "exposed_comm_ms_max_rank": round(max(exposed), 3) if world > 1 else None,
+                     # last timed step, rank 0: when each bucket's collective was issued and when
+                     # the backward ended (ms after the step started)
+                     "bucket_launch_ms": ctime.get("bucket_launch_ms"),
+                     "backward_end_ms": ctime.get("backward_end_ms"),
+                     "rank_step_ms_min": round(min(rank_ms), 3), "rank_step_ms_max": round(max(rank_ms), 3),
+                     "rccl_env": comm_env() if world > 1 else {}},
             "device": args.device,
         }
         print(json.dumps(rec), flush=True)

@@ -34,7 +34,11 @@ def main(argv=None):
     ap.add_argument("--dtype", default="bfloat16")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--rccl-channels", type=int, default=None, help="NCCL_MIN/MAX_NCHANNELS (before init)")
+    ap.add_argument("--rccl-env", default="", help="extra 'KEY=VAL,...' RCCL settings")
     args = ap.parse_args(argv)
+    from pretraining_llm_amd.utils.dist import apply_rccl_env, parse_env_list
+    apply_rccl_env(args.rccl_channels, parse_env_list(args.rccl_env))
     import torch
     import torch.distributed as dist
     from pretraining_llm_amd.utils.dist import init_distributed

@@ -86,6 +86,8 @@ default_config = {
     'synthetic_dir': 'data/synthetic',
     'bucket_mb': 64.0,                # DP all-reduce bucket size (xGMI-sized, see parallel/dp.py)
     'first_bucket_mb': 4.0,
+    'rccl_channels': None,            # pin RCCL's channel count (NCCL_MIN/MAX_NCHANNELS) before the communicator; None = RCCL's choice
+    'rccl_env': None,                 # extra RCCL / torch-NCCL env, dict or 'KEY=VAL,...' (utils/dist.apply_rccl_env)
     'activation_checkpointing': None,
     'override_preset_dims': False,    # with model_preset: the dims above (n_embed, n_head, n_blocks, ...) override the preset's
     'tuned_gemms': True,              # GPU: load the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/)

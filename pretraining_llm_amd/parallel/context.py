@@ -13,9 +13,10 @@ around the ring:
   their LSEs:  lse = logaddexp(lse_a, lse_b),  o = o_a e^(lse_a-lse) + o_b e^(lse_b-lse).
 * backward: the flash backward kernel is run per visible pair with the FINAL o and lse
   (so every pair's gradient is exact); dQ stays local, dK/dV accumulate in fp32
-  buffers that travel with the K/V and arrive back at their owner after W hops.
-* the next shard's send/recv is posted before the current pair's kernels run, so the
-  transfer over xGMI overlaps the attention compute (one peer per direction: a ring is
+  buffers that travel one ring step behind the K/V and arrive back at their owner after W hops.
+* forward and backward post the next K/V shard's send/recv before the current pair's kernels
+  run, and the backward's accumulator hop is waited for only after the next step's kernels, so
+  the transfers over xGMI overlap the attention compute (one peer per direction: a ring is
   exactly the per-link pattern xGMI's point-to-point links serve best).
 
 Layouts:
@@ -184,16 +185,24 @@ class _RingAttnFn(torch.autograd.Function):
         dq_parts = _split(dq, nq)
         qs, dos, os_ = _split(q, nq), _split(do, nq), _split(o, nq)
         lses = [t.contiguous() for t in lse.chunk(nq, dim=2)] if nq > 1 else [lse]
-        # traveling state: this rank's K/V plus fp32 dK/dV accumulated by every rank visited
-        kv = [k.contiguous(), v.contiguous(),
-              torch.zeros(k.shape, dtype=torch.float32, device=k.device),
-              torch.zeros(v.shape, dtype=torch.float32, device=v.device)]
-        ring = _Ring(group)
+        # Two rings.  K/V (read-only) hop before the pair kernels, as in the forward.  The fp32
+        # dK/dV accumulators of the visiting block travel ONE STEP BEHIND: each step's kernels
+        # add into fresh local buffers, and only after them does the rank wait for the
+        # accumulator the previous rank sent (one add), then pass the sum on.  So neither
+        # transfer sits between two steps' kernels: the K/V hop overlaps this step's compute and
+        # the accumulator hop overlaps the next step's.  After W hops every accumulator is back
+        # at its owner.
+        kv = [k.contiguous(), v.contiguous()]
+        kv_ring, acc_ring = _Ring(group), _Ring(group)
+        acc_in = False
         for step in range(W):
             src = (r - step) % W
+            nxt = kv_ring.start(kv) if step + 1 < W else None
             kids = _chunk_ids(src, W, layout)
             ks, vs = _split(kv[0], len(kids)), _split(kv[1], len(kids))
-            dks, dvs = _split(kv[2], len(kids)), _split(kv[3], len(kids))
+            dk = torch.zeros(k.shape, dtype=torch.float32, device=k.device)
+            dv = torch.zeros(v.shape, dtype=torch.float32, device=v.device)
+            dks, dvs = _split(dk, len(kids)), _split(dv, len(kids))
             for qi, qc in enumerate(qids):
                 for ki, kc in enumerate(kids):
                     m = _mode(qc, kc, causal)
@@ -204,12 +213,18 @@ class _RingAttnFn(torch.autograd.Function):
                     dq_parts[qi].add_(gq.float())
                     dks[ki].add_(gk.float())
                     dvs[ki].add_(gv.float())
+            if acc_in:  # the accumulator of this K/V block from the ranks it visited before
+                pdk, pdv = acc_ring.wait()
+                dk.add_(pdk)
+                dv.add_(pdv)
             if W > 1:
-                # K/V need W-1 hops; the dK/dV accumulators one more, back to their owner
-                nxt = ring.start(kv if step + 1 < W else kv[2:])
-                ring.wait()
-                kv = nxt if step + 1 < W else kv[:2] + nxt
-        return dq.to(q.dtype), kv[2].to(k.dtype), kv[3].to(v.dtype), None, None, None, None
+                acc_ring.start([dk, dv])
+                acc_in = True
+            if nxt is not None:
+                kv = kv_ring.wait()
+        if W > 1:
+            dk, dv = acc_ring.wait()  # this rank's own K/V gradient, summed over every rank
+        return dq.to(q.dtype), dk.to(k.dtype), dv.to(v.dtype), None, None, None, None
 
 
 def ring_attention(q: torch.Tensor, k: torch.Tensor, v: torch.Tensor, group=None, causal: bool = True,

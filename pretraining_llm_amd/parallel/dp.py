@@ -33,13 +33,68 @@ import torch
 import torch.distributed as dist
 
 
+class CommTimer:
+    """Where a DP step's communication time went, from HIP events on the compute stream (no host
+    sync inside the step): ``start()`` at the beginning of a step, ``launch(b)`` when bucket b's
+    collective is issued (its offset into the step = how early the backward released it),
+    ``backward_end()`` when ``finish_grad_sync`` is entered (the backward's last kernel is queued)
+    and ``sync_end()`` once the compute stream has waited for every collective.  The exposed
+    communication of a step is backward_end -> sync_end: the time the compute stream stalls on
+    RCCL after the backward (the un-overlapped tail).  Read with ``report()`` after a device sync."""
+
+    def __init__(self, enabled: bool):
+        self.enabled = bool(enabled) and torch.cuda.is_available()
+        self.steps = []  # per step: dict of events
+        self._cur = None
+
+    def _ev(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        return e
+
+    def start(self):
+        if self.enabled:
+            self._cur = {"start": self._ev(), "launch": {}}
+
+    def launch(self, b: int):
+        if self.enabled and self._cur is not None:
+            self._cur["launch"][b] = self._ev()
+
+    def backward_end(self):
+        if self.enabled and self._cur is not None:
+            self._cur["bwd_end"] = self._ev()
+
+    def sync_end(self):
+        if self.enabled and self._cur is not None and "bwd_end" in self._cur:
+            self._cur["sync_end"] = self._ev()
+            self.steps.append(self._cur)
+        self._cur = None
+
+    def reset(self):
+        self.steps, self._cur = [], None
+
+    def report(self) -> dict:
+        """Mean exposed communication ms/step and, for the last step, each bucket's launch offset
+        (ms after the step started) and the backward's end offset."""
+        if not self.steps:
+            return {"exposed_comm_ms": 0.0 if not self.enabled else None, "steps_timed": 0}
+        exp = [st["bwd_end"].elapsed_time(st["sync_end"]) for st in self.steps]
+        last = self.steps[-1]
+        t0 = last["start"]
+        return {"exposed_comm_ms": round(sum(exp) / len(exp), 3), "exposed_comm_ms_max": round(max(exp), 3),
+                "steps_timed": len(exp),
+                "backward_end_ms": round(t0.elapsed_time(last["bwd_end"]), 3),
+                "bucket_launch_ms": [round(t0.elapsed_time(last["launch"][b]), 3) for b in sorted(last["launch"])]}
+
+
 class DataParallelEngine:
     def __init__(self, optimizer, process_group=None, bucket_mb: float = 64.0, first_bucket_mb: float = 4.0,
-                 broadcast_params: bool = True, overlap: bool = True):
+                 broadcast_params: bool = True, overlap: bool = True, timing: bool = False):
         self.opt = optimizer
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.overlap = overlap
+        self.timer = CommTimer(timing and optimizer.flat_grad.is_cuda)
         self.enabled = True
         self._handles = []
         self._hooks = []
@@ -126,6 +181,7 @@ class DataParallelEngine:
         ops.sync_side_streams()  # side-stream weight gradients of this bucket must have landed
         bk = self.buckets[b]
         view = self.opt.flat_grad[bk["start"]:bk["end"]]
+        self.timer.launch(b)
         self._handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))
 
     def _launch_ready(self):
@@ -148,6 +204,7 @@ class DataParallelEngine:
         Returns the gradient scale the optimizer must apply (1/world)."""
         from .. import ops
         ops.sync_side_streams()
+        self.timer.backward_end()
         if self.world > 1:
             while self._next_launch < len(self.buckets):
                 self._launch(self._next_launch)
@@ -156,6 +213,7 @@ class DataParallelEngine:
                 h.wait()
             if self._expected is None and self.enabled and any(self._events):
                 self._expected = list(self._events)
+        self.timer.sync_end()
         self._reset_counters()
         return 1.0 / self.world
 

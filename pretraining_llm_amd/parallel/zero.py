@@ -131,6 +131,7 @@ class ShardedFlatAdamW(FlatAdamW):
     def step(self, grad_scale: float = 1.0, graph: bool = False):
         if graph:
             raise RuntimeError("ShardedFlatAdamW: graph-captured steps are not supported (collectives in the step)")
+        self.wait_params()  # a previous step's gathers not yet consumed (e.g. no forward in between)
         self._sync_lr()
         self.step_count += 1
         clip = None
@@ -138,16 +139,77 @@ class ShardedFlatAdamW(FlatAdamW):
             norm = self.grad_norm(grad_scale)
             self.last_grad_norm = norm
             clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).to(torch.float32).reshape(1)
-        handles = []
-        for (bs, be), (fs, fe, o) in zip(self.buckets, self.own):
+        # buckets in FORWARD order (start of the buffer = embeddings and first blocks first): the
+        # next forward needs them in that order, so the first gathers issued are the first waited
+        # for, and the later ones keep running under the first blocks' forward
+        self._gathers = {}
+        for b in reversed(range(len(self.buckets))):
+            bs, be = self.buckets[b]
+            fs, fe, o = self.own[b]
             self._update_part(fs, fe, o, grad_scale, clip)
             if self.world > 1:
                 src = self.flat_param[fs:fe] if self._inplace_ag else self.flat_param[fs:fe].clone()
-                handles.append(dist.all_gather_into_tensor(self.flat_param[bs:be], src, group=self.pg,
-                                                           async_op=True))
-        for h in handles:
-            h.wait()
-        self.refresh_shadows()
+                self._gathers[b] = dist.all_gather_into_tensor(self.flat_param[bs:be], src, group=self.pg,
+                                                               async_op=True)
+        self._shadows_stale = True
+        if not self.lazy_gather:
+            self.wait_params()
+
+    # ------------------------------------------------------------------ lazy parameter all-gather
+    lazy_gather = False  # set by install_lazy_gather
+
+    def wait_params(self, params=None):
+        """Make the compute stream wait for the all-gathers of the buckets holding ``params``
+        (every pending bucket when None; then also refresh the transposed weight shadows, which
+        read every parameter).  A wait on RCCL is a stream dependency, not a host block."""
+        pend = getattr(self, "_gathers", None) or {}
+        if params is None:
+            for b in list(pend):
+                pend.pop(b).wait()
+            if getattr(self, "_shadows_stale", False):
+                self._shadows_stale = False
+                self.refresh_shadows()
+            return
+        for b in self._buckets_of(params):
+            h = pend.pop(b, None)
+            if h is not None:
+                h.wait()
+
+    def _buckets_of(self, params):
+        key = tuple(id(p) for p in params)
+        cache = self.__dict__.setdefault("_bucket_cache", {})
+        if key not in cache:
+            idx = {id(p): i for i, p in enumerate(self.params)}
+            out = set()
+            for p in params:
+                i = idx.get(id(p))
+                if i is None:
+                    continue
+                a, e = self.offsets[i], self.offsets[i] + p.numel()
+                out.update(b for b, (bs, be) in enumerate(self.buckets) if bs < e and be > a)
+            cache[key] = sorted(out, reverse=True)  # forward order
+        return cache[key]
+
+    def install_lazy_gather(self, model):
+        """Wait for each bucket's parameter all-gather right before its first use in the next
+        forward instead of at the end of ``step()``: forward pre-hooks on the model (embeddings)
+        and on every transformer block and the final norm wait for the buckets holding their
+        parameters; a forward hook on the model waits for the rest (LM head, tied embedding) and
+        refreshes the weight shadows before any backward.  Returns the hook handles."""
+        if not (hasattr(model, "token_embed") and hasattr(model, "attn_blocks")):
+            return []  # not a GPT: keep the blanket wait in step()
+        self.lazy_gather = True
+        hooks = []
+        first = [p for m in (model.token_embed, getattr(model, "position_embed", None)) if m is not None
+                 for p in m.parameters()]
+        hooks.append(model.register_forward_pre_hook(lambda _m, _a: self.wait_params(first)))
+        for blk in list(getattr(model, "attn_blocks", [])) + [getattr(model, "layer_norm", None)]:
+            if blk is None:
+                continue
+            ps = list(blk.parameters())
+            hooks.append(blk.register_forward_pre_hook(lambda _m, _a, ps=ps: self.wait_params(ps)))
+        hooks.append(model.register_forward_hook(lambda _m, _a, _o: self.wait_params()))
+        return hooks
 
     # ------------------------------------------------------------------
     def _gather_full_cpu(self, shard: torch.Tensor, keep: bool) -> Optional[torch.Tensor]:
@@ -169,6 +231,7 @@ class ShardedFlatAdamW(FlatAdamW):
     def state_dict(self, writer_rank: int = 0) -> dict:
         """COLLECTIVE: every rank must call it.  Returns the full (unsharded) AdamW-format state
         on ``writer_rank`` (in host memory) and ``{}`` elsewhere."""
+        self.wait_params()
         keep = self.rank == writer_rank
         full = [self._gather_full_cpu(t, keep) for t in (self.master, self.exp_avg, self.exp_avg_sq)]
         if not keep:
@@ -184,6 +247,7 @@ class ShardedFlatAdamW(FlatAdamW):
     def load_state_dict(self, sd: dict):
         """Every rank reads the same full state and copies only the parts it owns (no collective,
         no unsharded device copy)."""
+        self.wait_params()
         st = sd["state"]
         steps = []
         for i, p in enumerate(self.params):
@@ -213,6 +277,7 @@ class ShardedFlatAdamW(FlatAdamW):
 
     @torch.no_grad()
     def sync_master_from_params(self):
+        self.wait_params()
         for fs, fe, o in self.own:
             self.master[o:o + fe - fs].copy_(self.flat_param[fs:fe].float())
         self.refresh_shadows()
@@ -222,7 +287,12 @@ class ZeroDataParallelEngine:
     """Gradient reduce-scatter engine for ``ShardedFlatAdamW`` (same surface as
     ``DataParallelEngine``: ``no_sync()``, ``finish_grad_sync() -> grad scale``)."""
 
-    def __init__(self, optimizer: ShardedFlatAdamW, broadcast_params: bool = True, overlap: bool = True):
+    def __init__(self, optimizer: ShardedFlatAdamW, broadcast_params: bool = True, overlap: bool = True,
+                 timing: bool = False, lazy_gather: bool = True):
+        from .dp import CommTimer
+        self.timer = CommTimer(timing and optimizer.flat_grad.is_cuda)
+        if lazy_gather:
+            self.hooks_lazy = optimizer.install_lazy_gather(optimizer.model)
         self.opt = optimizer
         self.pg = optimizer.pg
         self.world = optimizer.world
@@ -280,6 +350,7 @@ class ZeroDataParallelEngine:
         bs, be = opt.buckets[b]
         fs, fe, o = opt.own[b]
         out = opt.grad_shard[o:o + fe - fs]
+        self.timer.launch(b)
         self._handles.append(dist.reduce_scatter_tensor(out, opt.flat_grad[bs:be], op=dist.ReduceOp.SUM,
                                                         group=self.pg, async_op=True))
 
@@ -300,6 +371,7 @@ class ZeroDataParallelEngine:
     def finish_grad_sync(self):
         from .. import ops
         ops.sync_side_streams()
+        self.timer.backward_end()
         opt = self.opt
         if self.world > 1:
             while self._next_launch < len(opt.buckets):
@@ -312,6 +384,7 @@ class ZeroDataParallelEngine:
         else:
             for fs, fe, o in opt.own:
                 opt.grad_shard[o:o + fe - fs].copy_(opt.flat_grad[fs:fe])
+        self.timer.sync_end()
         self._reset_counters()
         return 1.0 / self.world
 

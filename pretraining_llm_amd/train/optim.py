@@ -285,6 +285,10 @@ class FlatAdamW:
                                 0.0, self.step_count, master=self.master)
         self.refresh_shadows()
 
+    def wait_params(self, params=None):
+        """Parameters are always current here (ZeRO-1's optimizer overrides this: its weights
+        arrive by all-gathers that the next forward waits for lazily)."""
+
     # ------------------------------------------------------------------
     def state_dict(self) -> dict:
         state = {}

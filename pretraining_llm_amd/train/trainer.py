@@ -35,7 +35,7 @@ from ..parallel.model_parallel import (build_dense_shell, gather_dense_state, in
                                        parallelize_gpt, sync_replicated_grads)
 from ..utils.checkpoint import load_checkpoint, save_checkpoint
 from .amp import DynamicLossScaler, autocast_ctx, loss_scaling_default, precision_mode
-from ..utils.dist import DistInfo, init_distributed
+from ..utils.dist import DistInfo, apply_rccl_env, init_distributed, parse_env_list
 from ..utils.metrics import MetricsLogger, mfu, peak_memory_gb
 from .optim import FlatAdamW, no_decay_1d
 
@@ -74,6 +74,8 @@ class Trainer:
     def __init__(self, cfg: dict, dist_info: Optional[DistInfo] = None, log=print):
         self.cfg = dict(cfg)
         self.log = log
+        if dist_info is None:  # RCCL's environment must be in place before the communicator exists
+            apply_rccl_env(self.cfg.get("rccl_channels"), parse_env_list(self.cfg.get("rccl_env")))
         self.di = dist_info or init_distributed(self.cfg.get("ddp_backend", "auto"), self.cfg.get("device", "auto"))
         self.device = self.di.device
         seed = int(self.cfg.get("seed", 1337))
@@ -300,6 +302,7 @@ class Trainer:
                 self.save(self._ckpt_path(periodic=True))
         if prof is not None:
             self._finish_profile(prof)
+        self.opt.wait_params()  # ZeRO-1: the last step's weight all-gathers
         out = cfg.get("t_out_path")
         if out:
             self.save(out)

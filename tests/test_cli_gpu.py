@@ -42,3 +42,7 @@ def test_bench_two_ranks_one_gpu_gloo():
     rec = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")][-1]
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["comm"]["hook_launched_buckets"]
     assert rec["device"] == "cuda" and rec["value"] > 0
+    c = rec["comm"]  # HIP-event diagnostics of the multi-rank path
+    assert c["exposed_comm_ms"] is not None and c["exposed_comm_ms"] >= 0.0 and c["exposed_comm_ms_max_rank"] >= 0.0
+    assert len(c["bucket_launch_ms"]) == c["n_buckets"] and c["backward_end_ms"] > 0
+    assert c["rank_step_ms_min"] <= c["rank_step_ms_max"]

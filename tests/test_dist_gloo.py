@@ -157,14 +157,24 @@ def test_bench_self_launches_ranks_cpu():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--device", "cpu",
-                        "--model", "gpt2-tiny", "--steps", "2", "--warmup", "1", "--batch", "2", "--seq", "64"],
+                        "--model", "gpt2-tiny", "--steps", "2", "--warmup", "1", "--batch", "2", "--seq", "64",
+                        "--rccl-channels", "8", "--rccl-env", "TORCH_NCCL_HIGH_PRIORITY=1", "--bucket-mb", "2",
+                        "--first-bucket-mb", "0.5"],
                        capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     recs = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(recs) == 1, r.stdout
     rec = recs[0]
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
-    assert rec["comm"]["world"] == 2 and rec["comm"]["hook_launched_buckets"]
+    c = rec["comm"]
+    assert c["world"] == 2 and c["hook_launched_buckets"]
+    # multi-GPU diagnostics: per-rank step times, the RCCL environment the run had (set before
+    # the process group existed), exposed-communication fields (HIP events: None on CPU)
+    assert c["rank_step_ms_min"] <= c["rank_step_ms_max"] and abs(c["rank_step_ms_max"] - rec["ms_per_step"]) < 1e-2
+    assert c["rccl_env"]["NCCL_MIN_NCHANNELS"] == "8" and c["rccl_env"]["NCCL_MAX_NCHANNELS"] == "8"
+    assert c["rccl_env"]["TORCH_NCCL_HIGH_PRIORITY"] == "1"
+    assert c["first_bucket_mb"] == 0.5 and c["n_buckets"] >= 2
+    assert "exposed_comm_ms" in c and "bucket_launch_ms" in c and "exposed_comm_ms_max_rank" in c
     assert rec["value"] > 0 and abs(rec["value"] - 2 * 2 * 64 * 2 / (rec["ms_per_step"] * 2 / 1000)) / rec["value"] < 0.01
 
 

@@ -75,7 +75,13 @@ def _worker(rank, world, port, outdir, accum):
 
     _train((m_ref, o_ref, e_ref), data, rank, 3, accum)
     _train((m_z, o_z, e_z), data, rank, 3, accum)
-    out = {"diff": (o_ref.flat_param[:o_ref.total] - o_z.flat_param[:o_ref.total]).abs().max().item(),
+    # the step leaves its bucket all-gathers pending; the next forward waits for each bucket at
+    # its first use (pre-hooks), so no blanket wait ends the step
+    pending_after_step = len(o_z._gathers)
+    with torch.no_grad():
+        m_z(data[:2, :-1], data[:2, 1:])
+    out_lazy = {"pending_after_step": pending_after_step, "pending_after_fwd": len(o_z._gathers)}
+    out = {**out_lazy, "diff": (o_ref.flat_param[:o_ref.total] - o_z.flat_param[:o_ref.total]).abs().max().item(),
            "shard_frac": o_z.master.numel() / o_z.total, "nbuckets": len(o_z.buckets)}
     sd_ref, sd_z = o_ref.state_dict(), o_z.state_dict()  # collective for the sharded one
     out["writer_only"] = (rank == 0) == bool(sd_z)  # full state on the writer rank only
@@ -93,6 +99,8 @@ def _worker(rank, world, port, outdir, accum):
     e_r = ZeroDataParallelEngine(o_r)
     _train((m_z, o_z, e_z), data, rank, 1, accum)
     _train((m_r, o_r, e_r), data, rank, 1, accum)
+    o_z.wait_params()
+    o_r.wait_params()
     out["resume_diff"] = (o_z.flat_param - o_r.flat_param).abs().max().item()
     ps = torch.tensor([o_z.flat_param.double().sum().item()])
     allp = [torch.zeros_like(ps) for _ in range(world)]
@@ -117,6 +125,7 @@ def _check(res, world):
         assert abs(r["shard_frac"] - 1.0 / world) < 1e-9
         assert r["nbuckets"] > 2
         assert len(set(r["replicas"])) == 1
+        assert r["pending_after_step"] == r["nbuckets"] and r["pending_after_fwd"] == 0, r
 
 
 def test_zero1_matches_replicated_world2():
