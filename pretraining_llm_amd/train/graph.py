@@ -9,34 +9,53 @@ is moved into device buffers first: the batch is copied into static input tensor
 the AdamW scalars (lr, bias corrections) into ``FlatAdamW.hyper``, the gradient-clip
 coefficient and CE normaliser are computed on device, and the data-parallel engine's
 bucket order is learned in eager warmup steps before capture.
+
+Gradient accumulation (``accum`` > 1) is captured too: the graph holds every micro-step's
+forward and backward -- all but the last under the DP engine's ``no_sync`` (no collective),
+the last one launching the bucketed all-reduces from the backward hooks -- then one optimizer
+step over the fp32 accumulated gradient scaled by 1/accum.  The static inputs are
+``[accum, B, T]``.
 """
 from __future__ import annotations
+
+import contextlib
 
 import torch
 
 
 class GraphedTrainStep:
-    def __init__(self, model, optimizer, engine, batch: int, seq: int, device, warmup: int = 2):
+    def __init__(self, model, optimizer, engine, batch: int, seq: int, device, warmup: int = 2, accum: int = 1):
         self.model, self.opt, self.engine = model, optimizer, engine
-        self.x = torch.zeros(batch, seq, dtype=torch.int64, device=device)
-        self.y = torch.zeros(batch, seq, dtype=torch.int64, device=device)
+        self.accum = int(accum)
+        self.xs = torch.zeros(self.accum, batch, seq, dtype=torch.int64, device=device)
+        self.ys = torch.zeros(self.accum, batch, seq, dtype=torch.int64, device=device)
+        self.x, self.y = self.xs[0], self.ys[0]  # accum == 1 views (bench.py)
         self.warmup = warmup
         self.graph = None
         self.loss = None
 
     def _body(self):
-        _, loss = self.model(self.x, self.y, return_logits=False)
-        loss.backward()
+        total = None
+        for m in range(self.accum):
+            ctx = self.engine.no_sync() if m < self.accum - 1 else contextlib.nullcontext()
+            with ctx:
+                _, loss = self.model(self.xs[m], self.ys[m], return_logits=False)
+                loss.backward()
+            total = loss.detach().float() if total is None else total + loss.detach().float()
         scale = self.engine.finish_grad_sync()
-        self.opt.step(grad_scale=scale, graph=True)
+        self.opt.step(grad_scale=scale / self.accum, graph=True)
         self.opt.zero_grad()
-        return loss.detach()
+        return total / self.accum
+
+    def _load(self, x, y, non_blocking=False):
+        # x, y: one micro-batch [B, T] (accum == 1) or all of them [accum, B, T]
+        self.xs.copy_(x.view(self.xs.shape), non_blocking=non_blocking)
+        self.ys.copy_(y.view(self.ys.shape), non_blocking=non_blocking)
 
     def capture(self, x, y, lr: float):
         """Run ``warmup`` eager steps on (x, y) (real optimizer steps) on a side stream, then capture.
         The loss of the last warmup step is kept in ``warmup_loss``."""
-        self.x.copy_(x)
-        self.y.copy_(y)
+        self._load(x, y)
         side = torch.cuda.Stream()
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -56,8 +75,7 @@ class GraphedTrainStep:
     def __call__(self, x, y, lr: float):
         if self.graph is None:
             raise RuntimeError("call capture() first")
-        self.x.copy_(x, non_blocking=True)
-        self.y.copy_(y, non_blocking=True)
+        self._load(x, y, non_blocking=True)
         self.opt.prepare_graph_step(lr)
         self.graph.replay()
         return self.loss

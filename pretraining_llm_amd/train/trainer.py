@@ -126,28 +126,34 @@ class Trainer:
             self.opt.set_tensor_parallel(self.pg.tp_group, self.pg.tp)  # global grad norm over TP shards
         self.accum = int(self.cfg.get("grad_accum_steps", 1))
         self.step = 0
-        # TORCH_COMPILE (reference: torch.compile(model) when the env var is "1",
+        # TORCH_COMPILE (reference: torch.compile(model) unless the env var is "0", default "1",
         # scripts/train_transformer.py:31-33,118-120).  The hot ops here are hand-written kernels, so
         # what a compiler would still remove is per-launch host cost: on the GPU the whole step
-        # (fwd, bwd, bucketed all-reduce, clip, AdamW, zero_grad) is captured once as a hipGraph
-        # and replayed (train/graph.py); on the CPU the model goes through torch.compile.
+        # (every micro-step's fwd + bwd, bucketed all-reduce, clip, AdamW, zero_grad) is captured
+        # once as a hipGraph and replayed (train/graph.py) -- on by default, like the reference's
+        # compile.  On the CPU (tests, plumbing) the default is eager; TORCH_COMPILE=1 there runs
+        # torch.compile.
         comp = self.cfg.get("compile")
         if comp is None:
-            comp = os.environ.get("TORCH_COMPILE", "0") == "1"
+            env = os.environ.get("TORCH_COMPILE")
+            comp = (env == "1") if env is not None else self.device.type == "cuda"
         self.compile = bool(comp)
         self.gstep = None
         self.use_graph = False
         self.fwd = self.model
         if self.compile and self.device.type == "cuda":
-            why = ("grad_accum_steps > 1" if self.accum > 1 else "ZeRO-1 (collectives inside the optimizer step)"
+            why = ("ZeRO-1 (collectives inside the optimizer step)"
                    if int(self.cfg.get("zero_stage", 0)) >= 1 else "tensor / context parallelism"
                    if self.pg.model_parallel else "loss scaling (host-side skip decision)" if self.scaler.enabled
                    else f"dtype={dtype_name} (the graphed step runs the bf16 HIP kernels)"
-                   if self.dtype != torch.bfloat16 else None)
+                   if self.dtype != torch.bfloat16 else "dist backend gloo (collectives cannot be captured)"
+                   if dist.is_initialized() and dist.get_backend() != "nccl" else None)
             if why is None:
                 self.use_graph = True
+                if self.di.is_master:
+                    self.log(f"TORCH_COMPILE: whole training step captured as a hipGraph (grad_accum_steps={self.accum})")
             elif self.di.is_master:
-                self.log(f"TORCH_COMPILE: hipGraph step disabled ({why}); running eagerly")
+                self.log(f"TORCH_COMPILE: hipGraph step disabled for this configuration ({why}); running eagerly")
         elif self.compile:
             self.fwd = torch.compile(self.model, backend=self.cfg.get("compile_backend", "inductor"))
         self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
@@ -223,13 +229,16 @@ class Trainer:
     def _graph_step(self, lr: float) -> torch.Tensor:
         """hipGraph-replayed step.  The first call runs one real (eager, side-stream) step on its
         batch -- it also teaches the DP engine its bucket order -- then captures the step; every
-        later call copies its batch into the static inputs and replays."""
+        later call copies its micro-batches into the static inputs and replays."""
         from .graph import GraphedTrainStep
-        x, y = self.train_loader.next()
+        batches = [self.train_loader.next() for _ in range(self.accum)]
+        x = torch.stack([b[0] for b in batches])
+        y = torch.stack([b[1] for b in batches])
         self.step += 1
         if self.gstep is None:
-            B, T = x.shape
-            self.gstep = GraphedTrainStep(self.model, self.opt, self.engine, B, T, self.device, warmup=1)
+            _, B, T = x.shape
+            self.gstep = GraphedTrainStep(self.model, self.opt, self.engine, B, T, self.device, warmup=1,
+                                          accum=self.accum)
             self.gstep.capture(x, y, lr)
             return self.gstep.warmup_loss
         return self.gstep(x, y, lr).clone()

@@ -27,11 +27,11 @@ sys.path.insert(0, REF)
 from src.models.transformer import Transformer
 from safetensors.torch import save_file
 torch.manual_seed(0)
-m = Transformer(n_head=4, n_embed=64, context_length=16, vocab_size=128, N_BLOCKS=2)
+m = Transformer(n_head=NH, n_embed=C, context_length=CTX, vocab_size=V, N_BLOCKS=L)
 m.eval()
 g = torch.Generator().manual_seed(1)
-idx = torch.randint(0, 128, (3, 16), generator=g)
-tgt = torch.randint(0, 128, (3, 16), generator=g)
+idx = torch.randint(0, V, (3, CTX), generator=g)
+tgt = torch.randint(0, V, (3, CTX), generator=g)
 with torch.no_grad():
     logits, loss = m(idx, tgt)
     out = {f"sd.{k}": v.contiguous() for k, v in m.state_dict().items()}
@@ -40,7 +40,7 @@ with torch.no_grad():
     start = idx[:, :5]
     seq = start
     for _ in range(20):
-        lg, _ = m(seq[:, -16:])
+        lg, _ = m(seq[:, -CTX:])
         seq = torch.cat([seq, lg[:, -1].argmax(-1, keepdim=True)], 1)
     out["greedy"] = seq
     torch.manual_seed(123)
@@ -55,8 +55,17 @@ def main(argv=None):
     ap.add_argument("--ref", default=os.environ.get("PLLM_REFERENCE", "/root/reference"))
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                                   "tests", "fixtures", "ref_tiny.safetensors"))
+    # dims of the reference Transformer (defaults: the ref_tiny fixture, head dim 16).  The GPU
+    # fixture ref_hd32.safetensors uses --n-head 2 --n-embed 64 --ctx 32 --vocab 256 (head dim
+    # 32: the HIP flash-attention kernels' smallest head dim)
+    ap.add_argument("--n-head", type=int, default=4)
+    ap.add_argument("--n-embed", type=int, default=64)
+    ap.add_argument("--ctx", type=int, default=16)
+    ap.add_argument("--vocab", type=int, default=128)
+    ap.add_argument("--n-blocks", type=int, default=2)
     args = ap.parse_args(argv)
-    code = f"REF = {args.ref!r}\nOUT = {os.path.abspath(args.out)!r}\n" + CHILD
+    code = (f"REF = {args.ref!r}\nOUT = {os.path.abspath(args.out)!r}\nNH = {args.n_head}\nC = {args.n_embed}\n"
+            f"CTX = {args.ctx}\nV = {args.vocab}\nL = {args.n_blocks}\n" + CHILD)
     r = subprocess.run([sys.executable, "-c", code], cwd="/tmp", capture_output=True, text=True)
     sys.stdout.write(r.stdout)
     sys.stderr.write(r.stderr[-3000:])

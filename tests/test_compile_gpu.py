@@ -107,3 +107,30 @@ def test_trainer_torch_compile_selects_graph_step(tmp_path):
     assert len(curves[True]) == 10
     for a, b in zip(curves[True], curves[False]):
         assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (curves[True], curves[False])
+
+
+def test_trainer_graph_step_grad_accum_matches_eager(tmp_path, monkeypatch):
+    """TORCH_COMPILE parity: the default (no TORCH_COMPILE in the env) on the GPU is the captured
+    step, and with grad_accum_steps=2 (both micro-steps captured, the first under no_sync) 10
+    graphed steps track eager loss and end at the same weights."""
+    from pretraining_llm_amd.train.trainer import Trainer
+    from config.config import default_config
+    monkeypatch.delenv("TORCH_COMPILE", raising=False)
+    base = dict(default_config)
+    base.update(model_preset="gpt2-tiny", t_batch_size=4, seq_len=128, t_train_steps=10, t_lr=1e-3, warmup_steps=2,
+                log_interval=1, t_eval_steps=1000, eval_at_start=False, t_out_path=None, synthetic_data=True,
+                synthetic_tokens=200_000, synthetic_dir=str(tmp_path), max_grad_norm=1.0, device="cuda",
+                grad_accum_steps=2)
+    curves, weights = {}, {}
+    for comp in (None, False):
+        recs = []
+        tr = Trainer(dict(base, compile=comp), log=lambda *_: None)
+        tr.metrics.log = recs.append
+        tr.train()
+        assert tr.use_graph == (comp is None)
+        curves[comp] = [r["train_loss"] for r in recs]
+        weights[comp] = tr.opt.master.clone()
+    assert len(curves[None]) == 10
+    for a, b in zip(curves[None], curves[False]):
+        assert abs(a - b) < 2e-3 * max(1.0, abs(b)), (curves[None], curves[False])
+    assert (weights[None] - weights[False]).abs().max().item() < 1e-3

@@ -9,21 +9,38 @@ import os
 import pytest
 import torch
 
-FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "ref_tiny.safetensors")
+FIXDIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures")
+FIX = os.path.join(FIXDIR, "ref_tiny.safetensors")
+# fixture -> reference Transformer dims (scripts/make_ref_fixture.py); ref_hd32 has head dim 32 so
+# its attention runs on the HIP flash kernels on the GPU (tests/test_ref_parity_gpu.py)
+DIMS = {"ref_tiny": dict(n_head=4, n_embed=64, context_length=16, vocab_size=128, N_BLOCKS=2),
+        "ref_hd32": dict(n_head=2, n_embed=64, context_length=32, vocab_size=256, N_BLOCKS=2)}
 
 
-def _load():
+def _load(name="ref_tiny"):
     from safetensors.torch import load_file
-    d = load_file(FIX)
+    d = load_file(os.path.join(FIXDIR, name + ".safetensors"))
     sd = {k[3:]: v for k, v in d.items() if k.startswith("sd.")}
     return d, sd
 
 
-def _model(sd):
+def _model(sd, name="ref_tiny"):
     from src.models import Transformer
-    m = Transformer(n_head=4, n_embed=64, context_length=16, vocab_size=128, N_BLOCKS=2)
+    m = Transformer(**DIMS[name])
     m.load_state_dict(sd, strict=True)
     return m.eval()
+
+
+@pytest.mark.parametrize("name", ["ref_tiny", "ref_hd32"])
+def test_reference_fixtures_cpu_fp32(name):
+    """Both fixtures: strict load, logits / loss and greedy continuation equal the reference's."""
+    d, sd = _load(name)
+    m = _model(sd, name)
+    with torch.no_grad():
+        logits, loss = m(d["idx"], d["tgt"])
+        assert torch.allclose(logits, d["logits"], atol=2e-5, rtol=1e-5), (logits - d["logits"]).abs().max()
+        assert abs(loss.item() - d["loss"].item()) < 1e-5
+        assert torch.equal(m.generate(d["idx"][:, :5], 20, temperature=0.0), d["greedy"])
 
 
 def test_reference_state_dict_loads_strictly_and_logits_match():
