@@ -146,7 +146,8 @@ class Trainer:
                    if int(self.cfg.get("zero_stage", 0)) >= 1 else "tensor / context parallelism"
                    if self.pg.model_parallel else "loss scaling (host-side skip decision)" if self.scaler.enabled
                    else f"dtype={dtype_name} (the graphed step runs the bf16 HIP kernels)"
-                   if self.dtype != torch.bfloat16 else "dist backend gloo (collectives cannot be captured)"
+                   if self.dtype != torch.bfloat16 else "stock torch ops backend (PLLM_TORCH_OPS / set_backend)"
+                   if not self._hip_step_ok() else "dist backend gloo (collectives cannot be captured)"
                    if dist.is_initialized() and dist.get_backend() != "nccl" else None)
             if why is None:
                 self.use_graph = True
@@ -191,6 +192,8 @@ class Trainer:
     def train_step(self) -> torch.Tensor:
         """One optimizer step (``grad_accum_steps`` micro-batches). Returns the mean loss (device tensor)."""
         lr = self.lr(self.step)
+        if self.use_graph and self.gstep is None and not self._hip_step_ok():
+            self.use_graph = False  # the op backend was switched to torch after construction
         if self.use_graph:
             return self._graph_step(lr)
         self.opt.param_groups[0]["lr"] = lr
@@ -225,6 +228,10 @@ class Trainer:
         self.opt.zero_grad()
         self.step += 1
         return total / self.accum
+
+    def _hip_step_ok(self) -> bool:
+        """The captured step replays the HIP kernels, AdamW included."""
+        return bool(getattr(self.opt, "use_hip", False)) and ops.get_backend() == "auto"
 
     def _graph_step(self, lr: float) -> torch.Tensor:
         """hipGraph-replayed step.  The first call runs one real (eager, side-stream) step on its
