@@ -164,6 +164,9 @@ struct Img {
 // 7 - w of the workgroup's eight, which gives every wave the same share of the
 // causal diagonal.  A block whose keys in a tile are all masked (or whose rows lie
 // past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
+// lazy-max threshold of the forward's online softmax, log2 units (p <= 2^8)
+constexpr float kLazyThr = 8.f;
+
 template <int D>
 struct FwdCfg {
   static constexpr int NW = 4;
@@ -276,7 +279,13 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
   const int fk = I::off(r, 8 * hh);
   const int fv0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), fv8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
   f32x16 o[QB][NDB];
-  float m[QB], l[QB];  // m: running max of RAW scores (scale applied in the exponent)
+  // m: the running max in log2 units (raw score x c2), the reference point of the exponent.  It is
+  // moved LAZILY (guide T13): only when some row's tile max exceeds it by more than kLazyThr, so
+  // p = exp2(s c2 - m) <= 2^kLazyThr and the O / l rescale runs on a few tiles instead of nearly
+  // every one (with an eager max, any of a wave's 32 rows gaining a new maximum -- most tiles --
+  // forced the whole O block through a rescale).  p up to 2^8 loses nothing in bf16 (same relative
+  // precision) and O / l accumulate in fp32.
+  float m[QB], l[QB];
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
 #pragma unroll
@@ -342,9 +351,19 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
         }
         float mx = fmaxf(mx0, mx1);
         mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m[j], mx);
-        const float mc = mnew == -INFINITY ? 0.f : mnew * c2;
-        const float alpha = fast_exp2(m[j] * c2 - mc);  // m = -inf -> 0
+        const float mx2 = mx * c2;  // this tile's row max in log2 units (-inf: row fully masked)
+        // (m = -inf: +inf > thr, the first visible tile always sets m; mx2 = m = -inf: NaN, false)
+        if (__any(mx2 - m[j] > kLazyThr)) {
+          const float mnew = fmaxf(m[j], mx2);
+          const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m[j] - mnew);  // m = -inf -> 0
+#pragma unroll
+          for (int db = 0; db < NDB; ++db)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) o[j][db][i] = o[j][db][i] * alpha;  // scalar multiplies
+          l[j] *= alpha;
+          m[j] = mnew;
+        }
+        const float mc = m[j] == -INFINITY ? 0.f : m[j];
         float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -355,13 +374,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
           ls0 += p0;
           ls1 += p1;
         }
-        l[j] = l[j] * alpha + (ls0 + ls1);
-        // rescale O only when some lane's running max moved (rare after the first tiles)
-        if (__any(mnew != m[j])) {
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) o[j][db] *= alpha;
-        }
-        m[j] = mnew;
+        l[j] += ls0 + ls1;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
           pf[j][2 * kb] = pack_frag(s[j][kb], 0);
@@ -395,7 +408,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       const float inv = lt > 0.f ? 1.f / lt : 0.f;
       store_row_bf16<NDB>(a.o + b * a.o_sb + (int64_t)qi * a.o_st + (int64_t)h * a.o_sh, o[j], inv, hh);
       if (hh == 0 && a.lse)
-        a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m[j] * c2 + log2f(lt)) * 0.69314718055994531f;
+        a.lse[((int64_t)b * a.H + h) * a.T + qi] = (m[j] + log2f(lt)) * 0.69314718055994531f;
     }
   }
 }

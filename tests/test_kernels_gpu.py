@@ -273,6 +273,31 @@ def test_attention_fwd(D, T, causal):
     assert (lse - lref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("D", [32, 64, 128])
+@pytest.mark.parametrize("causal", [True, False])
+def test_attention_fwd_lazy_max_rescale_branch(D, causal):
+    """The forward moves its running max lazily (only past a 2^8 threshold): force the rescale
+    branch -- scores of large dynamic range (x6) so row maxima grow by more than the threshold at
+    later tiles, plus spikes: one key per head aligned with one query at a chosen late tile so the
+    max jumps far (guide §5.4 rule 26) -- and check the FULL output against fp32."""
+    torch.manual_seed(11)
+    B, H, T = 2, 4, 640
+    q = torch.randn(B, T, H, D, device=DEV) * 2.5
+    k = torch.randn(B, T, H, D, device=DEV) * 2.5
+    v = torch.randn(B, T, H, D, device=DEV)
+    # spike: key 450 of head 0 (tile 7) matches query 500 strongly; key 130 of head 1 matches
+    # query 600 (an early tile jumping late rows' max only after many tiles were accumulated)
+    k[:, 450, 0] = q[:, 500, 0] * 3.0
+    k[:, 130, 1] = q[:, 600, 1] * 3.0
+    q, k, v = q.bfloat16(), k.bfloat16(), v.bfloat16()
+    scale = 1 / math.sqrt(D)
+    o, lse = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
+    oref, lref = _attn_ref(q, k, v, causal, scale)
+    assert _rel(o, oref) < 1.5e-2, _rel(o, oref)
+    assert (o.float() - oref).abs().max().item() < 0.1
+    assert ((lse - lref).abs() / lref.abs().clamp_min(1.0)).max().item() < 1e-2
+
+
 @pytest.mark.parametrize("D", [64, 128])
 @pytest.mark.parametrize("T", [128, 192, 512])
 @pytest.mark.parametrize("gqa", [1, 2])
