@@ -29,6 +29,7 @@
 //    per-key-block fp32 slab; a second kernel sums the slabs in a fixed order
 //    (deterministic; the first version's fp32 atomics were its floor).  The key blocks run
 //    in passes so the slab workspace is bounded independently of T (O(T) memory).
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
@@ -166,24 +167,43 @@ struct Img {
 // past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
 // lazy-max threshold of the forward's online softmax, log2 units (p <= 2^8)
 constexpr float kLazyThr = 8.f;
+#ifndef PLLM_FWD_SCHED
+#define PLLM_FWD_SCHED 1
+#endif
+#ifndef PLLM_ABL
+#define PLLM_ABL 0  // diagnostic ablations of the pipelined forward (scripts/gpu/r3_attn_abl.sh)
+#endif
+// explicit instruction interleave (sched_group_barrier) in the pipelined forward's tile regions
+constexpr bool kFwdSched = PLLM_FWD_SCHED != 0;
+
+#ifndef PLLM_FWD64_QB
+#define PLLM_FWD64_QB 2  // query blocks per wave at D <= 64 (A/B builds)
+#endif
+#ifndef PLLM_FWD_MINW
+#define PLLM_FWD_MINW 2  // __launch_bounds__ minimum waves per SIMD of the forward (A/B builds)
+#endif
 
 template <int D>
 struct FwdCfg {
   static constexpr int NW = 4;
-  static constexpr int QB = D <= 64 ? 2 : 1;
+  static constexpr int QB = D <= 64 ? PLLM_FWD64_QB : 1;
   static constexpr int BM = NW * 32 * QB, BN = 64;
   static constexpr int CPR = D / 8;   // 16 B chunks per row
   static constexpr int TILE = BN * D;  // elements per K (or V) tile
   static constexpr int LDS_ELEMS = 4 * TILE;
+  // pipelined loop (QB = 2): two K buffers and THREE V buffers -- a tile's V is still read by the
+  // deferred P.V of the next tile while the tile after that is being staged
+  static constexpr int LDS_ELEMS_PIPE = 5 * TILE;
 };
 
-template <int D, bool ROPE>
-__global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
+template <int D, bool ROPE, bool PIPE = false>
+__global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArgs a) {
+  static_assert(!PIPE || (FwdCfg<D>::QB == 2 && !ROPE), "pipelined tile loop: QB = 2, no fused RoPE");
   using C = FwdCfg<D>;
   using I = Img<D>;
   constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, TILE = C::TILE, QB = C::QB, NW = C::NW;
   constexpr int NKS = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[PIPE ? C::LDS_ELEMS_PIPE : C::LDS_ELEMS];
 
   const int nqb = (a.T + BM - 1) / BM;
   // heaviest (last) query blocks of every head first.  A head-local order (a head's blocks
@@ -256,9 +276,9 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
       }
     }
   };
-  auto swrite = [&](int buf, int t) {
+  auto swrite = [&](int buf, int t, int vbuf) {
     uint16_t* Kb = smem + buf * TILE;
-    uint16_t* Vb = smem + 2 * TILE + buf * TILE;
+    uint16_t* Vb = smem + 2 * TILE + vbuf * TILE;
 #pragma unroll
     for (int i = 0; i < 2 * NPAIR; i += 2) {
       const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2;
@@ -297,9 +317,222 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
 
   if (ntiles > 0) {
     gload(0);
-    swrite(0, 0);
+    swrite(0, 0, 0);
   }
   __syncthreads();
+  if constexpr (PIPE) {
+    // ---- software-pipelined tile loop (QB = 2) ------------------------------------------
+    // A tile's work is split in two scheduling regions separated only by the (rare) lazy-max
+    // rescale branch:
+    //   region 1: S^T of both blocks (16 MFMAs, one K fragment read feeding two), mask, row max;
+    //   region 2: the PREVIOUS tile's P.V of block 1 (8 MFMAs) beside the exponentials of block
+    //             0 (VALU), then block 0's P.V (8 MFMAs) beside the exponentials of block 1.
+    // So each wave keeps its matrix pipe fed while its own softmax runs, instead of a QK^T burst,
+    // an MFMA-idle softmax and a PV burst per tile.  Block 1's P.V is deferred one tile: its P
+    // fragments live across the barrier and its V tile stays in one of three rotating V buffers
+    // (the stage of tile t+1 must not overwrite V(t-1) while a slower wave still runs its
+    // deferred P.V of tile t-1: K is read only in region 1, so two K buffers suffice).  A rescale
+    // of block 1 first retires the pending P.V (it was exponentiated against the old max: guide
+    // T13 hazard (a)).
+    bf16x8 pfp[4];       // P of block 1 from the previous tile (P.V pending)
+#pragma unroll
+    for (int kst = 0; kst < 4; ++kst) pfp[kst] = zero_frag();
+    bool pend = false;
+    auto pv = [&](auto j_c, const bf16x8 (&pf)[4], const uint16_t* Vb) {
+      constexpr int J = decltype(j_c)::value;
+#pragma unroll
+      for (int kst = 0; kst < 4; ++kst)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+          const int rb = kst * 16 * D;
+          const bf16x8 va = cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
+          o[J][db] = mfma32(va, pf[kst], o[J][db]);
+        }
+    };
+    auto sexp = [&](auto j_c, f32x16 (&sj)[2], bf16x8 (&pf)[4]) {
+      constexpr int J = decltype(j_c)::value;
+      const float mc = m[J] == -INFINITY ? 0.f : m[J];
+      float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float p0 = fast_exp2(__builtin_fmaf(sj[0][i], c2, -mc));
+        const float p1 = fast_exp2(__builtin_fmaf(sj[1][i], c2, -mc));
+        sj[0][i] = p0;
+        sj[1][i] = p1;
+        ls0 += p0;
+        ls1 += p1;
+      }
+      l[J] += ls0 + ls1;
+      pf[0] = pack_frag(sj[0], 0);
+      pf[1] = pack_frag(sj[0], 1);
+      pf[2] = pack_frag(sj[1], 0);
+      pf[3] = pack_frag(sj[1], 1);
+    };
+    // P.V of block J (fragments pf, V image Vb) interleaved with the exponentials + row sum of
+    // block E (scores se, in place) -- see the MASK == 3 region 2 below
+    auto pvx = [&](auto j_c, const bf16x8 (&pf)[4], const uint16_t* Vb, auto e_c, f32x16 (&se)[2]) {
+      constexpr int J = decltype(j_c)::value;
+      constexpr int E = decltype(e_c)::value;
+      constexpr int NSTEP = 4 * NDB, PER = 32 / NSTEP;  // MFMAs, softmax elements per MFMA
+      const float mc = m[E] == -INFINITY ? 0.f : m[E];
+      auto vread = [&](int step) {
+        const int kst = step / NDB, db = step % NDB, rb = kst * 16 * D;
+        return cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
+      };
+      float ls0 = 0.f, ls1 = 0.f;
+      bf16x8 va = vread(0);
+#pragma unroll
+      for (int step = 0; step < NSTEP; ++step) {
+        const bf16x8 vcur = va;
+        if (step + 1 < NSTEP) va = vread(step + 1);
+        o[J][step % NDB] = mfma32(vcur, pf[step / NDB], o[J][step % NDB]);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int e = 0; e < PER; ++e) {
+          const int i = step * PER + e;  // elements i of key half 0 and i of key half 1... (i < 16)
+          const int kb = i >> 4, ii = i & 15;
+          const float p = fast_exp2(__builtin_fmaf(se[kb][ii], c2, -mc));
+          se[kb][ii] = p;
+          if (e & 1) ls1 += p;
+          else ls0 += p;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      l[E] += ls0 + ls1;
+    };
+    auto packp = [&](f32x16 (&sj)[2], bf16x8 (&pf)[4]) {
+      pf[0] = pack_frag(sj[0], 0);
+      pf[1] = pack_frag(sj[0], 1);
+      pf[2] = pack_frag(sj[1], 0);
+      pf[3] = pack_frag(sj[1], 1);
+    };
+    auto rescale = [&](auto j_c, float mx2) {
+      constexpr int J = decltype(j_c)::value;
+      const float mnew = fmaxf(m[J], mx2);
+      const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m[J] - mnew);
+#pragma unroll
+      for (int db = 0; db < NDB; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[J][db][i] = o[J][db][i] * alpha;
+      l[J] *= alpha;
+      m[J] = mnew;
+    };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    int vcur = 0, vprev = 2;  // V buffers of tiles t and t-1 (t % 3, (t-1) % 3)
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      const int vnext = 3 - vcur - vprev;  // (t+1) % 3: neither V(t) nor V(t-1)
+#if PLLM_ABL == 1  // diagnostic: no K/V loads after the first tile (stale registers restaged)
+      if (t == 0 && t + 1 < ntiles) gload(t + 1);
+#else
+      if (t + 1 < ntiles) gload(t + 1);
+#endif
+      const int kv0 = t * BN;
+      const int mask = (kv0 < qend[0] ? 1 : 0) | (kv0 < qend[1] ? 2 : 0);
+      const uint16_t* Kb = smem + buf * TILE;
+      const uint16_t* Vb = smem + 2 * TILE + vcur * TILE;
+      const uint16_t* Vp = smem + 2 * TILE + vprev * TILE;
+      auto tile = [&](auto mask_c) {
+        constexpr int MASK = decltype(mask_c)::value;
+        f32x16 s[2][2];
+        s[0][0] = s[0][1] = s[1][0] = s[1][1] = zero16();
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+          for (int ks = 0; ks < NKS; ++ks) {
+            const bf16x8 kf = as_frag(ld16(Kb + kb * 32 * D + (fk ^ (ks << 4))));
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
+          }
+        if constexpr (MASK == 3 && kFwdSched) {
+          // K fragment reads one to two fragments ahead of the MFMAs that consume them (left to
+          // itself hipcc waited lgkmcnt(0) right before each pair of MFMAs)
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+#pragma unroll
+          for (int i = 0; i < 2 * NKS - 2; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        }
+        float mx2[2] = {-INFINITY, -INFINITY};
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          if (!((MASK >> j) & 1)) continue;
+          const int qi = qw[j] + r;
+          if ((kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off)) {
+            const int lim0 = (a.causal ? min(a.S - 1, qi + off) : a.S - 1) - (kv0 + 4 * hh);
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) s[j][kb][i] = acc_row(i, 0) > lim0 - 32 * kb ? -INFINITY : s[j][kb][i];
+          }
+          float mx0 = -INFINITY, mx1 = -INFINITY;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            mx0 = fmaxf(mx0, s[j][0][i]);
+            mx1 = fmaxf(mx1, s[j][1][i]);
+          }
+          float mx = fmaxf(mx0, mx1);
+          mx2[j] = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c2;
+        }
+        const bool r0 = (MASK & 1) && __any(mx2[0] - m[0] > kLazyThr);
+        const bool r1 = (MASK & 2) && __any(mx2[1] - m[1] > kLazyThr);
+        if (r0 || r1) {  // rare
+          if (pend && r1) {  // retire the pending P.V at the old max, then region 2 adds zeros
+            pv(I1{}, pfp, Vp);
+#pragma unroll
+            for (int kst = 0; kst < 4; ++kst) pfp[kst] = zero_frag();
+          }
+          if (r0) rescale(I0{}, mx2[0]);
+          if (r1) rescale(I1{}, mx2[1]);
+        }
+        // region 2 (one code path per MASK: a second variant of it doubled the live ranges the
+        // register allocator saw and spilled).  Without a pending P.V (first tile of block 1),
+        // pfp is zero and the current V tile stands in (finite data, adds nothing).
+        if constexpr (MASK == 3 && kFwdSched) {
+          // hand interleave (sched_barrier fences: hipcc otherwise clusters the MFMAs and the
+          // exponentials): each of the 4 NDB MFMAs of one block's P.V is followed by the softmax
+          // of 32 / (4 NDB) elements of the other block, with the next V fragment read issued one
+          // MFMA ahead
+          pvx(I1{}, pfp, pend ? Vp : Vb, I0{}, s[0]);
+          bf16x8 pf0[4];
+          packp(s[0], pf0);
+          pvx(I0{}, pf0, Vb, I1{}, s[1]);
+          packp(s[1], pfp);
+        } else {
+          if constexpr ((MASK & 2) != 0) pv(I1{}, pfp, pend ? Vp : Vb);
+          if constexpr ((MASK & 1) != 0) {
+            bf16x8 pf0[4];
+            sexp(I0{}, s[0], pf0);
+            pv(I0{}, pf0, Vb);
+          }
+          if constexpr ((MASK & 2) != 0) sexp(I1{}, s[1], pfp);
+        }
+        pend = (MASK & 2) != 0;
+      };
+      if (mask == 3) tile(std::integral_constant<int, 3>{});
+      else if (mask == 1) tile(std::integral_constant<int, 1>{});
+      else if (mask == 2) tile(std::integral_constant<int, 2>{});
+      else if (pend) {  // both blocks done with keys: retire the pending P.V
+        pv(I1{}, pfp, Vp);
+        pend = false;
+      }
+#if PLLM_ABL == 2  // diagnostic: no LDS restage, no barrier (every tile reads tile 0's images)
+      (void)vnext;
+#elif PLLM_ABL == 3  // diagnostic: restage without the barrier
+      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, vnext);
+#else
+      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, vnext);
+      __syncthreads();
+#endif
+      vprev = vcur;
+      vcur = vnext;
+    }
+    if (pend) pv(I1{}, pfp, smem + 2 * TILE + vprev * TILE);
+  } else
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     if (t + 1 < ntiles) gload(t + 1);
@@ -396,7 +629,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(AttnFwdArgs a) {
     if (mask == 3) tile(std::integral_constant<int, 3>{});
     else if (mask == 1) tile(std::integral_constant<int, 1>{});
     else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
-    if (t + 1 < ntiles) swrite(buf ^ 1, t + 1);
+    if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
     __syncthreads();
   }
 
@@ -1311,11 +1544,24 @@ bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
 int attn_bwd_key_block(int D) { return D == 128 ? RsCfg<128>::BK : BwdCfg<64>::BK; }
 
+// PLLM_ATTN_FWD_PIPE=0 selects the unpipelined tile loop for D <= 64 (A/B switch)
+static bool attn_fwd_pipe() {
+  static const bool on = [] {
+    const char* e = std::getenv("PLLM_ATTN_FWD_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
-  if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
-  else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), dim3(nqb * a.B * a.H), dim3(256), 0, st, a);
+  const dim3 grid(nqb * a.B * a.H);
+  if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, st, a);
+  else if constexpr (FwdCfg<D>::QB == 2) {
+    if (attn_fwd_pipe()) hipLaunchKernelGGL((attn_fwd_kernel<D, false, true>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);
+  } else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);
 }
 
 template <int D, int ROPE>

@@ -440,9 +440,28 @@ class _FlashAttnPacked(torch.autograd.Function):
             k = qk[..., H * D:].view(B, T, Hkv, D)
         dqkv = torch.empty_like(qkv)
         dq, dk, dv = _split_qkv(dqkv, H, Hkv, D)
+        _attn_ws(qkv.device)
         _ops().attn_bwd(do.contiguous().view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin,
                         qk is None)
         return dqkv, None, None, None, None, None, None
+
+
+_ATTN_WS_MB = [None]
+
+
+def _attn_ws(device):
+    """Attention-backward dQ slab budget from the HBM still free (utils/memory.py: a quarter of
+    it, capped at the 4 GiB that keeps every shipped config in one pass, floored at 64 MiB),
+    quantised to 256 MiB steps so it is re-sent to the extension only when it moves;
+    PLLM_ATTN_BWD_WS_MB fixes it instead."""
+    if "PLLM_ATTN_BWD_WS_MB" in os.environ:
+        return
+    from ..utils import memory as _mem
+    b = _mem.workspace_budget(device, _mem.ATTN_WS_CAP, _mem.ATTN_WS_FRACTION, _mem.ATTN_WS_FLOOR)
+    mb = max(64.0, float(b // (256 * _mem.MiB) * 256))
+    if mb != _ATTN_WS_MB[0]:
+        _ops().attn_bwd_set_workspace_mb(mb)
+        _ATTN_WS_MB[0] = mb
 
 
 # RoPE for the HIP attention: pre-pass rotation (default) or rotation inside the kernels' tile loops
@@ -544,6 +563,7 @@ def attention_block_bwd(do, q, k, v, o, lse, causal: bool = True, scale: Optiona
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     if _hip(q):
         dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+        _attn_ws(q.device)
         _ops().attn_bwd(do, q, k, v, o, lse.contiguous(), dq, dk, dv, causal, scale)
         return dq, dk, dv
     return ref.attention_bwd(do, q, k, v, o, lse, causal=causal, scale=scale)
@@ -695,16 +715,26 @@ def embedding(idx, wte, wpe=None, pos_offset: int = 0):
 # measured slower: sub-chunks of 1K / 2K / 4K rows for GEMM -> CE -> dgrad (logits kept in the
 # Infinity Cache between them) with one weight-gradient GEMM over the whole dlogits afterwards:
 # 75.7 / 68.5 / 66.6 ms vs 60.5 ms per step (scripts/gpu/r2_cesub.sh, profiles/r2_ce_subchunk_negative.txt).
+# The workspace budget is a quarter of the HBM the device can still give (utils/memory.py),
+# capped at those 8 GiB and floored at 256 MiB; PLLM_CE_WORKSPACE_MB fixes it instead.
 CE_CHUNK_ROWS = int(_os.environ.get("PLLM_CE_CHUNK_ROWS", "0"))
-CE_WORKSPACE_MB = float(_os.environ.get("PLLM_CE_WORKSPACE_MB", "8192"))
+CE_WORKSPACE_MB = float(_os.environ["PLLM_CE_WORKSPACE_MB"]) if "PLLM_CE_WORKSPACE_MB" in _os.environ else None
 
 
-def _ce_chunk_rows(N: int, V: int = 50304) -> int:
+def _ce_budget_bytes(device) -> int:
+    if CE_WORKSPACE_MB is not None:
+        return int(CE_WORKSPACE_MB * 2 ** 20)
+    from ..utils import memory as _mem
+    return _mem.workspace_budget(device, _mem.CE_CAP, _mem.CE_FRACTION, _mem.CE_FLOOR)
+
+
+def _ce_chunk_rows(N: int, V: int = 50304, budget_bytes: Optional[int] = None) -> int:
     if CE_CHUNK_ROWS > 0:
         r = max(64, CE_CHUNK_ROWS // 64 * 64)
         return N if N <= r else r
     per_row = 2 * V
-    n_chunks = max(1, math.ceil(N * per_row / (CE_WORKSPACE_MB * 2 ** 20)))
+    budget = budget_bytes if budget_bytes is not None else 8192 * 2 ** 20
+    n_chunks = max(1, math.ceil(N * per_row / budget))
     if n_chunks == 1:
         return N
     return max(64, (math.ceil(N / n_chunks) + 63) // 64 * 64)
@@ -720,7 +750,7 @@ class _LMHeadCEFn(torch.autograd.Function):
         need_h = ctx.needs_input_grad[0]
         need_w = ctx.needs_input_grad[1]
         need_b = bias is not None and ctx.needs_input_grad[2]
-        R = _ce_chunk_rows(N, V)
+        R = _ce_chunk_rows(N, V, _ce_budget_bytes(h.device))
         ws = torch.empty(R, V, dtype=h.dtype, device=h.device)
         dh = torch.empty_like(h) if need_h else None
         dw = torch.zeros(V, C, dtype=torch.float32, device=h.device) if need_w else None
@@ -782,7 +812,7 @@ def lm_head_cross_entropy(h, weight, bias, targets, ignore_index: int = -100):
         return _LMHeadCEFn.apply(h, weight, bias, targets, ignore_index)
     if _hip_op("ce", h):
         N, V = h.shape[0], weight.shape[0]
-        R = _ce_chunk_rows(N, V)
+        R = _ce_chunk_rows(N, V, _ce_budget_bytes(h.device))
         ws = torch.empty(R, V, dtype=h.dtype, device=h.device)
         rows = torch.empty(N, dtype=torch.float32, device=h.device)
         for r0 in range(0, N, R):

@@ -1,0 +1,49 @@
+"""Workspace budgets derived from the HBM actually free on the device.
+
+Two transient workspaces scale with the problem rather than with the model: the LM-head +
+cross-entropy logits chunk (``ops._LMHeadCEFn``: rows x vocab bf16) and the attention
+backward's dQ partial slabs (``attn_bwd``: key blocks x B x H x T x D bf16).  Fixed budgets
+(8 GiB / 4 GiB) were sized on one box; with tensor / context-parallel shards, larger
+vocabularies or a fuller HBM they either waste memory or run the device out of it.  Here each
+budget is ``fraction`` of what the device can still give -- free HBM (``hipMemGetInfo``) plus
+what the caching allocator holds reserved but unused -- clamped to [floor, cap].  The cap keeps
+the measured single-chunk / single-pass behaviour of the shipped configs (bigger chunks buy
+nothing); the floor keeps the chunking from degenerating.  Environment overrides
+(``PLLM_CE_WORKSPACE_MB``, ``PLLM_ATTN_BWD_WS_MB``) still win.
+"""
+from __future__ import annotations
+
+from typing import Callable, Optional
+
+import torch
+
+MiB = 2 ** 20
+
+
+def free_hbm_bytes(device: torch.device) -> int:
+    """Bytes a new allocation on ``device`` can get: free device memory plus the caching
+    allocator's reserved-but-unallocated pool."""
+    if device.type != "cuda":
+        return 1 << 62
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    free, _total = torch.cuda.mem_get_info(idx)
+    slack = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)
+    return int(free + max(0, slack))
+
+
+def workspace_budget(device: torch.device, cap_bytes: int, fraction: float, floor_bytes: int,
+                     free_fn: Optional[Callable[[torch.device], int]] = None) -> int:
+    """``fraction`` x free HBM, clamped to [floor_bytes, cap_bytes] (CPU: the cap)."""
+    if device.type != "cuda" and free_fn is None:
+        return int(cap_bytes)
+    free = (free_fn or free_hbm_bytes)(device)
+    return int(max(floor_bytes, min(cap_bytes, fraction * free)))
+
+
+# defaults: caps = the budgets measured to keep every shipped config in one chunk / pass
+CE_CAP = 8192 * MiB
+CE_FRACTION = 0.25
+CE_FLOOR = 256 * MiB
+ATTN_WS_CAP = 4096 * MiB
+ATTN_WS_FRACTION = 0.25
+ATTN_WS_FLOOR = 64 * MiB

@@ -131,3 +131,20 @@ def test_grad_clipping():
     assert torch.allclose(n, ref, rtol=1e-5)
     opt.step()
     assert opt.last_grad_norm is not None
+
+
+def test_workspace_budgets_follow_free_hbm():
+    """LM-head/CE chunk and attention-backward slab budgets: a quarter of the free HBM, clamped to
+    [floor, cap] (utils/memory.py); a small budget splits the CE rows into 64-aligned chunks."""
+    from pretraining_llm_amd.ops import _ce_chunk_rows
+    from pretraining_llm_amd.utils import memory as M
+    dev = torch.device("cuda", 0)
+    GiB = 2 ** 30
+    assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 200 * GiB) == M.CE_CAP
+    assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 8 * GiB) == 2 * GiB
+    assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 0) == M.CE_FLOOR
+    assert M.workspace_budget(torch.device("cpu"), 5, 0.25, 1) == 5
+    N, V = 65536, 50304  # GPT-2 small B64 x T1024
+    assert _ce_chunk_rows(N, V, M.CE_CAP) == N                     # one chunk with a roomy device
+    r = _ce_chunk_rows(N, V, 2 * GiB)                               # a fuller device: 4 chunks
+    assert r % 64 == 0 and -(-N // r) == 4 and r * V * 2 <= 2 * GiB + 64 * V * 2
