@@ -167,8 +167,17 @@ struct Img {
 // past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
 // lazy-max threshold of the forward's online softmax, log2 units (p <= 2^8)
 constexpr float kLazyThr = 8.f;
+#ifndef PLLM_FWD_V3
+#define PLLM_FWD_V3 0
+#endif
 #ifndef PLLM_FWD_SCHED
 #define PLLM_FWD_SCHED 1
+#endif
+#ifndef PLLM_FWD_STAMPS
+#define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the plain forward loop
+#endif
+#ifndef PLLM_BWD_STAGGER
+#define PLLM_BWD_STAGGER 0  // diagnostic: s_sleep units (64 cycles) for waves 4-7 per backward iteration
 #endif
 #ifndef PLLM_ABL
 #define PLLM_ABL 0  // diagnostic ablations of the pipelined forward (scripts/gpu/r3_attn_abl.sh)
@@ -196,9 +205,10 @@ struct FwdCfg {
   static constexpr int LDS_ELEMS_PIPE = 5 * TILE;
 };
 
-template <int D, bool ROPE, bool PIPE = false>
+template <int D, bool ROPE, bool PIPE = false, bool V3 = false>
 __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArgs a) {
   static_assert(!PIPE || (FwdCfg<D>::QB == 2 && !ROPE), "pipelined tile loop: QB = 2, no fused RoPE");
+  static_assert(!V3 || (!PIPE && !ROPE), "sum-checked softmax: plain tile loop, no fused RoPE");
   using C = FwdCfg<D>;
   using I = Img<D>;
   constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, TILE = C::TILE, QB = C::QB, NW = C::NW;
@@ -243,6 +253,17 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
       for (int ks = 0; ks < NKS / 2; ++ks)
         rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
               1.f);
+    }
+    if constexpr (V3) {
+      // scores straight in log2 units: Q x (scale log2 e), rounded once to bf16
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        float f[8];
+        unpack8(raw[ks], f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] *= a.scale_log2;
+        raw[ks] = pack8(f);
+      }
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) qf[j][ks] = as_frag(raw[ks]);
@@ -315,6 +336,10 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
   }
   const float c2 = a.scale_log2;
 
+#if PLLM_FWD_STAMPS
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t st_start = __builtin_amdgcn_s_memtime();
+#endif
   if (ntiles > 0) {
     gload(0);
     swrite(0, 0, 0);
@@ -532,10 +557,146 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
       vcur = vnext;
     }
     if (pend) pv(I1{}, pfp, smem + 2 * TILE + vprev * TILE);
+  } else if constexpr (V3) {
+    // ---- exponent-ready scores ---------------------------------------------------------------
+    // Q is prescaled by scale log2(e), so S' = Q'K^T - m is already the exponent: the MFMA chain
+    // of every score block starts from a register block holding -m (nm, the chain's C operand)
+    // and p = exp2(S') needs no per-element multiply-add.  m is set from the row max on a block's
+    // first live tile and moved lazily (when a row's tile max exceeds it by kLazyThr, as in the
+    // plain loop), the rare move shifting S' and the -m block.
+    f32x16 nm[QB];
+    bool started[QB];
+#pragma unroll
+    for (int j = 0; j < QB; ++j) {
+      nm[j] = zero16();
+      started[j] = false;
+    }
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = t & 1;
+      if (t + 1 < ntiles) gload(t + 1);
+      const int kv0 = t * BN;
+      const int mask = (kv0 < qend[0] ? 1 : 0) | (QB > 1 && kv0 < qend[QB - 1] ? 2 : 0);
+      const uint16_t* Kb = smem + buf * TILE;
+      const uint16_t* Vb = smem + 2 * TILE + buf * TILE;
+      auto tile = [&](auto mask_c) {
+        constexpr int MASK = decltype(mask_c)::value;
+        f32x16 s[QB][2];
+        auto qk = [&](auto only_c) {  // only_c: -1 = every live block, else that block alone
+          constexpr int ONLY = decltype(only_c)::value;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int ks = 0; ks < NKS; ++ks) {
+              const bf16x8 kf = as_frag(ld16(Kb + kb * 32 * D + (fk ^ (ks << 4))));
+#pragma unroll
+              for (int j = 0; j < QB; ++j)
+                if (((MASK >> j) & 1) && (ONLY < 0 || ONLY == j))
+                  s[j][kb] = mfma32(kf, qf[j][ks], ks == 0 ? nm[j] : s[j][kb]);
+            }
+        };
+        qk(std::integral_constant<int, -1>{});
+        bf16x8 pf[QB][4];
+#pragma unroll
+        for (int j = 0; j < QB; ++j) {
+          if (!((MASK >> j) & 1)) continue;
+          const int qi = qw[j] + r;
+          const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off);
+          const int lim0 = (a.causal ? min(a.S - 1, qi + off) : a.S - 1) - (kv0 + 4 * hh);
+          auto apply_mask = [&]() {
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) s[j][kb][i] = acc_row(i, 0) > lim0 - 32 * kb ? -INFINITY : s[j][kb][i];
+          };
+          auto rowmax = [&]() {
+            float mx0 = -INFINITY, mx1 = -INFINITY;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              mx0 = fmaxf(mx0, s[j][0][i]);
+              mx1 = fmaxf(mx1, s[j][1][i]);
+            }
+            const float mx = fmaxf(mx0, mx1);
+            return fmaxf(mx, __shfl_xor(mx, 32, 64));
+          };
+          auto shift = [&](float dm) {  // S' -= dm, m += dm, -m block follows
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) s[j][kb][i] -= dm;
+            m[j] += dm;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) nm[j][i] = -m[j];
+          };
+          auto expsum = [&]() {
+            float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const float p0 = fast_exp2(s[j][0][i]);
+              const float p1 = fast_exp2(s[j][1][i]);
+              s[j][0][i] = p0;
+              s[j][1][i] = p1;
+              ls0 += p0;
+              ls1 += p1;
+            }
+            return ls0 + ls1;
+          };
+          if (need_mask) apply_mask();
+          const float mx = rowmax();  // relative to the current reference m
+          if (!started[j]) {  // wave-uniform: the block's first live tile sets m
+            m[j] = 0.f;
+            shift(mx == -INFINITY ? 0.f : mx);
+            started[j] = true;
+          } else if (__any(mx > kLazyThr)) {  // rare: move the reference max
+            const float dm = fmaxf(mx, 0.f);
+            const float alpha = fast_exp2(-dm);
+#pragma unroll
+            for (int db = 0; db < NDB; ++db)
+#pragma unroll
+              for (int i = 0; i < 16; ++i) o[j][db][i] = o[j][db][i] * alpha;
+            l[j] *= alpha;
+            shift(dm);
+          }
+          const float ls = expsum();
+          l[j] += ls;
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            pf[j][2 * kb] = pack_frag(s[j][kb], 0);
+            pf[j][2 * kb + 1] = pack_frag(s[j][kb], 1);
+          }
+        }
+#pragma unroll
+        for (int kst = 0; kst < 4; ++kst)
+#pragma unroll
+          for (int db = 0; db < NDB; ++db) {
+            const int rb = kst * 16 * D;
+            const bf16x8 va = cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
+#pragma unroll
+            for (int j = 0; j < QB; ++j)
+              if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
+          }
+      };
+      if (mask == 3) tile(std::integral_constant<int, 3>{});
+      else if (mask == 1) tile(std::integral_constant<int, 1>{});
+      else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
+      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
+      __syncthreads();
+    }
   } else
   for (int t = 0; t < ntiles; ++t) {
+#if PLLM_FWD_STAMPS
+    uint64_t ts_prev = __builtin_amdgcn_s_memtime();
+    auto stamp = [&](int i) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      st_acc[i] += now - ts_prev;
+      ts_prev = now;
+    };
+#define PLLM_STAMP(i) stamp(i)
+#else
+#define PLLM_STAMP(i)
+#endif
     const int buf = t & 1;
     if (t + 1 < ntiles) gload(t + 1);
+    PLLM_STAMP(0);
     const int kv0 = t * BN;
     // which of this wave's blocks see keys of this tile: a compile-time mask per code
     // path, so no MFMA is predicated (an if-converted MFMA keeps both results live)
@@ -557,6 +718,7 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
             if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
         }
       }
+      PLLM_STAMP(1);
       bf16x8 pf[QB][4];
 #pragma unroll
       for (int j = 0; j < QB; ++j) {
@@ -614,6 +776,7 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
           pf[j][2 * kb + 1] = pack_frag(s[j][kb], 1);
         }
       }
+      PLLM_STAMP(2);
 #pragma unroll
       for (int kst = 0; kst < 4; ++kst) {
 #pragma unroll
@@ -629,10 +792,26 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
     if (mask == 3) tile(std::integral_constant<int, 3>{});
     else if (mask == 1) tile(std::integral_constant<int, 1>{});
     else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
+    PLLM_STAMP(3);
     if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
+    PLLM_STAMP(4);
     __syncthreads();
+    PLLM_STAMP(5);
+#if PLLM_FWD_STAMPS
+    st_acc[6] += 1;
+    st_acc[7] += (uint64_t)mask;
+#endif
   }
+#undef PLLM_STAMP
 
+#if PLLM_FWD_STAMPS
+  if (a.stamps && lane == 0) {
+    unsigned long long* st = a.stamps + ((int64_t)blockIdx.x * NW + w) * 9;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) st[i] = st_acc[i];
+    st[8] = __builtin_amdgcn_s_memtime() - st_start;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < QB; ++j) {
     const int qi = qw[j] + r;
@@ -906,6 +1085,10 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     flush_dq();
     __syncthreads();
     if (it + 1 < total) gload(it + 1);
+#if PLLM_BWD_STAGGER > 0
+    // diagnostic: delay the second half of the workgroup (the SIMD partners of waves 0-3)
+    if (__builtin_amdgcn_readfirstlane(w) >= 4) __builtin_amdgcn_s_sleep(PLLM_BWD_STAGGER);
+#endif
 
     // rows past T need no mask: their Q / dO rows are zero-filled, their row constants 0
     const bool need_mask = (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
@@ -1544,11 +1727,11 @@ bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
 int attn_bwd_key_block(int D) { return D == 128 ? RsCfg<128>::BK : BwdCfg<64>::BK; }
 
-// PLLM_ATTN_FWD_PIPE=0 selects the unpipelined tile loop for D <= 64 (A/B switch)
+// PLLM_ATTN_FWD_PIPE=1 selects the software-pipelined tile loop for D <= 64 (A/B switch)
 static bool attn_fwd_pipe() {
   static const bool on = [] {
     const char* e = std::getenv("PLLM_ATTN_FWD_PIPE");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';  // opt-in: measured no faster than the plain loop (profiles/r3_attn_fwd_*)
   }();
   return on;
 }
@@ -1558,6 +1741,7 @@ static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
   const dim3 grid(nqb * a.B * a.H);
   if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, st, a);
+  else if constexpr (PLLM_FWD_V3 != 0) hipLaunchKernelGGL((attn_fwd_kernel<D, false, false, true>), grid, dim3(256), 0, st, a);
   else if constexpr (FwdCfg<D>::QB == 2) {
     if (attn_fwd_pipe()) hipLaunchKernelGGL((attn_fwd_kernel<D, false, true>), grid, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);

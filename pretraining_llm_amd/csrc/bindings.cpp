@@ -4,6 +4,7 @@
 // (a wrong shape must fail here, never fault on the GPU) and launches on the
 // current HIP stream, so the ops compose with torch streams and hipGraph capture.
 #include <ATen/ATen.h>
+#include <cstdio>
 #include <cstdlib>
 #include <c10/hip/HIPStream.h>
 #include <torch/library.h>
@@ -686,7 +687,25 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
+  // diagnostic (a PLLM_FWD_STAMPS=1 build of attention.hip + this env): per-wave phase cycles of
+  // the forward's tile loop, summed and printed to stderr after the launch
+  static const bool stamps = std::getenv("PLLM_FWD_STAMPS") != nullptr;
+  Tensor st;
+  if (stamps && D <= 64) {
+    const int64_t nqb = (T + 255) / 256;
+    st = at::zeros({nqb * B * H * 4 * 9}, q.options().dtype(at::kLong));
+    a.stamps = (unsigned long long*)st.data_ptr();
+  }
   if (B * T * H > 0 && S > 0) pllm::attn_fwd(a, cur_stream());
+  if (st.defined()) {
+    auto h = st.view({-1, 9}).to(at::kCPU).to(at::kDouble);
+    auto tot = h.sum(0);
+    const double tiles = tot[6].item<double>();
+    fprintf(stderr, "[fwd stamps] waves %lld tiles %.0f | per tile: gload %.0f qk %.0f softmax %.0f pv %.0f swrite %.0f barrier %.0f | per wave total %.0f (mask sum %.0f)\n",
+            (long long)h.size(0), tiles, tot[0].item<double>() / tiles, tot[1].item<double>() / tiles,
+            tot[2].item<double>() / tiles, tot[3].item<double>() / tiles, tot[4].item<double>() / tiles,
+            tot[5].item<double>() / tiles, tot[8].item<double>() / h.size(0), tot[7].item<double>());
+  }
   return {o, lse};
 }
 

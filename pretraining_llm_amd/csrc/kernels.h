@@ -17,6 +17,7 @@ struct AttnFwdArgs {
   int64_t q_sb, q_st, q_sh, k_sb, k_st, k_sh, v_sb, v_st, v_sh, o_sb, o_st, o_sh;
   float scale, scale_log2;
   int causal;
+  unsigned long long* stamps;  // diagnostic builds only (PLLM_FWD_STAMPS): per-wave phase cycles
 };
 
 // q [B, H, D] (one query per sequence), k/v rows of a [B, S_max, Hkv, D]-strided cache
