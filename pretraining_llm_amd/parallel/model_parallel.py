@@ -17,6 +17,10 @@ per-layer all-reduces are the latency-critical traffic):
   per rank; all-gather before each column-parallel GEMM, reduce-scatter after each
   row-parallel one, LM head + CE on the local tokens.  Replicated parameters then carry
   partial gradients, which ``sync_replicated_grads`` sums over the TP group.
+* **TP x CP**: both at once -- each rank keeps its heads (TP) of its sequence shard (CP) and runs
+  ring / Ulysses attention over the CP group on the local heads; the MLP is TP-sharded.
+* **SP without W_o** (the reference architecture): the concatenated heads return to sequence
+  shards by one all-to-all over the TP group instead of a W_o reduce-scatter.
 * **CP** (``cp_size``): the sequence is sharded over the CP group.  ``cp_mode="ring"``:
   load-balanced zigzag layout, ring attention over RCCL point-to-point with the flash kernels'
   LSE merge (``parallel/context.py``); ``cp_mode="ulysses"``: contiguous shards, all-to-all to
@@ -152,16 +156,25 @@ class TPAttention(nn.Module):
                 if dense.proj.bias is not None:
                     self.proj.bias.copy_(dense.proj.bias)
             _mark_sharded(self.proj.weight)  # the bias stays replicated
-        elif pg.sequence_parallel:
-            raise ValueError("sequence_parallel needs an attention output projection (arch without W_o: use plain TP)")
 
     def forward(self, x, rope=None, fuse_out_bias: bool = False):
         g = self.pg.tp_group
         x = tpar.gather_from_sequence(x, g) if self.pg.sequence_parallel else tpar.copy_to_tensor_parallel(x, g)
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
-        cos, sin = rope if rope is not None else (None, None)
-        y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
+        if self.pg.cp > 1:
+            # 2-D: this rank's heads (TP) of this rank's sequence shard (CP), attention over the CP
+            # group -- ring or Ulysses on the local heads
+            y = cp_attention(qkv, self.n_head, self.n_kv_head, self.head_dim, rope, self.pg)
+        else:
+            cos, sin = rope if rope is not None else (None, None)
+            y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is None:  # reference architecture: no W_o -> the heads are concatenated
+            if self.pg.sequence_parallel:
+                # back to sequence shards with every head: one all-to-all (head -> sequence
+                # re-sharding, the Ulysses primitive) instead of a W_o reduce-scatter
+                B, T, _ = y.shape
+                yh = y.view(B, T, self.n_head, self.head_dim)
+                return tpar.head_to_seq_all_to_all(yh, g).reshape(B, T // self.pg.tp, -1)
             return tpar.gather_from_tensor_parallel(y, g)
         y = ops.linear(y, self.proj.weight, None)
         y = tpar.reduce_scatter_to_sequence(y, g) if self.pg.sequence_parallel else tpar.reduce_from_tensor_parallel(y, g)
@@ -218,6 +231,28 @@ class TPMLP(nn.Module):
         return y + self.proj.bias if self.proj.bias is not None else y
 
 
+def cp_attention(qkv, H: int, Hkv: int, D: int, rope, pg: ParallelGroups):
+    """Causal attention of a context-parallel shard: ``qkv`` [B, T_l, (H + 2 Hkv) D] (packed, this
+    rank's heads) -> [B, T_l, H D].  RoPE is applied on the shard with its own position tables
+    first; then ring attention over the CP group (zigzag shards) or Ulysses (contiguous shards:
+    all-to-all to head sharding, full-sequence flash attention, all-to-all back)."""
+    g = pg.cp_group
+    if rope is not None:
+        qkv = ops.rope_packed(qkv, rope[0], rope[1], H, Hkv)
+    B, Tl, _ = qkv.shape
+    q, k, v = ops._split_qkv(qkv, H, Hkv, D)
+    if pg.cp_mode == "ulysses":
+        if H % pg.cp or Hkv % pg.cp:
+            raise ValueError(f"Ulysses: local n_head {H} and n_kv_head {Hkv} must be divisible by cp_size {pg.cp}")
+        qh, kh, vh = (tpar.seq_to_head_all_to_all(t.contiguous(), g) for t in (q, k, v))  # [B, T, h/cp, D]
+        T, Hl, Hkl = qh.shape[1], qh.shape[2], kh.shape[2]
+        packed = torch.cat([qh, kh, vh], dim=2).reshape(B, T, (Hl + 2 * Hkl) * D)
+        o = ops.attention_packed(packed, Hl, Hkl, causal=True).view(B, T, Hl, D)
+        return tpar.head_to_seq_all_to_all(o, g).reshape(B, Tl, H * D)
+    y = cpar.ring_attention(q, k, v, g, causal=True, layout="zigzag")
+    return y.reshape(B, Tl, H * D)
+
+
 class CPAttention(nn.Module):
     """Attention of a zigzag sequence shard: dense projections, ring attention over the CP group
     (RoPE applied with the shard's own position tables before the ring)."""
@@ -231,13 +266,8 @@ class CPAttention(nn.Module):
         self.n_head, self.n_kv_head, self.head_dim = dense.n_head, dense.n_kv_head, dense.head_dim
 
     def forward(self, x, rope=None, fuse_out_bias: bool = False):
-        H, Hkv, D = self.n_head, self.n_kv_head, self.head_dim
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
-        if rope is not None:
-            qkv = ops.rope_packed(qkv, rope[0], rope[1], H, Hkv)  # local (zigzag) position tables
-        q, k, v = ops._split_qkv(qkv, H, Hkv, D)
-        y = cpar.ring_attention(q, k, v, self.pg.cp_group, causal=True, layout="zigzag")
-        y = y.reshape(*qkv.shape[:2], H * D)
+        y = cp_attention(qkv, self.n_head, self.n_kv_head, self.head_dim, rope, self.pg)
         if self.proj is not None:
             y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
         return y
@@ -264,17 +294,8 @@ class UlyssesAttention(nn.Module):
         self.n_head, self.n_kv_head, self.head_dim = dense.n_head, dense.n_kv_head, dense.head_dim
 
     def forward(self, x, rope=None, fuse_out_bias: bool = False):
-        H, Hkv, D, g = self.n_head, self.n_kv_head, self.head_dim, self.pg.cp_group
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
-        if rope is not None:
-            qkv = ops.rope_packed(qkv, rope[0], rope[1], H, Hkv)  # the shard's own position tables
-        B, Tl, _ = qkv.shape
-        q, k, v = ops._split_qkv(qkv, H, Hkv, D)
-        qh, kh, vh = (tpar.seq_to_head_all_to_all(t.contiguous(), g) for t in (q, k, v))  # [B, T, h/cp, D]
-        T, Hl, Hkl = qh.shape[1], qh.shape[2], kh.shape[2]
-        packed = torch.cat([qh, kh, vh], dim=2).reshape(B, T, (Hl + 2 * Hkl) * D)
-        o = ops.attention_packed(packed, Hl, Hkl, causal=True).view(B, T, Hl, D)
-        y = tpar.head_to_seq_all_to_all(o, g).reshape(B, Tl, H * D)
+        y = cp_attention(qkv, self.n_head, self.n_kv_head, self.head_dim, rope, self.pg)
         if self.proj is not None:
             y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
         return y
@@ -282,8 +303,8 @@ class UlyssesAttention(nn.Module):
 
 def parallelize_gpt(model, pg: ParallelGroups):
     """Shard a dense ``GPT`` in place for ``pg`` (TP: heads / FFN columns; CP: ring attention)."""
-    if pg.tp > 1 and pg.cp > 1:
-        raise ValueError("choose tensor parallelism OR context parallelism for one model (tp_size or cp_size)")
+    if pg.tp > 1 and pg.cp > 1 and pg.sequence_parallel:
+        raise ValueError("sequence_parallel with context parallelism is not supported (use tp x cp without SP)")
     cfg = model.config
     for blk in model.attn_blocks:
         if pg.tp > 1:

@@ -100,14 +100,20 @@ class Trainer:
             # the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/), as bench.py uses them
             from ..utils.gemm_tuning import enable_tuned_gemms
             self.tuned_gemms = enable_tuned_gemms(self.device.index or 0)
-        self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
         # model parallelism (parallel/model_parallel.py): a dp x cp x tp mesh; the model is built
-        # dense from the shared seed, then sharded, so every layout starts from the same weights
+        # dense from the shared seed, then sharded, so every layout starts from the same weights.
+        # Sharded layouts build and slice the dense model in HOST memory and move only this
+        # rank's shards to the GPU: no rank ever holds the dense model in HBM (the point of TP
+        # is models that do not fit one device)
         tp, cp = int(self.cfg.get("tp_size", 1)), int(self.cfg.get("cp_size", 1))
         self.pg = init_parallel_groups(tp, cp, bool(self.cfg.get("sequence_parallel", False)),
                                        self.cfg.get("cp_mode", "ring"))
         if self.pg.model_parallel:
+            self.model = GPT(self.mcfg)
             parallelize_gpt(self.model, self.pg)
+            self.model = self.model.to(device=self.device, dtype=self.dtype)
+        else:
+            self.model = GPT(self.mcfg).to(device=self.device, dtype=self.dtype)
         decay_filter = None if self.cfg.get("weight_decay_all", True) else no_decay_1d
         okw = dict(lr=self.cfg["t_lr"], betas=tuple(self.cfg.get("betas", (0.9, 0.999))),
                    eps=self.cfg.get("eps", 1e-8), weight_decay=self.cfg.get("weight_decay", 0.01),

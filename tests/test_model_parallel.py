@@ -137,6 +137,13 @@ CASES = {
     "ulysses2_gpt2": (2, "gpt2", 1, 2, False, False, "ulysses"),
     "ulysses2_llama_gqa_rope": (2, "llama", 1, 2, False, False, "ulysses"),
     "ulysses2_dp2_zero_llama": (4, "llama", 1, 2, False, True, "ulysses"),
+    # 2-D: tensor x context parallelism (heads over TP, sequence over CP), and sequence
+    # parallelism for the reference architecture (no W_o: heads return to sequence shards by an
+    # all-to-all)
+    "tp2_ulysses2_gpt2": (4, "gpt2", 2, 2, False, False, "ulysses"),
+    "tp2_ring2_llama_gqa_rope": (4, "llama", 2, 2, False, False, "ring"),
+    "tp2_ring2_ref_no_wo": (4, "ref", 2, 2, False, False, "ring"),
+    "tp2_sp_ref_no_wo": (2, "ref", 2, 1, True, False),
 }
 
 
