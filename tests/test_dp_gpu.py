@@ -159,6 +159,7 @@ def _zero_worker(rank, world, port, outdir):
             _, loss = model(x, y, return_logits=False)
             loss.backward()
             opt.step(grad_scale=eng.finish_grad_sync())
+        opt.wait_params()  # ZeRO-1 weight all-gathers are consumed lazily by the next forward
         torch.cuda.synchronize()
         out[name] = opt.flat_param[:opt.params[-1].numel() + max(opt.offsets.values())].float().cpu()
         out[name + "_state"] = opt.master.numel()

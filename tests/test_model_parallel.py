@@ -95,6 +95,7 @@ def _worker(rank, world, port, outdir, arch, tp, cp, sp, zero, cp_mode="ring"):
         out["grads"] = {n: p.detach().clone() for n, p in gd.named_parameters()}
     out["norm"] = float(opt.grad_norm(scale))
     opt.step(grad_scale=scale)
+    opt.wait_params()  # ZeRO-1: the step's weight all-gathers are consumed lazily (next forward)
     wd = gather_dense_state(model, GPT(cfg), pg)
     out["weights"] = {n: p.detach().clone() for n, p in wd.named_parameters()}
     lt = loss.detach().reshape(1).clone()
