@@ -176,6 +176,9 @@ constexpr float kLazyThr = 8.f;
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the plain forward loop
 #endif
+#ifndef PLLM_BWD_STAMPS
+#define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
+#endif
 #ifndef PLLM_BWD_STAGGER
 #define PLLM_BWD_STAGGER 0  // diagnostic: s_sleep units (64 cycles) for waves 4-7 per backward iteration
 #endif
@@ -1055,8 +1058,22 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   if (total > 0) gload(0);
   // (head, query block) of iteration it, advanced incrementally (no integer division per step)
   int h = hk * G, qbi = qb_start;
+#if PLLM_BWD_STAMPS
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t st_start = __builtin_amdgcn_s_memtime();
+  uint64_t ts_prev = st_start;
+  auto stamp = [&](int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    st_acc[i] += now - ts_prev;
+    ts_prev = now;
+  };
+#define PLLM_BSTAMP(i) stamp(i)
+#else
+#define PLLM_BSTAMP(i)
+#endif
   for (int it = 0; it < total; ++it, (++qbi == nqb) ? (qbi = qb_start, ++h) : 0) {
     const int q0 = qbi * BQ;
+    PLLM_BSTAMP(7);
     // opaque per iteration: the (j, g) store offsets derived from it are formed next to their
     // stores instead of being hoisted out of the loop as 16 live registers
     int fs = fs0;
@@ -1066,6 +1083,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     // join and wait vmcnt(0) again before the next prefetch -- on the fresh dQ stores
     vm_wait_all();
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done
+    PLLM_BSTAMP(0);
 #pragma unroll
     for (int i = 0; i < 2 * QPAIR; i += 2) {
       const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
@@ -1084,7 +1102,9 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     }
     flush_dq();
     __syncthreads();
+    PLLM_BSTAMP(1);
     if (it + 1 < total) gload(it + 1);
+    PLLM_BSTAMP(2);
 #if PLLM_BWD_STAGGER > 0
     // diagnostic: delay the second half of the workgroup (the SIMD partners of waves 0-3)
     if (__builtin_amdgcn_readfirstlane(w) >= 4) __builtin_amdgcn_s_sleep(PLLM_BWD_STAGGER);
@@ -1220,7 +1240,9 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         body(std::integral_constant<int, 1>{}, TT{});
       }
     }
+    PLLM_BSTAMP(3);
     __syncthreads();
+    PLLM_BSTAMP(4);
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
     // this pass's fp32 slab of the key block.
@@ -1231,11 +1253,12 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
       if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
-      // causal: key steps entirely after the task's last query contribute zeros -> skip
-      int ks_end = BK / 16;
-      if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
       // dQ^T tile = K^T dS^T (query on the lane), dumped as a coalesced fragment-order block
-      // (attn_dq_reduce_frag_kernel reads it back)
+      // (attn_dq_reduce_frag_kernel reads it back).  Every key step runs, also the causal ones
+      // past the task's last query: their dS^T rows are zeros in the image (dead sub-blocks are
+      // zero-filled, masked elements give p = 0), and with no data-dependent exit the LDS reads
+      // pipeline ahead of the MFMAs (the early exit serialised read -> wait -> MFMA per step:
+      // ~2.9k of a 13.4k-cycle iteration, profiles/r3_attn_bwd_stamps.md)
       f32x16 acc = zero16();
       // key rows 16 ks + 8 hh + tq (+4): the 16 ks steps are additions (see fq above)
       const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
@@ -1243,7 +1266,6 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       const int ka0 = I::off(8 * hh + tq, dc), ka4 = I::off(8 * hh + tq + 4, dc);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        if (ks >= ks_end) break;
         const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
         const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
@@ -1259,7 +1281,20 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
                 ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
     }
+    PLLM_BSTAMP(5);
+#if PLLM_BWD_STAMPS
+    st_acc[6] += 1;
+#endif
   }
+#undef PLLM_BSTAMP
+#if PLLM_BWD_STAMPS
+  if (a.stamps && lane == 0) {
+    unsigned long long* stp = a.stamps + ((int64_t)blockIdx.x * C::NW + w) * 9;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stp[i] = st_acc[i];
+    stp[8] = __builtin_amdgcn_s_memtime() - st_start;
+  }
+#endif
   flush_dq();
   // write dK (scaled) and dV for this lane's keys; with RoPE, dK is rotated back (R^T): the
   // lane's d-blocks db and db + NDB/2 hold the partner elements i and i + D/2
@@ -1589,18 +1624,17 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       const int tq_blk = task / NDB, tdb = task % NDB;
       const int qt0 = q0 + 32 * tq_blk;
       if (qt0 >= a.T) continue;  // a query tile past T (ragged last block): no fragment block exists
-      int ks_end = BK / 16;
-      if (a.causal) ks_end = qt0 + 31 + off < k0 ? 0 : min(ks_end, (qt0 + 31 + off - k0) / 16 + 1);
       // dQ^T tile = K^T dS^T: the accumulator has the QUERY on the lane and 16 head-dim values
       // per lane, dumped as one contiguous 2-KiB fragment-order block (two 16-B stores per lane,
-      // coalesced) that attn_dq_reduce_frag_kernel reads back by (query, head-dim) position
+      // coalesced) that attn_dq_reduce_frag_kernel reads back by (query, head-dim) position.
+      // Every key step runs (causal steps past the task's queries read zero dS^T rows: see the
+      // fused-role kernel), so the LDS reads pipeline ahead of the MFMAs
       f32x16 dqa = zero16();
       const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = tdb * 32 + 16 * g1 + 4 * tp;
       const int sa0 = IS::off(8 * hh + tq, qc), sa4 = IS::off(8 * hh + tq + 4, qc);
       const int ka0 = I::off(8 * hh + tq, dc), ka4 = I::off(8 * hh + tq + 4, dc);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        if (ks >= ks_end) break;
         const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
         const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         dqa = mfma32(Bf, A, dqa);

@@ -829,7 +829,22 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
+  static const bool bstamps = std::getenv("PLLM_BWD_STAMPS") != nullptr;
+  Tensor bst;
+  if (bstamps && D <= 64) {  // diagnostic, with a PLLM_BWD_STAMPS=1 build of attention.hip
+    bst = at::zeros({nkb * B * Hkv * 8 * 9}, q.options().dtype(at::kLong));
+    a.stamps = (unsigned long long*)bst.data_ptr();
+  }
   if (B * T * H > 0 && S > 0) pllm::attn_bwd(a, cur_stream());
+  if (bst.defined()) {
+    auto hs = bst.view({-1, 9}).to(at::kCPU).to(at::kDouble);
+    auto tot = hs.sum(0);
+    const double its = tot[6].item<double>();
+    fprintf(stderr, "[bwd stamps] waves %lld iters %.0f | per iter: wait+barrier %.0f stage+barrier %.0f gload %.0f subblocks %.0f barrier %.0f dq %.0f loop-top %.0f | per wave %.0f\n",
+            (long long)hs.size(0), its, tot[0].item<double>() / its, tot[1].item<double>() / its,
+            tot[2].item<double>() / its, tot[3].item<double>() / its, tot[4].item<double>() / its,
+            tot[5].item<double>() / its, tot[7].item<double>() / its, tot[8].item<double>() / hs.size(0));
+  }
 }
 
 }  // namespace

@@ -49,6 +49,7 @@ struct AttnBwdArgs {
   int64_t dq_sb, dq_st, dq_sh, dk_sb, dk_st, dk_sh, dv_sb, dv_st, dv_sh;
   float scale, scale_log2;
   int causal;
+  unsigned long long* stamps;  // diagnostic builds only (PLLM_BWD_STAMPS): per-wave phase cycles
 };
 
 namespace pllm {
