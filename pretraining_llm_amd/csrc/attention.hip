@@ -173,6 +173,10 @@ constexpr float kLazyThr = 8.f;
 #ifndef PLLM_FWD_SCHED
 #define PLLM_FWD_SCHED 1
 #endif
+#ifndef PLLM_FWD_SGB
+#define PLLM_FWD_SGB 1  // read-ahead interleave (sched_group_barrier) in the plain forward loop
+#endif
+constexpr bool kFwdSgb = PLLM_FWD_SGB != 0;
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the plain forward loop
 #endif
@@ -721,6 +725,17 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
             if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
         }
       }
+      if constexpr (MASK == 3 && QB == 2 && kFwdSgb) {
+        // K fragment reads issued ahead of the MFMA pairs that consume them (hipcc's own order
+        // waited lgkmcnt(0) before every pair)
+        __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
+#pragma unroll
+        for (int i = 0; i < 2 * NKS - 2; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 2);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 2);
+      }
       PLLM_STAMP(1);
       bf16x8 pf[QB][4];
 #pragma unroll
@@ -790,6 +805,16 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
           for (int j = 0; j < QB; ++j)
             if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
         }
+      }
+      if constexpr (MASK == 3 && QB == 2 && kFwdSgb) {
+        // V transposed reads two steps (4 reads) ahead of their MFMA pairs
+        __builtin_amdgcn_sched_group_barrier(0x100, 4, 3);
+#pragma unroll
+        for (int i = 0; i < 4 * NDB - 2; ++i) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 3);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 3);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 3);
       }
     };
     if (mask == 3) tile(std::integral_constant<int, 3>{});
