@@ -38,10 +38,23 @@
 //    192 KiB of LDS reads per stage (profiles/r2_wgrad_4wave_negative.jsonl) -- LDS read volume is not
 //    the limiter; the second wave per SIMD covering the per-stage barrier / DMA latency is worth more.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
+#include <cstdio>
+#include <cstdlib>
 #include <type_traits>
 
 #include "common.h"
 #include "kernels.h"
+
+#ifndef PLLM_WGRAD_STAMPS
+#define PLLM_WGRAD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the stage loop
+#endif
+#if PLLM_WGRAD_STAMPS
+__device__ unsigned long long g_wg_stamps[8];
+#endif
+#ifndef PLLM_WGRAD_SPREAD
+#define PLLM_WGRAD_SPREAD 0  // 1: spread the next stage's DMA over the k-steps (measured 0-6 % slower)
+#endif
+constexpr bool kWgradSpread = PLLM_WGRAD_SPREAD != 0;
 
 namespace {
 
@@ -117,15 +130,18 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   }
   const int64_t astep = (int64_t)BKM * lda, bstep = (int64_t)BKM * ldb;
   const unsigned lds_base = (unsigned)(uintptr_t)smem;
-  auto issue = [&](int st) {
+  // pieces [k0, k1) of stage st's DMA plan
+  auto issue_part = [&](int st, int k0, int k1) {
     const int slot = st & 1;
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
+      if (k < k0 || k >= k1) continue;
       const int opnd = (w * PPW + k) / (2 * QUADS);
       const uint16_t* g = src[k] + st * (opnd == 0 ? astep : bstep);
       glds16(g, lds_base + 2u * (unsigned)(slot * STAGE + dst[k]));
     }
   };
+  auto issue = [&](int st) { issue_part(st, 0, PPW); };
 
   // MF = 32: 4x2 v_mfma_f32_32x32x16_bf16 accumulators per wave (128x64 sub-tile);
   // MF = 16: 8x4 v_mfma_f32_16x16x32_bf16 accumulators -- same LDS traffic per FLOP.
@@ -140,12 +156,33 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
+#if PLLM_WGRAD_STAMPS
+  uint64_t st_acc[4] = {0, 0, 0, 0};
+  uint64_t ts_prev = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    st_acc[i] += now - ts_prev;
+    ts_prev = now;
+  };
+#define PLLM_WSTAMP(i) stamp(i)
+#else
+#define PLLM_WSTAMP(i)
+#endif
   if (nstage > 0) issue(0);
   for (int st = 0; st < nstage; ++st) {
     const int slot = st & 1;
+    PLLM_WSTAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PLLM_WSTAMP(0);
     __syncthreads();  // stage st landed for every wave; nobody still reads the other slot
-    if (st + 1 < nstage) issue(st + 1);
+    PLLM_WSTAMP(1);
+    // the next stage's DMA: eight 1-KiB pieces per wave, issued as one burst after the barrier.
+    // Issuing them costs a wave ~1.1k cycles per stage (~140 per piece); spreading them over the
+    // k-steps (kWgradSpread) moves that cost into the compute segment and measured 0-6 % slower
+    // (profiles/r3_wgrad_stamps.md)
+    const bool pre = st + 1 < nstage;
+    if (!kWgradSpread && pre) issue(st + 1);
+    PLLM_WSTAMP(2);
     const uint16_t* Ai = smem + slot * STAGE + wp * HALF;
     const uint16_t* Bi = smem + slot * STAGE + (2 + (wq >> 1)) * HALF;
     const int bcol = (wq & 1) * 64;
@@ -164,6 +201,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           const int col = bcol + 32 * j + 16 * g1 + 4 * tp;
           bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
         }
+        if (kWgradSpread && pre) issue_part(st + 1, k16 * (PPW / (BKM / 16)), (k16 + 1) * (PPW / (BKM / 16)));
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -186,6 +224,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           const int col = 16 * i + 4 * tp;
           af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
         }
+        if (kWgradSpread && pre) issue_part(st + 1, k32 * (PPW / (BKM / 32)), (k32 + 1) * (PPW / (BKM / 32)));
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -193,6 +232,15 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       }
     }
   }
+#if PLLM_WGRAD_STAMPS
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) atomicAdd(&g_wg_stamps[i], (unsigned long long)st_acc[i]);
+    atomicAdd(&g_wg_stamps[4], (unsigned long long)nstage);
+    atomicAdd(&g_wg_stamps[5], 1ull);
+  }
+#endif
+#undef PLLM_WSTAMP
   // accumulator element e of fragment (i, j) -> output (row p, column q) of the tile
   auto prow = [&](int i, int e) {
     return MF == 32 ? p0 + wp * 128 + 32 * i + acc_row(e, hh) : p0 + wp * 128 + 16 * i + 4 * (lane >> 4) + e;
@@ -314,6 +362,18 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
     else PLLM_WGRAD_LAUNCH(32, false);
   }
 #undef PLLM_WGRAD_LAUNCH
+#if PLLM_WGRAD_STAMPS
+  if (std::getenv("PLLM_WGRAD_STAMPS")) {
+    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipStreamSynchronize(st);
+    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wg_stamps), sizeof(h));
+    const double n = (double)h[4] > 0 ? (double)h[4] : 1.0;  // wave-stages (x8 waves per WG counted per wave)
+    fprintf(stderr, "[wgrad stamps] M %d P %d Q %d S %d | per wave-stage: vmcnt wait %.0f barrier %.0f dma issue %.0f compute %.0f\n",
+            M, P, Q, S, h[0] / n, h[1] / n, h[2] / n, h[3] / n);
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wg_stamps), z, sizeof(z));
+  }
+#endif
   if (S == 1) return;
   const int64_t PQ = (int64_t)P * Q;
   const dim3 rg((unsigned)((PQ / 8 + 255) / 256));
