@@ -177,6 +177,10 @@ constexpr float kLazyThr = 8.f;
 #define PLLM_FWD_SGB 1  // read-ahead interleave (sched_group_barrier) in the plain forward loop
 #endif
 constexpr bool kFwdSgb = PLLM_FWD_SGB != 0;
+#ifndef PLLM_FWD_DMA
+#define PLLM_FWD_DMA 1  // plain forward loop: K/V tiles by LDS DMA (buffer_load ... lds)
+#endif
+constexpr bool kFwdDma = PLLM_FWD_DMA != 0;
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the plain forward loop
 #endif
@@ -321,6 +325,33 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
     }
   };
 
+  // LDS DMA of the plain loop (no fused RoPE): each wave moves PPW 1-KiB pieces of the K then V
+  // tile straight into the swizzled image -- lane l of a piece fills LDS chunk 64 p + l, so it
+  // loads the logical chunk that the image stores there (row g / CPR, chunk (g % CPR) ^ f(row)).
+  // No staging registers, no ds_write restage; rows past S read as zeros (descriptor range).
+  constexpr bool DMA = kFwdDma && !ROPE && !PIPE && !V3;
+  constexpr int PCS = BN * CPR / 64;  // pieces per tile
+  constexpr int PPW = 2 * PCS / NW;   // K + V pieces per wave
+  static_assert(2 * PCS % NW == 0 && PCS % PPW == 0, "a wave's pieces lie in one operand");
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const bool dv = (wu * PPW) / PCS != 0;  // this wave moves V pieces (else K)
+  uint32_t doff[PPW];
+#pragma unroll
+  for (int k = 0; k < PPW; ++k) {
+    const int g = ((wu * PPW + k) % PCS) * 64 + lane, row = g / CPR, cc = (g % CPR) ^ I::f(row);
+    doff[k] = (uint32_t)(row * (int)(dv ? a.v_st : a.k_st) + cc * 8) * 2u;
+  }
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  auto gdma = [&](int t, int buf) {
+    const int kv0 = t * BN, rows = min(a.S - kv0, BN);
+    const int64_t st = dv ? a.v_st : a.k_st;
+    const uint16_t* base = (dv ? vp : kp) + (int64_t)kv0 * st;
+    const i32x4v srd = srd_of(base, (uint32_t)(((int64_t)(rows - 1) * st + D) * 2));
+    const unsigned dst = lds0 + 2u * (unsigned)((dv ? 2 * TILE : 0) + buf * TILE);
+#pragma unroll
+    for (int k = 0; k < PPW; ++k) blds16(srd, doff[k], dst + 1024u * (unsigned)((wu * PPW + k) % PCS));
+  };
+
   // per-lane LDS element offsets with the swizzle applied once (see attn_bwd_kernel): K
   // fragment reads fk ^ (ks << 4) + 32 kb D, V transposed reads fv0 / fv8 ^ (db << 5) + 16 kst D
   const int g1 = (lane >> 4) & 1, tq = (lane & 15) >> 2, tp = lane & 3;
@@ -348,8 +379,13 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
   const uint64_t st_start = __builtin_amdgcn_s_memtime();
 #endif
   if (ntiles > 0) {
-    gload(0);
-    swrite(0, 0, 0);
+    if constexpr (DMA) {
+      gdma(0, 0);
+      vm_wait_all();
+    } else {
+      gload(0);
+      swrite(0, 0, 0);
+    }
   }
   __syncthreads();
   if constexpr (PIPE) {
@@ -702,7 +738,10 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
 #define PLLM_STAMP(i)
 #endif
     const int buf = t & 1;
-    if (t + 1 < ntiles) gload(t + 1);
+    if (t + 1 < ntiles) {
+      if constexpr (DMA) gdma(t + 1, buf ^ 1);
+      else gload(t + 1);
+    }
     PLLM_STAMP(0);
     const int kv0 = t * BN;
     // which of this wave's blocks see keys of this tile: a compile-time mask per code
@@ -821,7 +860,8 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
     else if (mask == 1) tile(std::integral_constant<int, 1>{});
     else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
     PLLM_STAMP(3);
-    if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
+    if constexpr (DMA) vm_wait_all();
+    else if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
     PLLM_STAMP(4);
     __syncthreads();
     PLLM_STAMP(5);

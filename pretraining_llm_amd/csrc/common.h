@@ -193,6 +193,27 @@ PLLM_DEV u32x4 buf_ld16(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
   return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0u, 0));
 }
 
+// global -> LDS DMA of 16 B per lane into [m0 + 16 * lane] (m0 = wave-uniform LDS byte address)
+// through a buffer descriptor: a wave-uniform base (4 SGPRs, range-checked: out-of-range lanes
+// read zeros) plus a 32-bit per-lane byte offset.  Measured 7-11 % faster in the wgrad GEMM than
+// global_load_lds with 64-bit per-lane addresses (profiles/r3_wgrad_stamps.md).  Inline asm so
+// hipcc's waitcnt pass does not drain the prefetch before unrelated LDS reads: the caller retires
+// these loads with vm_wait_all() ahead of the barrier that publishes the data.
+typedef int i32x4v __attribute__((ext_vector_type(4)));
+PLLM_DEV i32x4v srd_of(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  i32x4v r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
+  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
+  r[3] = 0x00020000;
+  return r;
+}
+PLLM_DEV void blds16(const i32x4v& srd, uint32_t voff, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(srd),
+               "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+               : "memory", "m0");
+}
 #define PLLM_CHECK_LAUNCH() (void)hipGetLastError()
 
 // Debug builds (python -m pretraining_llm_amd.build --debug): report a violated device-side

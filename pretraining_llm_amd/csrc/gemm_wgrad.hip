@@ -90,24 +90,7 @@ PLLM_DEV void glds16(const void* src, unsigned lds_byte) {
                "s"(__builtin_amdgcn_readfirstlane(lds_byte))
                : "memory", "m0");
 }
-// the same DMA through a buffer descriptor: a 32-bit per-lane byte offset from a wave-uniform
-// base (4 SGPRs) instead of a 64-bit per-lane address (the guide's price list gives buffer...lds
-// pieces ~60 cycles of issue against the ~140 measured here for global_load_lds)
-typedef int i32x4v __attribute__((ext_vector_type(4)));
-PLLM_DEV i32x4v srd_of(const void* base, uint32_t bytes) {
-  const uint64_t a = (uint64_t)(uintptr_t)base;
-  i32x4v r;
-  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
-  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
-  r[2] = __builtin_amdgcn_readfirstlane((int)bytes);
-  r[3] = 0x00020000;
-  return r;
-}
-PLLM_DEV void blds16(const i32x4v& srd, uint32_t voff, unsigned lds_byte) {
-  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(srd),
-               "s"(__builtin_amdgcn_readfirstlane(lds_byte))
-               : "memory", "m0");
-}
+// buffer-descriptor form (srd_of / blds16): common.h
 PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
 
 // [rows][128] bf16 image, 16-B chunk ch of row r at ch ^ f(r) (conflict-free tr reads)
