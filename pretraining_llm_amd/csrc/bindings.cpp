@@ -200,6 +200,76 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   return out_acc ? at::empty({0}, dy.options()) : out;
 }
 
+// ---------------------------------------------------------------- fused-epilogue GEMM
+// a [M, K] (row stride lda), b [N, K] contiguous -> [out [M, N], aux]:
+// epi 0: out = a b^T (+ bias); 1: out = gelu(pre), aux = pre = a b^T + bias; 2: out = relu(a b^T + bias);
+// 3 / 4: out = (a b^T) * gelu'(aux) / * (aux > 0), and when bias_acc is given its column sums are
+// added into it (the producing layer's bias gradient, bf16 or fp32)
+std::vector<Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
+                            const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_acc) {
+  check_bf16(a, "a");
+  check_bf16(b, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_tn: a [M, K], b [N, K]");
+  TORCH_CHECK(a.stride(1) == 1 && b.is_contiguous(), "gemm_tn: K-contiguous operands");
+  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm_tn: epi 0..4");
+  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(K % 64 == 0 && K > 0, "gemm_tn: K must be a positive multiple of 64, got ", K);
+  TORCH_CHECK(N % 8 == 0 && a.stride(0) % 8 == 0, "gemm_tn: N and lda must be multiples of 8");
+  TORCH_CHECK(M < (1 << 30) && N < (1 << 30), "gemm_tn: dims");
+  TORCH_CHECK((int64_t)(std::min<int64_t>(M, 256) - 1) * a.stride(0) * 2 + K * 2 < (1ll << 31) &&
+                  (int64_t)(std::min<int64_t>(N, 256) - 1) * K * 2 + K * 2 < (1ll << 31),
+              "gemm_tn: a 256-row panel must span < 2 GiB");
+  check_aligned16(a, "a");
+  check_aligned16(b, "b");
+  if (bias) {
+    check_bf16(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm_tn: bias [N]");
+    TORCH_CHECK((reinterpret_cast<uintptr_t>(bias->data_ptr()) & 7) == 0, "gemm_tn: bias 8-byte aligned");
+    TORCH_CHECK(epi <= 2, "gemm_tn: bias only in the forward epilogues");
+  }
+  Tensor out = at::empty({M, N}, a.options());
+  Tensor aux_out = at::empty({epi == 1 ? M : 0, N}, a.options());
+  pllm::GemmArgs g{};
+  g.A = (const uint16_t*)a.data_ptr();
+  g.B = (const uint16_t*)b.data_ptr();
+  g.C = (uint16_t*)out.data_ptr();
+  g.bias = bias ? (const uint16_t*)bias->data_ptr() : nullptr;
+  g.lda = a.stride(0);
+  g.ldb = K;
+  g.ldc = N;
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  Tensor part;
+  if (epi == 1) {
+    g.aux = (uint16_t*)aux_out.data_ptr();
+    g.ldaux = N;
+  } else if (epi >= 3) {
+    TORCH_CHECK(aux.has_value(), "gemm_tn: epi 3 / 4 need aux");
+    check_bf16(*aux, "aux");
+    TORCH_CHECK(aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N && aux->stride(1) == 1 &&
+                    aux->stride(0) % 8 == 0, "gemm_tn: aux [M, N]");
+    check_aligned16(*aux, "aux");
+    g.aux = (uint16_t*)aux->data_ptr();
+    g.ldaux = aux->stride(0);
+    part = at::empty({pllm::gemm_colsum_groups((int)M), N}, a.options().dtype(at::kFloat));
+    g.colpart = part.data_ptr<float>();
+  }
+  bool of32 = false;
+  if (bias_acc) {
+    TORCH_CHECK(epi >= 3, "gemm_tn: bias_acc only with epi 3 / 4");
+    of32 = check_grad(*bias_acc, "bias_acc");
+    TORCH_CHECK(bias_acc->numel() == N && bias_acc->is_contiguous(), "gemm_tn: bias_acc [N]");
+  }
+  if (M > 0) {
+    pllm::gemm_tn(g, (int)epi, cur_stream());
+    if (bias_acc)
+      pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M), (int)N, bias_acc->data_ptr(), of32, true,
+                       cur_stream());
+  }
+  return {out, aux_out};
+}
+
 // ---------------------------------------------------------------- skinny GEMM (decode)
 // y[M, N] = act(in[M, K] w[N, K]^T (+ bias)) for M <= 8 token rows; in = x, or (gamma given)
 // norm(x (+ res)) -- then also returns the residual stream s = x + res when res is given
@@ -855,6 +925,8 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
+  m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None) -> Tensor[]");
+  m.def("gemm_set_config(int mfma, int group_m) -> ()", [](int64_t mf, int64_t gm) { pllm::gemm_set_config((int)mf, (int)gm); });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");
@@ -886,6 +958,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("norm_bwd_acc", norm_bwd_acc_op);
   m.impl("bias_grad", bias_grad);
   m.impl("wgrad", wgrad);
+  m.impl("gemm_tn", gemm_tn);
   m.impl("act_fwd", act_fwd);
   m.impl("act_bwd", act_bwd);
   m.impl("act_bwd_bias", act_bwd_bias);

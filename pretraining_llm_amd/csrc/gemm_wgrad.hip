@@ -63,6 +63,10 @@ constexpr bool kWgradLoaders = PLLM_WGRAD_LOADERS != 0;
 #define PLLM_WGRAD_BUFLDS 1  // buffer_load ... lds (SRD + 32-bit offsets) instead of global_load_lds
 #endif
 constexpr bool kWgradBufLds = PLLM_WGRAD_BUFLDS != 0;
+#ifndef PLLM_WGRAD_STAGGER
+#define PLLM_WGRAD_STAGGER 0  // n > 0: waves 4-7 (the SIMD partners of 0-3) issue the next stage's DMA before k-step n
+#endif
+constexpr int kWgradStagger = PLLM_WGRAD_STAGGER;
 
 namespace {
 
@@ -212,7 +216,10 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
     // k-steps (kWgradSpread) moves that cost into the compute segment and measured 0-6 % slower
     // (profiles/r3_wgrad_stamps.md)
     const bool pre = st + 1 < nstage;
-    if (!kWgradSpread && pre) issue(st + 1);
+    // stagger: the SIMD partners (waves w and w + 4) issue their bursts at different times, so one of
+    // them keeps the matrix pipe busy while the other is stuck issuing pieces
+    const bool late = kWgradStagger > 0 && w >= 4;
+    if (!kWgradSpread && pre && !late) issue(st + 1);
     PLLM_WSTAMP(2);
     const uint16_t* Ai = smem + slot * STAGE + wp * HALF;
     const uint16_t* Bi = smem + slot * STAGE + (2 + (wq >> 1)) * HALF;
@@ -233,6 +240,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
         }
         if (kWgradSpread && pre) issue_part(st + 1, k16 * (PPW / (BKM / 16)), (k16 + 1) * (PPW / (BKM / 16)));
+        if (late && pre && k16 == kWgradStagger) issue(st + 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -256,6 +264,7 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
         }
         if (kWgradSpread && pre) issue_part(st + 1, k32 * (PPW / (BKM / 32)), (k32 + 1) * (PPW / (BKM / 32)));
+        if (late && pre && k32 == (kWgradStagger + 1) / 2) issue(st + 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll

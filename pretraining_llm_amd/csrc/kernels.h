@@ -101,6 +101,23 @@ int64_t embedding_bwd_chunks(int64_t N);  // fp32 workspace: 2 * chunks * C floa
 void embedding_bwd(const void* dx, const int32_t* sorted, const int32_t* perm, void* dwte, void* dwpe, bool grad_f32,
                    float* part, int64_t N, int Bn, int T, int C, int64_t V, hipStream_t st);
 
+// gemm.hip: C[M,N] = epi(A[M,K] B[N,K]^T); epi 0 plain (+bias), 1 GELU (aux <- pre-activation),
+// 2 ReLU, 3 GELU backward (aux = pre-activation in), 4 ReLU backward (aux = ReLU output in);
+// 3 / 4 write column sums of C to colpart [gemm_colsum_groups(M)][N] (fp32)
+struct GemmArgs {
+  const uint16_t* A;
+  const uint16_t* B;
+  uint16_t* C;
+  const uint16_t* bias;
+  uint16_t* aux;
+  float* colpart;
+  int64_t lda, ldb, ldc, ldaux;
+  int M, N, K;
+  int group_m;  // set by gemm_tn
+};
+void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
+void gemm_set_config(int mfma, int group_m);
+int gemm_colsum_groups(int M);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad_set_mfma(int mf);

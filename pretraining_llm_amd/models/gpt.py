@@ -157,6 +157,10 @@ class MLP(nn.Module):
 
     def forward(self, x, fuse_out_bias: bool = False):
         """``fuse_out_bias``: the down-projection's bias gradient is emitted by the next norm."""
+        if ops.fused_mlp_ok(x, self.hidden.weight, self.hidden.bias, self.proj.weight, self.kind):
+            # activation in the GEMM epilogues (csrc/gemm.hip)
+            return ops.fused_mlp(x, self.hidden.weight, self.hidden.bias, self.proj.weight, self.proj.bias,
+                                 self.kind, out_bias_ext=fuse_out_bias)
         fuse_act = ops._hip(x) and self.kind in ("gelu", "relu") and self.hidden.bias is not None \
             and torch.is_grad_enabled()
         h = ops.linear(x, self.hidden.weight, self.hidden.bias, bias_grad_external=fuse_act)

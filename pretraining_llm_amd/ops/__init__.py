@@ -231,6 +231,115 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
     return F.linear(x, weight, bias)
 
 
+# ---------------------------------------------------------------------------
+# MLP with the activation in the GEMM epilogues (csrc/gemm.hip)
+# ---------------------------------------------------------------------------
+# PLLM_FUSED_MLP: "bwd" (default) = forward on hipBLASLt + the activation kernel, backward through
+# the fused data-gradient epilogue (act' + b1's gradient: 476-480 vs 512 us per GPT-2 layer, bench/
+# gemm_tn_bench.py); "all" = the forward activation in the GEMM epilogue too (its main loop is
+# still slower than hipBLASLt's: 423-440 vs 408 us with the separate GELU pass); "0" = neither
+_FM = _os.environ.get("PLLM_FUSED_MLP", "bwd")
+FUSED_MLP = _FM in ("1", "all", "bwd")
+FUSED_MLP_FWD = _FM in ("1", "all")
+
+
+def fused_mlp_ok(x, w1, b1, w2, act: str) -> bool:
+    """The fused path: GELU / ReLU MLPs with an up-projection bias on the HIP training path."""
+    if not FUSED_MLP or act not in ("gelu", "relu") or b1 is None or not torch.is_grad_enabled():
+        return False
+    if not (_hip_op("linear", x) and _hip_op("act", x) and w1.requires_grad):
+        return False
+    C, Fh = x.shape[-1], w1.shape[0]
+    return (C % 64 == 0 and Fh % 64 == 0 and x.numel() > 0 and tuple(w1.shape) == (Fh, C)
+            and tuple(w2.shape) == (C, Fh) and w1.is_contiguous() and w2.is_contiguous()
+            and _aligned16(w1) and _aligned16(w2) and b1.is_contiguous())
+
+
+class _FusedMLPFn(torch.autograd.Function):
+    """y = proj(act(hidden(x))) with the activation fused into the GEMM epilogues:
+
+    forward   [pre,] a = act(x W1^T + b1)    one gemm_tn launch (GELU keeps the pre-activation);
+                                             PLLM_FUSED_MLP=bwd: hipBLASLt + the activation kernel
+              y = a W2^T + b2                hipBLASLt
+    backward  dW2 += dy^T a, db2             (b2 skipped when the next norm emits it)
+              da_pre = (dy W2) * act'(.)     one gemm_tn launch through W2's transposed shadow,
+                                             + b1's gradient from the epilogue's column sums
+              dx = da_pre W1, dW1 += da_pre^T x
+    Gradient-ready notifications keep the unfused order (W2, b2, b1, W1) for the DP buckets.
+    Reference: the MLP of /root/reference/src/models/mlp.py:24-26,39-41."""
+
+    @staticmethod
+    def forward(ctx, x, w1, b1, w2, b2, gelu, out_bias_ext):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        if not FUSED_MLP_FWD:
+            pre = F.linear(x2, w1, b1)
+            a = _ops().act_fwd(pre, 1 if gelu else 0)
+            if gelu:
+                ctx.save_for_backward(x2, a, pre)
+            else:
+                ctx.save_for_backward(x2, a)
+        elif gelu:
+            a, pre = _ops().gemm_tn(x2, w1, b1, 1)
+            ctx.save_for_backward(x2, a, pre)
+        else:
+            a, _ = _ops().gemm_tn(x2, w1, b1, 2)
+            ctx.save_for_backward(x2, a)
+        ctx.gelu, ctx.ext = gelu, out_bias_ext
+        ctx.params = (w1, b1, w2, b2)
+        ctx.xshape = x.shape
+        return F.linear(a, w2, b2).view(*x.shape[:-1], C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        if ctx.gelu:
+            x2, a, pre = ctx.saved_tensors
+        else:
+            x2, a = ctx.saved_tensors
+            pre = a
+        w1, b1, w2, b2 = ctx.params
+        ctx.params = None
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        dw1 = db1 = dw2 = db2 = None
+        # down projection: weight and bias gradients
+        tgt = _acc_target(w2)
+        dw2 = _weight_grad(dy2, a, tgt)
+        if tgt is not None:
+            _notify(w2)
+        if b2 is not None and not ctx.ext:
+            tgt = _acc_target(b2)
+            if tgt is not None:
+                _ops().bias_grad(dy2, tgt)
+                _notify(b2)
+            else:
+                db2 = _ops().bias_grad(dy2)
+        # its data gradient fused with the activation backward and b1's gradient
+        w2t = getattr(w2, "_pllm_wT", None)
+        if w2t is None or getattr(w2, "_pllm_wT_ver", None) != w2._version:
+            w2t = w2.t().contiguous()
+        tgt = _acc_target(b1)
+        bacc = tgt if tgt is not None else torch.zeros(b1.shape[0], device=dy2.device, dtype=torch.float32)
+        dpre = _ops().gemm_tn(dy2, w2t, None, 3 if ctx.gelu else 4, pre, bacc)[0]
+        if tgt is not None:
+            _notify(b1)
+        else:
+            db1 = bacc.to(b1.dtype)
+        # up projection
+        dx = _dgrad(dpre, w1) if ctx.needs_input_grad[0] else None
+        tgt = _acc_target(w1)
+        dw1 = _weight_grad(dpre, x2, tgt)
+        if tgt is not None:
+            _notify(w1)
+        if dx is not None:
+            dx = dx.view(ctx.xshape)
+        return dx, dw1, db1, dw2, db2, None, None
+
+
+def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False):
+    ext = bool(out_bias_ext and b2 is not None and not (_TORCH_OPS & {"norm", "act"}))
+    return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext)
+
+
 _ACT_IDS = {None: 0, "gelu": 1, "relu": 2}
 
 

@@ -23,8 +23,8 @@ MiB = 2 ** 20
 def free_hbm_bytes(device: torch.device) -> int:
     """Bytes a new allocation on ``device`` can get: free device memory plus the caching
     allocator's reserved-but-unallocated pool."""
-    if device.type != "cuda":
-        return 1 << 62
+    if device.type != "cuda" or not torch.cuda.is_available():
+        return 1 << 62  # CPU, or fake CUDA tensors traced on a host without a GPU
     idx = device.index if device.index is not None else torch.cuda.current_device()
     free, _total = torch.cuda.mem_get_info(idx)
     slack = torch.cuda.memory_reserved(idx) - torch.cuda.memory_allocated(idx)

@@ -57,10 +57,12 @@ def _op_cases():
         ("attn_decode", (r(B, 1, H, D), k, v, 0.125)),
         ("gemv", (r(4, C), r(768, C), r(768))),
         ("sample", (r(4, V, dt=f32), 0.0, 0)),
+        ("gemm_tn", (r(N, C), r(768, C), r(768), 1)),
+        ("gemm_tn", (r(N, C), r(768, C), None, 3, r(N, 768), torch.zeros(768, device=DEV))),
     ]
 
 
-@pytest.mark.parametrize("i", range(25))
+@pytest.mark.parametrize("i", range(27))
 def test_opcheck_fake_matches_kernel(i):
     torch.manual_seed(i)
     cases = _op_cases()

@@ -1,0 +1,149 @@
+"""Numerics of the fused-epilogue TN GEMM (csrc/gemm.hip) against fp32 PyTorch math.
+
+C = epi(A B^T): plain (+bias), bias+GELU (pre-activation kept), bias+ReLU, and the data
+gradient fused with the GELU / ReLU backward plus the bias-gradient column sums."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _ext():
+    from pretraining_llm_amd.ops import _lib
+    _lib.require()
+    yield
+
+
+def _rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).norm() / (b.norm() + 1e-12)).item()
+
+
+def _gelu(x):
+    return torch.nn.functional.gelu(x, approximate="tanh")
+
+
+def _gelu_df(x):
+    k, c = 0.7978845608028654, 0.044715
+    u = k * (x + c * x ** 3)
+    t = torch.tanh(u)
+    return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * c * x * x)
+
+
+SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192)]
+
+
+@pytest.mark.parametrize("mf", [32, 16])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_tn_forward_epilogues(M, N, K, mf):
+    torch.manual_seed(3)
+    big = torch.randn(M, K + 64, device=DEV).bfloat16()
+    a = big[:, 32:32 + K]  # row-strided A
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = (0.5 * torch.randn(N, device=DEV)).bfloat16()
+    ref = a.float() @ b.float().t()
+    torch.ops.pllm.gemm_set_config(mf, 4)
+    try:
+        out, _ = torch.ops.pllm.gemm_tn(a, b, None, 0)
+        assert out.shape == (M, N)
+        assert _rel(out, ref) < 5e-3, _rel(out, ref)
+        out, _ = torch.ops.pllm.gemm_tn(a, b, bias, 0)
+        pre_ref = ref + bias.float()
+        assert _rel(out, pre_ref) < 5e-3
+        act, pre = torch.ops.pllm.gemm_tn(a, b, bias, 1)
+        assert _rel(pre, pre_ref) < 5e-3
+        # the activation is computed from the bf16-rounded pre-activation, like the unfused path
+        assert _rel(act, _gelu(pre.float())) < 5e-3, _rel(act, _gelu(pre.float()))
+        assert _rel(act, _gelu(pre_ref)) < 1e-2
+        y, _ = torch.ops.pllm.gemm_tn(a, b, bias, 2)
+        assert _rel(y, torch.relu(pre_ref)) < 5e-3
+        assert torch.equal(torch.ops.pllm.gemm_tn(a, b, bias, 1)[0], act)  # deterministic
+    finally:
+        torch.ops.pllm.gemm_set_config(32, 4)
+
+
+@pytest.mark.parametrize("mf", [32, 16])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("f32_bias_grad", [True, False])
+def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad):
+    torch.manual_seed(5)
+    dy = (0.3 * torch.randn(M, K, device=DEV)).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    pre = torch.randn(M, N, device=DEV).bfloat16()
+    da = (dy.float() @ wt.float().t()).bfloat16().float()  # the unfused path's bf16 data gradient
+    torch.ops.pllm.gemm_set_config(mf, 4)
+    try:
+        for epi, aux, ref in ((3, pre, da * _gelu_df(pre.float())),
+                              (4, torch.relu(pre), da * (pre.float() > 0))):
+            acc = torch.randn(N, device=DEV)
+            acc = acc if f32_bias_grad else acc.bfloat16()
+            acc0 = acc.clone()
+            out, _ = torch.ops.pllm.gemm_tn(dy, wt, None, epi, aux, acc)
+            assert _rel(out, ref) < 1e-2, (epi, _rel(out, ref))
+            db_ref = acc0.double() + out.double().sum(0)  # column sums of the bf16 output
+            tol = 1e-5 if f32_bias_grad else 1e-2
+            assert _rel(acc.double(), db_ref) < tol, (epi, _rel(acc.double(), db_ref))
+            out2, _ = torch.ops.pllm.gemm_tn(dy, wt, None, epi, aux)
+            assert torch.equal(out, out2)
+    finally:
+        torch.ops.pllm.gemm_set_config(32, 4)
+
+
+def test_gemm_tn_contract_checks():
+    a = torch.randn(64, 100, device=DEV).bfloat16()
+    b = torch.randn(64, 100, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_tn(a, b, None, 0)  # K % 64
+    a = torch.randn(64, 128, device=DEV).bfloat16()
+    b = torch.randn(60, 128, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_tn(a, b, None, 0)  # N % 8
+    b = torch.randn(64, 128, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_tn(a, b, None, 3)  # epi 3 without aux
+
+
+@pytest.mark.parametrize("kind", ["gelu", "relu"])
+@pytest.mark.parametrize("ext", [False, True])
+@pytest.mark.parametrize("fwd", [False, True])
+def test_fused_mlp_matches_unfused(kind, ext, fwd, monkeypatch):
+    """ops.fused_mlp (activation in the GEMM epilogues; fwd=False: backward only) vs hipBLASLt
+    GEMMs + activation kernels."""
+    from pretraining_llm_amd import ops
+    monkeypatch.setattr(ops, "FUSED_MLP_FWD", fwd)
+    torch.manual_seed(11)
+    C, Fh = 256, 1024
+    x0 = torch.randn(4, 128, C, device=DEV).bfloat16()
+    w1 = (torch.randn(Fh, C, device=DEV) / C ** 0.5).bfloat16()
+    b1 = (0.1 * torch.randn(Fh, device=DEV)).bfloat16()
+    w2 = (torch.randn(C, Fh, device=DEV) / Fh ** 0.5).bfloat16()
+    b2 = (0.1 * torch.randn(C, device=DEV)).bfloat16()
+    dy = torch.randn(4, 128, C, device=DEV).bfloat16()
+
+    def run(fused):
+        ps = [t.clone().requires_grad_() for t in (x0, w1, b1, w2, b2)]
+        x, W1, B1, W2, B2 = ps
+        with torch.enable_grad():
+            if fused:
+                assert ops.fused_mlp_ok(x, W1, B1, W2, kind)
+                y = ops.fused_mlp(x, W1, B1, W2, B2, kind, out_bias_ext=ext)
+            else:
+                h = ops.linear(x, W1, B1)
+                a = ops.gelu(h) if kind == "gelu" else ops.relu(h)
+                y = ops.linear(a, W2, B2)
+            y.backward(dy)
+        return y.detach(), [p.grad for p in ps]
+
+    yf, gf = run(True)
+    yu, gu = run(False)
+    assert _rel(yf, yu) < 1e-2
+    names = ["x", "w1", "b1", "w2", "b2"]
+    for n, a, b in zip(names, gf, gu):
+        if n == "b2" and ext:
+            assert a is None  # left to the next norm's backward
+            continue
+        assert a is not None, n
+        assert _rel(a, b) < 2e-2, (n, _rel(a, b))
