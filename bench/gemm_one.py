@@ -14,12 +14,12 @@ def main():
     ap.add_argument("--M", type=int, default=65536)
     ap.add_argument("--N", type=int, default=768)
     ap.add_argument("--K", type=int, default=3072)
-    ap.add_argument("--mf", type=int, default=32)
+    ap.add_argument("--mf", type=int, default=16)
     ap.add_argument("--reps", type=int, default=5)
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
-    torch.ops.pllm.gemm_set_config(args.mf, 4)
+    torch.ops.pllm.gemm_set_config(args.mf, 4, 0)
     a = torch.randn(args.M, args.K, device="cuda").bfloat16()
     w = (torch.randn(args.N, args.K, device="cuda") / args.K ** 0.5).bfloat16()
     b = torch.randn(args.N, device="cuda").bfloat16()

@@ -34,14 +34,15 @@ def timeit(fn, rounds=5, reps=5):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mf", type=int, default=32)
+    ap.add_argument("--mf", type=int, default=16)
     ap.add_argument("--group", type=int, default=4)
     ap.add_argument("--fused", action="store_true", help="also time the fused MLP epilogues")
+    ap.add_argument("--phased", type=int, default=0)
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
     P = torch.ops.pllm
-    P.gemm_set_config(args.mf, args.group)
+    P.gemm_set_config(args.mf, args.group, args.phased)
     for M, N, K in SHAPES:
         a = torch.randn(M, K, device="cuda").bfloat16()
         w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
@@ -49,7 +50,7 @@ def main():
         fl = 2 * M * N * K
         ours = timeit(lambda: P.gemm_tn(a, w, b, 0))
         lib = timeit(lambda: F.linear(a, w, b))
-        rec = {"M": M, "N": N, "K": K, "mf": args.mf, "group": args.group, "ours_us": round(ours, 1),
+        rec = {"M": M, "N": N, "K": K, "mf": args.mf, "group": args.group, "phased": args.phased, "ours_us": round(ours, 1),
                "ours_tflops": round(fl / ours / 1e6, 1), "blas_us": round(lib, 1),
                "blas_tflops": round(fl / lib / 1e6, 1)}
         if args.fused and N > K:

@@ -71,11 +71,121 @@ PLLM_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 
+// Epilogue of one 256x256 tile: acc (+ bias) -> bf16 -> the wave's [64][64] LDS region (8 KiB, two
+// passes of 64 rows; 8-B granule g of row r at g ^ (r & 15)) -> rows read back as 16 B per lane,
+// whole 128-B rows per 8 lanes -> epilogue op -> global by unconditional buffer ops (out-of-range
+// lanes get an offset past the descriptor), exactly kEpiOps<MF, EPI> vector-memory instructions
+template <int MF, int EPI>
+constexpr int kEpiOps = EPI == 1 ? 32 + (MF == 32 ? 8 : 4) : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
+
+template <int MF, int EPI, typename Acc, int NI, int NJ>
+PLLM_DEV void gemm_epilogue(const Acc (&acc)[NI][NJ], uint16_t* tile, const pllm::GemmArgs& g,
+                            const __amdgpu_buffer_rsrc_t& brs, int tm, int tn, int wm, int wn, int lane) {
+  constexpr int NE = MF == 32 ? 16 : 4;
+  constexpr int NQ = NE / 4;
+  const int M = g.M, N = g.N;
+  const int m0 = tm * GT, n0 = tn * GT, ncol0 = n0 + wn * 64;
+    const int rows_ok = min(GT, M - m0);
+  const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, N);
+  const __amdgpu_buffer_rsrc_t ars = rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)m0 * g.ldaux : g.C, rows_ok,
+                                               g.ldaux, N);
+  const int rsub = lane >> 3, c8 = lane & 7;
+  const int col = ncol0 + 8 * c8;
+  const bool col_ok = col < N;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u32x2 bias[NI][NQ];  // bias of the wave's columns (zeros without one: empty descriptor)
+  if constexpr (EPI <= 2) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int c = MF == 32 ? 32 * i + 8 * q + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
+        bias[i][q] = bld8(brs, (uint32_t)(ncol0 + c) * 2u);
+      }
+  }
+#pragma unroll
+  for (int hf = 0; hf < 2; ++hf) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+#pragma unroll
+      for (int jj = 0; jj < NJ / 2; ++jj) {
+        const int j = hf * (NJ / 2) + jj;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          // 4 consecutive columns [c, c + 4) of local row r
+          const int c = MF == 32 ? 32 * i + 8 * q + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
+          const int r = MF == 32 ? 32 * jj + (lane & 31) : 16 * jj + (lane & 15);
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          if constexpr (EPI <= 2) {
+            v[0] += lo_bf(bias[i][q][0]);
+            v[1] += hi_bf(bias[i][q][0]);
+            v[2] += lo_bf(bias[i][q][1]);
+            v[3] += hi_bf(bias[i][q][1]);
+          }
+          const u32x2 pk = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
+          *reinterpret_cast<u32x2*>(tile + r * 64 + (((c >> 2) ^ (r & 15)) << 2)) = pk;
+        }
+      }
+    }
+    // one wave writes and reads its own region: LDS executes a wave's accesses in order
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+    for (int it = 0; it < 8; ++it) {
+      const int r = 8 * it + rsub;
+      const int s = r & 15;
+      u32x4 v = *reinterpret_cast<const u32x4*>(tile + r * 64 + ((((2 * c8) ^ s) & ~1) << 2));
+      if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
+      const int rt = wm * 128 + hf * 64 + r;  // row within the tile
+      const uint32_t off = col_ok ? (uint32_t)(((int64_t)rt * g.ldc + col) * 2) : kOff;
+      if constexpr (EPI == 0) {
+        bst16(crs, off, v);
+      } else if constexpr (EPI == 1 || EPI == 2) {
+        float f[8];
+        unpack8(v, f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = EPI == 1 ? gelu_f(f[e]) : fmaxf(f[e], 0.f);
+        if constexpr (EPI == 1) bst16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff, v);
+        bst16(crs, off, pack8(f));
+      } else {
+        float f[8], a[8];
+        unpack8(v, f);
+        unpack8(buf_ld16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff), a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = EPI == 3 ? f[e] * gelu_df(a[e]) : (a[e] > 0.f ? f[e] : 0.f);
+        const u32x4 o = pack8(f);
+        bst16(crs, off, o);
+        unpack8(o, f);  // the bias gradient sums the bf16-rounded values, like act_bwd_colsum
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[e] += f[e];
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (EPI >= 3) {
+    // lanes l, l + 8, ..., l + 56 hold the same 8 columns; rows past M contributed zeros
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      csum[e] += __shfl_xor(csum[e], 8, 64);
+      csum[e] += __shfl_xor(csum[e], 16, 64);
+      csum[e] += __shfl_xor(csum[e], 32, 64);
+    }
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.colpart + (int64_t)(2 * tm + wm) * N), (short)0, N * 4, 0x00020000);
+    const uint32_t po = (lane < 8 && col_ok) ? (uint32_t)col * 4u : kOff;
+    bst16(prs, po, __builtin_bit_cast(u32x4, f32x4{csum[0], csum[1], csum[2], csum[3]}));
+    bst16(prs, po == kOff ? kOff : po + 16u, __builtin_bit_cast(u32x4, f32x4{csum[4], csum[5], csum[6], csum[7]}));
+  }
+}
+
 // Persistent: one workgroup per CU walks tiles lid, lid + grid, ...; the DMA pipeline runs across
 // tile boundaries (the last stage of a tile prefetches the next tile's first stage), and the
 // epilogue's output goes through half of the LDS -- the other half already holds that prefetch --
 // so a tile's stores drain under the next tile's first stage instead of stalling every CU at once.
-template <int MF, int EPI>
+template <int MF, int EPI, bool ASYM>
 __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * GSTAGE];
   const int M = g.M, N = g.N, K = g.K;
@@ -90,16 +200,22 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
   // ---- DMA plan: piece k of wave w = 8 rows x 128 B (waves 0-3: A rows, 4-7: B rows).  Lane l
   // fills image row 8 * blk + l / 8 at chunk position l % 8, which holds logical chunk
   // (l % 8) ^ gswz(row).  Rows past M / N fall outside the descriptor's range: they read zeros.
-  const int opnd = w >> 2;
+  // ASYM: waves 0-3 issue all 64 pieces of a stage (16 each: waves 0-1 A, 2-3 B) and waves 4-7
+  // none, so after each barrier the partner wave of every SIMD goes straight to its MFMAs while
+  // the loader wave is stuck issuing pieces (a DMA burst costs ~1.1k cycles per stage, CU-wide)
+  constexpr int PPW = ASYM ? 16 : 8;
+  const int opnd = ASYM ? (w >> 1) & 1 : w >> 2;
+  const bool loader = !ASYM || w < 4;
   const int64_t ld = opnd == 0 ? g.lda : g.ldb;
-  uint32_t voff[8];
+  uint32_t voff[PPW];
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int blk = (w & 3) * 8 + k, row = 8 * blk + (lane >> 3);
+  for (int k = 0; k < PPW; ++k) {
+    const int blk = (ASYM ? (w & 1) * 16 : (w & 3) * 8) + k, row = 8 * blk + (lane >> 3);
     voff[k] = (uint32_t)((row * ld + (((lane & 7) ^ gswz(row)) << 3)) * 2);
   }
   const unsigned lds_base = (unsigned)(uintptr_t)smem;
   auto issue = [&](int t, int st, int slot) {
+    if (!loader) return;
     int tm, tn;
     tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
     const uint16_t* base = opnd == 0 ? g.A + (int64_t)tm * GT * g.lda : g.B + (int64_t)tn * GT * g.ldb;
@@ -107,18 +223,16 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
     const int64_t koff = (int64_t)st * GBK * 2;
     const int64_t span = (int64_t)(rows_ok - 1) * ld * 2 + (int64_t)K * 2 - koff;
     const i32x4v srd = srd_of(reinterpret_cast<const char*>(base) + koff, (uint32_t)span);
-    const unsigned dst = lds_base + 2u * (unsigned)(slot * GSTAGE + opnd * GIMG + (w & 3) * 8 * 512);
+    const int blk0 = ASYM ? (w & 1) * 16 : (w & 3) * 8;
+    const unsigned dst = lds_base + 2u * (unsigned)(slot * GSTAGE + opnd * GIMG + blk0 * 512);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) blds16(srd, voff[k], dst + 1024u * k);
+    for (int k = 0; k < PPW; ++k) blds16(srd, voff[k], dst + 1024u * k);
   };
 
   constexpr int NI = MF == 32 ? 2 : 4;  // column fragments (64 columns)
   constexpr int NJ = MF == 32 ? 4 : 8;  // row fragments (128 rows)
   using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
   constexpr int NE = MF == 32 ? 16 : 4;
-  constexpr int NQ = NE / 4;            // 4-column groups per accumulator
-  // vector-memory instructions one wave issues in an epilogue (all unconditional buffer ops)
-  constexpr int kEpiOps = EPI == 1 ? 32 + NI * NQ : (EPI >= 3 ? 16 + 16 + 2 : 16 + NI * NQ);
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(g.bias != nullptr ? g.bias : g.A), (short)0, (EPI <= 2 && g.bias != nullptr) ? N * 2 : 0, 0x00020000);
 
@@ -128,7 +242,6 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
   for (int t = lid; t < ntiles; t += G) {
     int tm, tn;
     tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
-    const int m0 = tm * GT, n0 = tn * GT, ncol0 = n0 + wn * 64;
     Acc acc[NI][NJ];
 #pragma unroll
     for (int i = 0; i < NI; ++i)
@@ -138,7 +251,7 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
         for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
     for (int st = 0; st < nstage; ++st) {
       // the stage's DMA was issued before the previous tile's epilogue: its stores may stay in flight
-      if (st == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiOps) : "memory");
+      if (st == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kEpiOps<MF, EPI>) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // stage landed for every wave; nobody still reads the other slot
       if (st + 1 < nstage) issue(t, st + 1, slot ^ 1);
@@ -180,117 +293,191 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
     }
     first = false;
 
-    // ---- epilogue through the last stage's slot (the other one holds the next tile's prefetch):
-    // per wave an [64][64] bf16 region, two passes of 64 rows; 8-B granule g of row r at
-    // g ^ (r & 15); rows read back as 16 B per lane, whole 128-B rows per 8 lanes
+    // ---- epilogue through the last stage's slot (the other one holds the next tile's prefetch)
     __syncthreads();  // every wave is done with the last stage's images
-    uint16_t* tile = smem + (slot ^ 1) * GSTAGE + w * (64 * 64);
-    const int rows_ok = min(GT, M - m0);
-    const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, N);
-    const __amdgpu_buffer_rsrc_t ars = rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)m0 * g.ldaux : g.C, rows_ok,
-                                                 g.ldaux, N);
-    const int rsub = lane >> 3, c8 = lane & 7;
-    const int col = ncol0 + 8 * c8;
-    const bool col_ok = col < N;
-    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    u32x2 bias[NI][NQ];  // bias of the wave's columns (zeros without one: empty descriptor)
-    if constexpr (EPI <= 2) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i)
-#pragma unroll
-        for (int q = 0; q < NQ; ++q) {
-          const int c = MF == 32 ? 32 * i + 8 * q + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
-          bias[i][q] = bld8(brs, (uint32_t)(ncol0 + c) * 2u);
-        }
-    }
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-#pragma unroll
-      for (int i = 0; i < NI; ++i) {
-#pragma unroll
-        for (int jj = 0; jj < NJ / 2; ++jj) {
-          const int j = hf * (NJ / 2) + jj;
-#pragma unroll
-          for (int q = 0; q < NQ; ++q) {
-            // 4 consecutive columns [c, c + 4) of local row r
-            const int c = MF == 32 ? 32 * i + 8 * q + 4 * (lane >> 5) : 16 * i + 4 * (lane >> 4);
-            const int r = MF == 32 ? 32 * jj + (lane & 31) : 16 * jj + (lane & 15);
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
-            if constexpr (EPI <= 2) {
-              v[0] += lo_bf(bias[i][q][0]);
-              v[1] += hi_bf(bias[i][q][0]);
-              v[2] += lo_bf(bias[i][q][1]);
-              v[3] += hi_bf(bias[i][q][1]);
-            }
-            const u32x2 pk = {pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-            *reinterpret_cast<u32x2*>(tile + r * 64 + (((c >> 2) ^ (r & 15)) << 2)) = pk;
-          }
-        }
-      }
-      // one wave writes and reads its own region: LDS executes a wave's accesses in order
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-      for (int it = 0; it < 8; ++it) {
-        const int r = 8 * it + rsub;
-        const int s = r & 15;
-        u32x4 v = *reinterpret_cast<const u32x4*>(tile + r * 64 + ((((2 * c8) ^ s) & ~1) << 2));
-        if (s & 1) v = u32x4{v[2], v[3], v[0], v[1]};
-        const int rt = wm * 128 + hf * 64 + r;  // row within the tile
-        const uint32_t off = col_ok ? (uint32_t)(((int64_t)rt * g.ldc + col) * 2) : kOff;
-        if constexpr (EPI == 0) {
-          bst16(crs, off, v);
-        } else if constexpr (EPI == 1 || EPI == 2) {
-          float f[8];
-          unpack8(v, f);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = EPI == 1 ? gelu_f(f[e]) : fmaxf(f[e], 0.f);
-          if constexpr (EPI == 1) bst16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff, v);
-          bst16(crs, off, pack8(f));
-        } else {
-          float f[8], a[8];
-          unpack8(v, f);
-          unpack8(buf_ld16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff), a);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) f[e] = EPI == 3 ? f[e] * gelu_df(a[e]) : (a[e] > 0.f ? f[e] : 0.f);
-          const u32x4 o = pack8(f);
-          bst16(crs, off, o);
-          unpack8(o, f);  // the bias gradient sums the bf16-rounded values, like act_bwd_colsum
-#pragma unroll
-          for (int e = 0; e < 8; ++e) csum[e] += f[e];
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-    }
-    if constexpr (EPI >= 3) {
-      // lanes l, l + 8, ..., l + 56 hold the same 8 columns; rows past M contributed zeros
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        csum[e] += __shfl_xor(csum[e], 8, 64);
-        csum[e] += __shfl_xor(csum[e], 16, 64);
-        csum[e] += __shfl_xor(csum[e], 32, 64);
-      }
-      const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(g.colpart + (int64_t)(2 * tm + wm) * N), (short)0, N * 4, 0x00020000);
-      const uint32_t po = (lane < 8 && col_ok) ? (uint32_t)col * 4u : kOff;
-      bst16(prs, po, __builtin_bit_cast(u32x4, f32x4{csum[0], csum[1], csum[2], csum[3]}));
-      bst16(prs, po == kOff ? kOff : po + 16u, __builtin_bit_cast(u32x4, f32x4{csum[4], csum[5], csum[6], csum[7]}));
-    }
+    gemm_epilogue<MF, EPI>(acc, smem + (slot ^ 1) * GSTAGE + w * (64 * 64), g, brs, tm, tn, wm, wn, lane);
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Phased variant (PH): each 64-deep K-tile is two k32 phases with their own LDS images
+// ([256 rows][32] bf16, 64-B rows, chunk ^ ((row >> 1) ^ (row >> 2)) & 3: conflict-free
+// ds_read_b128 for both MFMA shapes), one raw s_barrier per phase and the LDS-DMA of the same
+// phase of the NEXT K-tile issued right after it, so every piece has two phases (one K-tile of
+// MFMAs) to land and stays in flight across a barrier: the wait before a phase is a counted
+// s_waitcnt vmcnt(N) for the pieces issued one phase earlier (never a drain to 0 in the loop).
+// Per phase and wave: 4 DMA pieces (a 16-KiB A or B quarter is 2 pieces x 8 waves), 12
+// ds_read_b128 and 32 (16x16x32) or 16 (32x32x16) MFMAs.  Persistent with cross-tile prefetch and
+// the same epilogue as gemm_tn_kernel.
+PLLM_DEV int pswz(int row) { return ((row >> 1) ^ (row >> 2)) & 3; }
+constexpr int PIMG = GT * 32;     // one operand's k32 image [256][32] (16 KiB)
+constexpr int PHASE = 2 * PIMG;   // A then B image of one phase (32 KiB); a K-tile = 2 phases
+
+template <int N>
+PLLM_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+// raw s_barrier (no vmcnt(0) drain, unlike __syncthreads) fenced for the compiler: no LDS access
+// moves across it
+PLLM_DEV void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MF, int EPI>
+__global__ __launch_bounds__(GNT) void gemm_tn_ph_kernel(pllm::GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * 2 * PHASE];  // [K-tile buffer][phase][A|B]
+  const int M = g.M, N = g.N, K = g.K;
+  const int tiles_m = (M + GT - 1) / GT, tiles_n = (N + GT - 1) / GT, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
+  const int wm = w >> 2, wn = w & 3;
+  const int nkt = K / GBK;
+  if (lid >= ntiles) return;
+
+  // DMA plan per phase: wave w fills rows [32 w, 32 w + 32) of the A and of the B image, as 2 pieces
+  // each (16 rows x 64 B); lane l -> row 32 w + 16 p + l / 4, chunk position l % 4 = logical chunk
+  // (l % 4) ^ pswz(row)
+  uint32_t voa[2], vob[2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p) {
+    const int row = 32 * w + 16 * p + (lane >> 2);
+    const int ch = (lane & 3) ^ pswz(row);
+    voa[p] = (uint32_t)((row * g.lda + 8 * ch) * 2);
+    vob[p] = (uint32_t)((row * g.ldb + 8 * ch) * 2);
+  }
+  const unsigned lds_base = (unsigned)(uintptr_t)smem;
+  // issue phase h of K-tile kt of tile t into K-tile buffer b
+  auto issue = [&](int t, int kt, int h, int b) {
+    int tm, tn;
+    tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    const int64_t koff = ((int64_t)kt * GBK + h * 32) * 2;
+    const int ra = min(GT, M - tm * GT), rb = min(GT, N - tn * GT);
+    const i32x4v sa = srd_of(reinterpret_cast<const char*>(g.A + (int64_t)tm * GT * g.lda) + koff,
+                             (uint32_t)((int64_t)(ra - 1) * g.lda * 2 + (int64_t)K * 2 - koff));
+    const i32x4v sb = srd_of(reinterpret_cast<const char*>(g.B + (int64_t)tn * GT * g.ldb) + koff,
+                             (uint32_t)((int64_t)(rb - 1) * g.ldb * 2 + (int64_t)K * 2 - koff));
+    const unsigned dst = lds_base + 2u * (unsigned)((b * 2 + h) * PHASE + 32 * w * 32);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) blds16(sa, voa[p], dst + 1024u * p);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) blds16(sb, vob[p], dst + 2u * PIMG + 1024u * p);
+  };
+
+  constexpr int NI = MF == 32 ? 2 : 4;  // column fragments (64 columns)
+  constexpr int NJ = MF == 32 ? 4 : 8;  // row fragments (128 rows)
+  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
+  constexpr int NE = MF == 32 ? 16 : 4;
+  constexpr int EO = kEpiOps<MF, EPI>;
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.bias != nullptr ? g.bias : g.A), (short)0, (EPI <= 2 && g.bias != nullptr) ? N * 2 : 0, 0x00020000);
+
+  // prologue: both phases of the first K-tile
+  issue(lid, 0, 0, 0);
+  issue(lid, 0, 1, 0);
+  int buf = 0;        // K-tile buffer being computed
+  int epi_pend = 0;   // 1: an epilogue's EO ops were issued after the data of the next 2 phases
+  for (int t = lid; t < ntiles; t += G) {
+    int tm, tn;
+    tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    Acc acc[NI][NJ];
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
+    for (int kt = 0; kt < nkt; ++kt) {
+      const bool more = kt + 1 < nkt || t + G < ntiles;  // a next K-tile (this or the next tile)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // retire this phase's pieces: younger = the other phase's 4 pieces (issued after them, if
+        // any were: the very first K-tile issues both phases back to back; a K-tile's phase 1 of
+        // the last tile has none after it) + an epilogue's EO ops in the first K-tile of a tile
+        if (h == 0) {
+          if (epi_pend) vm_wait<4 + EO>();
+          else vm_wait<4>();
+        } else {
+          // younger than phase 1's pieces: this K-tile's phase-0 prefetch (4, if `more`)
+          if (epi_pend) {  // the epilogue came after phase 1's pieces, then phase 0's prefetch
+            if (more) vm_wait<4 + EO>();
+            else vm_wait<EO>();
+          } else if (more) {
+            vm_wait<4>();
+          } else {
+            vm_wait<0>();
+          }
+        }
+        raw_barrier();  // the phase's images landed for every wave; nobody still reads the other
+                        // K-tile buffer's phase-h image
+        if (more) {
+          if (kt + 1 < nkt) issue(t, kt + 1, h, buf ^ 1);
+          else issue(t + G, 0, h, buf ^ 1);
+        }
+        if (h == 1) epi_pend = 0;
+        const uint16_t* Ai = smem + (buf * 2 + h) * PHASE;
+        const uint16_t* Bi = Ai + PIMG;
+        if constexpr (MF == 32) {
+#pragma unroll
+          for (int k16 = 0; k16 < 2; ++k16) {
+            const int ch = 2 * k16 + (lane >> 5);
+            bf16x8 bf[NI], af[NJ];
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+              const int r = wn * 64 + 32 * i + (lane & 31);
+              bf[i] = lds_frag(Bi + r * 32 + ((ch ^ pswz(r)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+              const int r = wm * 128 + 32 * j + (lane & 31);
+              af[j] = lds_frag(Ai + r * 32 + ((ch ^ pswz(r)) << 3));
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+              for (int i = 0; i < NI; ++i)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
+          }
+        } else {
+          const int ch = lane >> 4;
+          bf16x8 bf[NI], af[NJ];
+#pragma unroll
+          for (int i = 0; i < NI; ++i) {
+            const int r = wn * 64 + 16 * i + (lane & 15);
+            bf[i] = lds_frag(Bi + r * 32 + ((ch ^ pswz(r)) << 3));
+          }
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+            const int r = wm * 128 + 16 * j + (lane & 15);
+            af[j] = lds_frag(Ai + r * 32 + ((ch ^ pswz(r)) << 3));
+          }
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
+        }
+      }
+      buf ^= 1;
+    }
+    // ---- epilogue through the last K-tile's buffer (64 KiB; the other holds the next prefetch)
+    raw_barrier();  // every wave is done reading it
+    gemm_epilogue<MF, EPI>(acc, smem + (buf ^ 1) * 2 * PHASE + w * (64 * 64), g, brs, tm, tn, wm, wn, lane);
+    epi_pend = 1;
+  }
+}
 }  // namespace
 
 namespace pllm {
 
-static int g_gemm_mfma = 32;
+static int g_gemm_mfma = 16;
 static int g_gemm_group_m = 4;
-void gemm_set_config(int mfma, int group_m) {
+static int g_gemm_phased = 0;  // 0 single-phase, 1 phased (gemm_tn_ph_kernel), 2 single-phase ASYM DMA
+void gemm_set_config(int mfma, int group_m, int phased) {
   if (mfma == 16 || mfma == 32) g_gemm_mfma = mfma;
   if (group_m > 0) g_gemm_group_m = group_m;
+  if (phased >= 0) g_gemm_phased = phased;
 }
 
 int gemm_colsum_groups(int M) { return 2 * ((M + GT - 1) / GT); }
@@ -311,8 +498,15 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
   const int ntiles = ((a.M + GT - 1) / GT) * ((a.N + GT - 1) / GT);
   if (ntiles == 0) return;
   const int tiles = ntiles < num_cus() ? ntiles : num_cus();  // persistent grid: one workgroup per CU
-#define PLLM_GEMM_CASE(MFV, E) \
-  hipLaunchKernelGGL((gemm_tn_kernel<MFV, E>), dim3(tiles), dim3(GNT), 0, st, a)
+#define PLLM_GEMM_CASE(MFV, E)                                                       \
+  do {                                                                               \
+    if (g_gemm_phased == 1)                                                          \
+      hipLaunchKernelGGL((gemm_tn_ph_kernel<MFV, E>), dim3(tiles), dim3(GNT), 0, st, a); \
+    else if (g_gemm_phased == 2)                                                     \
+      hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, true>), dim3(tiles), dim3(GNT), 0, st, a); \
+    else                                                                             \
+      hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, false>), dim3(tiles), dim3(GNT), 0, st, a); \
+  } while (0)
 #define PLLM_GEMM_EPIS(MFV)          \
   switch (epi) {                     \
     case 0: PLLM_GEMM_CASE(MFV, 0); break; \

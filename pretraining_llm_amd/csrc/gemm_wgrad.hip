@@ -107,13 +107,15 @@ constexpr int NT = 512;             // 8 waves
 constexpr int HALF = BKM * 128;     // elements of one [64][128] image
 constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 2,3 (64 KiB)
 
-template <int MF, bool OF32>
+template <int MF, bool OF32, bool ASYM>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part, void* __restrict__ out,
                                                    int accumulate) {
   constexpr int QUADS = BKM / 4;  // row-quads per image
-  constexpr int PPW = BKM / 8;    // 1-KiB pieces per wave and stage
+  // 1-KiB pieces per wave and stage; ASYM: waves 0-3 issue all 64 (16 each) and waves 4-7 none,
+  // so each SIMD's partner wave computes while the loader wave is stuck issuing its burst
+  constexpr int PPW = ASYM ? BKM / 4 : BKM / 8;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
@@ -154,7 +156,9 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
                         : (uint32_t)((row * ldb + min(q0 + col, Q - 8)) * 2);
   }
   // pieces [k0, k1) of stage st's DMA plan
+  const bool loader = !ASYM || w < 4;
   auto issue_part = [&](int st, int k0, int k1) {
+    if (!loader) return;
     const int slot = st & 1;
     if constexpr (kWgradBufLds) {
       const int64_t m0 = (int64_t)m_begin + (int64_t)st * BKM;
@@ -504,10 +508,16 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 
 namespace pllm {
 
-// MFMA shape of the wgrad main loop (16 or 32); 32x32 measured 0-6% faster on the GPT-2 shapes
-// (profiles/r1_wgrad_mfma_ab.jsonl), so it is the default
-static int g_wgrad_mfma = 32;
-void wgrad_set_mfma(int mf) { g_wgrad_mfma = mf == 16 ? 16 : 32; }
+// Variant selection (wgrad_set_mfma: 16 / 32 = that MFMA shape with every wave loading, 116 / 132 =
+// the asymmetric-DMA kernel, 0 = per shape).  Same-box A/B (profiles/r3_wgrad_asym_ab.md): the
+// asymmetric DMA is +1-8 % over the symmetric kernel; 16x16x32 wins everywhere except the LM-head
+// shapes (P = vocabulary), where 32x32x16 does (+0.5-4 %)
+static int g_wgrad_mfma = 0;
+static int g_wgrad_asym = 1;
+void wgrad_set_mfma(int mf) {
+  g_wgrad_mfma = mf == 0 ? 0 : ((mf % 100) == 16 ? 16 : 32);
+  g_wgrad_asym = mf == 0 || mf >= 100;
+}
 
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   // Split-K slice count from a cost model: rounds of 256 workgroups (one per CU) x stages per
@@ -547,10 +557,15 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
       hipLaunchKernelGGL((wgrad_ld_kernel<MFV, OF>), dim3(ntiles * S), dim3(NTL), 0, st, (const uint16_t*)dy, \
                          lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
     else                                                                                                       \
-      hipLaunchKernelGGL((wgrad_kernel<MFV, OF>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda, \
-                         (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);              \
+      if (g_wgrad_asym)                                                                                        \
+        hipLaunchKernelGGL((wgrad_kernel<MFV, OF, true>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
+                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
+      else                                                                                                     \
+        hipLaunchKernelGGL((wgrad_kernel<MFV, OF, false>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
+                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
   } while (0)
-  if (g_wgrad_mfma == 16) {
+  const int mfma = g_wgrad_mfma != 0 ? g_wgrad_mfma : (P >= 16384 ? 32 : 16);
+  if (mfma == 16) {
     if (out_f32) PLLM_WGRAD_LAUNCH(16, true);
     else PLLM_WGRAD_LAUNCH(16, false);
   } else {

@@ -116,7 +116,7 @@ struct GemmArgs {
   int group_m;  // set by gemm_tn
 };
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
-void gemm_set_config(int mfma, int group_m);
+void gemm_set_config(int mfma, int group_m, int phased);  // phased: 0 single-phase, 1 gemm_tn_ph_kernel, 2 asym DMA
 int gemm_colsum_groups(int M);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);

@@ -33,19 +33,21 @@ def _gelu_df(x):
     return 0.5 * (1 + t) + 0.5 * x * (1 - t * t) * k * (1 + 3 * c * x * x)
 
 
-SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192)]
+SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192), (8448, 2056, 64),
+          (16640, 1032, 320)]
 
 
+@pytest.mark.parametrize("phased", [0, 1, 2])
 @pytest.mark.parametrize("mf", [32, 16])
 @pytest.mark.parametrize("M,N,K", SHAPES)
-def test_gemm_tn_forward_epilogues(M, N, K, mf):
+def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
     torch.manual_seed(3)
     big = torch.randn(M, K + 64, device=DEV).bfloat16()
     a = big[:, 32:32 + K]  # row-strided A
     b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
     bias = (0.5 * torch.randn(N, device=DEV)).bfloat16()
     ref = a.float() @ b.float().t()
-    torch.ops.pllm.gemm_set_config(mf, 4)
+    torch.ops.pllm.gemm_set_config(mf, 4, phased)
     try:
         out, _ = torch.ops.pllm.gemm_tn(a, b, None, 0)
         assert out.shape == (M, N)
@@ -62,19 +64,20 @@ def test_gemm_tn_forward_epilogues(M, N, K, mf):
         assert _rel(y, torch.relu(pre_ref)) < 5e-3
         assert torch.equal(torch.ops.pllm.gemm_tn(a, b, bias, 1)[0], act)  # deterministic
     finally:
-        torch.ops.pllm.gemm_set_config(32, 4)
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
 
 
+@pytest.mark.parametrize("phased", [0, 1, 2])
 @pytest.mark.parametrize("mf", [32, 16])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("f32_bias_grad", [True, False])
-def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad):
+def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad, phased):
     torch.manual_seed(5)
     dy = (0.3 * torch.randn(M, K, device=DEV)).bfloat16()
     wt = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
     pre = torch.randn(M, N, device=DEV).bfloat16()
     da = (dy.float() @ wt.float().t()).bfloat16().float()  # the unfused path's bf16 data gradient
-    torch.ops.pllm.gemm_set_config(mf, 4)
+    torch.ops.pllm.gemm_set_config(mf, 4, phased)
     try:
         for epi, aux, ref in ((3, pre, da * _gelu_df(pre.float())),
                               (4, torch.relu(pre), da * (pre.float() > 0))):
@@ -89,7 +92,7 @@ def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad):
             out2, _ = torch.ops.pllm.gemm_tn(dy, wt, None, epi, aux)
             assert torch.equal(out, out2)
     finally:
-        torch.ops.pllm.gemm_set_config(32, 4)
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
 
 
 def test_gemm_tn_contract_checks():

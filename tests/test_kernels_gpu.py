@@ -577,7 +577,7 @@ def test_wgrad_kernel(M, P, Q):
     assert _rel(acc32.double(), ref3) < 1e-5, _rel(acc32.double(), ref3)
     # the 16x16x32 MFMA variant computes the same product
     try:
-        for variant in (16,):
+        for variant in (16, 32, 116, 132):  # 1xx: the asymmetric-DMA variant
             torch.ops.pllm.wgrad_set_mfma(variant)
             assert _rel(torch.ops.pllm.wgrad(dy, x), ref) < 5e-3, variant
             acc32 = torch.randn(P, Q, device=DEV)
@@ -585,7 +585,7 @@ def test_wgrad_kernel(M, P, Q):
             torch.ops.pllm.wgrad(dy, x, acc32)
             assert _rel(acc32.double(), ref3) < 1e-5, (variant, _rel(acc32.double(), ref3))
     finally:
-        torch.ops.pllm.wgrad_set_mfma(32)
+        torch.ops.pllm.wgrad_set_mfma(0)
     # strided (non-contiguous rows) operands, e.g. a column slice of a packed buffer
     big = torch.randn(M, P + 64, device=DEV).bfloat16()
     v = big[:, 32:32 + P]
