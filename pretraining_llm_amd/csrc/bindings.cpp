@@ -205,7 +205,7 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 // epi 0: out = a b^T (+ bias); 1: out = gelu(pre), aux = pre = a b^T + bias; 2: out = relu(a b^T + bias);
 // 3 / 4: out = (a b^T) * gelu'(aux) / * (aux > 0), and when bias_acc is given its column sums are
 // added into it (the producing layer's bias gradient, bf16 or fp32)
-std::vector<Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
+std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
                             const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_acc) {
   check_bf16(a, "a");
   check_bf16(b, "b");
@@ -267,7 +267,7 @@ std::vector<Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optiona
       pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M), (int)N, bias_acc->data_ptr(), of32, true,
                        cur_stream());
   }
-  return {out, aux_out};
+  return {out, aux_out};  // a (Tensor, Tensor) tuple: functionalization rejects Tensor[] beside an (a!) arg
 }
 
 // ---------------------------------------------------------------- skinny GEMM (decode)
@@ -925,7 +925,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
-  m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None) -> Tensor[]");
+  m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None) -> (Tensor, Tensor)");
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1) -> ()",
         [](int64_t mf, int64_t gm, int64_t ph) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph); });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });

@@ -78,9 +78,12 @@ PLLM_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 template <int MF, int EPI>
 constexpr int kEpiOps = EPI == 1 ? 32 + (MF == 32 ? 8 : 4) : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
 
-template <int MF, int EPI, typename Acc, int NI, int NJ>
-PLLM_DEV void gemm_epilogue(const Acc (&acc)[NI][NJ], uint16_t* tile, const pllm::GemmArgs& g,
+// (acc columns fragments [I0, I0 + NIE) are the wave's 64 columns)
+template <int MF, int EPI, int I0 = 0, typename Acc, int NIA, int NJ>
+PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pllm::GemmArgs& g,
                             const __amdgpu_buffer_rsrc_t& brs, int tm, int tn, int wm, int wn, int lane) {
+  constexpr int NI = MF == 32 ? 2 : 4;
+  static_assert(I0 + NI <= NIA, "column fragments");
   constexpr int NE = MF == 32 ? 16 : 4;
   constexpr int NQ = NE / 4;
   const int M = g.M, N = g.N;
@@ -117,7 +120,7 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NI][NJ], uint16_t* tile, const pllm
           const int r = MF == 32 ? 32 * jj + (lane & 31) : 16 * jj + (lane & 15);
           float v[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * q + e];
+          for (int e = 0; e < 4; ++e) v[e] = acc[I0 + i][j][4 * q + e];
           if constexpr (EPI <= 2) {
             v[0] += lo_bf(bias[i][q][0]);
             v[1] += hi_bf(bias[i][q][0]);
@@ -300,180 +303,17 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
 }
 
 
-// ---------------------------------------------------------------------------------------------
-// Phased variant (PH): each 64-deep K-tile is two k32 phases with their own LDS images
-// ([256 rows][32] bf16, 64-B rows, chunk ^ ((row >> 1) ^ (row >> 2)) & 3: conflict-free
-// ds_read_b128 for both MFMA shapes), one raw s_barrier per phase and the LDS-DMA of the same
-// phase of the NEXT K-tile issued right after it, so every piece has two phases (one K-tile of
-// MFMAs) to land and stays in flight across a barrier: the wait before a phase is a counted
-// s_waitcnt vmcnt(N) for the pieces issued one phase earlier (never a drain to 0 in the loop).
-// Per phase and wave: 4 DMA pieces (a 16-KiB A or B quarter is 2 pieces x 8 waves), 12
-// ds_read_b128 and 32 (16x16x32) or 16 (32x32x16) MFMAs.  Persistent with cross-tile prefetch and
-// the same epilogue as gemm_tn_kernel.
-PLLM_DEV int pswz(int row) { return ((row >> 1) ^ (row >> 2)) & 3; }
-constexpr int PIMG = GT * 32;     // one operand's k32 image [256][32] (16 KiB)
-constexpr int PHASE = 2 * PIMG;   // A then B image of one phase (32 KiB); a K-tile = 2 phases
-
-template <int N>
-PLLM_DEV void vm_wait() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-// raw s_barrier (no vmcnt(0) drain, unlike __syncthreads) fenced for the compiler: no LDS access
-// moves across it
-PLLM_DEV void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int MF, int EPI>
-__global__ __launch_bounds__(GNT) void gemm_tn_ph_kernel(pllm::GemmArgs g) {
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * 2 * PHASE];  // [K-tile buffer][phase][A|B]
-  const int M = g.M, N = g.N, K = g.K;
-  const int tiles_m = (M + GT - 1) / GT, tiles_n = (N + GT - 1) / GT, ntiles = tiles_m * tiles_n;
-  const int G = gridDim.x;
-  const int lid = xcd_remap(blockIdx.x, G);
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const int wm = w >> 2, wn = w & 3;
-  const int nkt = K / GBK;
-  if (lid >= ntiles) return;
-
-  // DMA plan per phase: wave w fills rows [32 w, 32 w + 32) of the A and of the B image, as 2 pieces
-  // each (16 rows x 64 B); lane l -> row 32 w + 16 p + l / 4, chunk position l % 4 = logical chunk
-  // (l % 4) ^ pswz(row)
-  uint32_t voa[2], vob[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    const int row = 32 * w + 16 * p + (lane >> 2);
-    const int ch = (lane & 3) ^ pswz(row);
-    voa[p] = (uint32_t)((row * g.lda + 8 * ch) * 2);
-    vob[p] = (uint32_t)((row * g.ldb + 8 * ch) * 2);
-  }
-  const unsigned lds_base = (unsigned)(uintptr_t)smem;
-  // issue phase h of K-tile kt of tile t into K-tile buffer b
-  auto issue = [&](int t, int kt, int h, int b) {
-    int tm, tn;
-    tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
-    const int64_t koff = ((int64_t)kt * GBK + h * 32) * 2;
-    const int ra = min(GT, M - tm * GT), rb = min(GT, N - tn * GT);
-    const i32x4v sa = srd_of(reinterpret_cast<const char*>(g.A + (int64_t)tm * GT * g.lda) + koff,
-                             (uint32_t)((int64_t)(ra - 1) * g.lda * 2 + (int64_t)K * 2 - koff));
-    const i32x4v sb = srd_of(reinterpret_cast<const char*>(g.B + (int64_t)tn * GT * g.ldb) + koff,
-                             (uint32_t)((int64_t)(rb - 1) * g.ldb * 2 + (int64_t)K * 2 - koff));
-    const unsigned dst = lds_base + 2u * (unsigned)((b * 2 + h) * PHASE + 32 * w * 32);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) blds16(sa, voa[p], dst + 1024u * p);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) blds16(sb, vob[p], dst + 2u * PIMG + 1024u * p);
-  };
-
-  constexpr int NI = MF == 32 ? 2 : 4;  // column fragments (64 columns)
-  constexpr int NJ = MF == 32 ? 4 : 8;  // row fragments (128 rows)
-  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
-  constexpr int NE = MF == 32 ? 16 : 4;
-  constexpr int EO = kEpiOps<MF, EPI>;
-  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(g.bias != nullptr ? g.bias : g.A), (short)0, (EPI <= 2 && g.bias != nullptr) ? N * 2 : 0, 0x00020000);
-
-  // prologue: both phases of the first K-tile
-  issue(lid, 0, 0, 0);
-  issue(lid, 0, 1, 0);
-  int buf = 0;        // K-tile buffer being computed
-  int epi_pend = 0;   // 1: an epilogue's EO ops were issued after the data of the next 2 phases
-  for (int t = lid; t < ntiles; t += G) {
-    int tm, tn;
-    tile_of(t, tiles_m, tiles_n, g.group_m, tm, tn);
-    Acc acc[NI][NJ];
-#pragma unroll
-    for (int i = 0; i < NI; ++i)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j)
-#pragma unroll
-        for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
-    for (int kt = 0; kt < nkt; ++kt) {
-      const bool more = kt + 1 < nkt || t + G < ntiles;  // a next K-tile (this or the next tile)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        // retire this phase's pieces: younger = the other phase's 4 pieces (issued after them, if
-        // any were: the very first K-tile issues both phases back to back; a K-tile's phase 1 of
-        // the last tile has none after it) + an epilogue's EO ops in the first K-tile of a tile
-        if (h == 0) {
-          if (epi_pend) vm_wait<4 + EO>();
-          else vm_wait<4>();
-        } else {
-          // younger than phase 1's pieces: this K-tile's phase-0 prefetch (4, if `more`)
-          if (epi_pend) {  // the epilogue came after phase 1's pieces, then phase 0's prefetch
-            if (more) vm_wait<4 + EO>();
-            else vm_wait<EO>();
-          } else if (more) {
-            vm_wait<4>();
-          } else {
-            vm_wait<0>();
-          }
-        }
-        raw_barrier();  // the phase's images landed for every wave; nobody still reads the other
-                        // K-tile buffer's phase-h image
-        if (more) {
-          if (kt + 1 < nkt) issue(t, kt + 1, h, buf ^ 1);
-          else issue(t + G, 0, h, buf ^ 1);
-        }
-        if (h == 1) epi_pend = 0;
-        const uint16_t* Ai = smem + (buf * 2 + h) * PHASE;
-        const uint16_t* Bi = Ai + PIMG;
-        if constexpr (MF == 32) {
-#pragma unroll
-          for (int k16 = 0; k16 < 2; ++k16) {
-            const int ch = 2 * k16 + (lane >> 5);
-            bf16x8 bf[NI], af[NJ];
-#pragma unroll
-            for (int i = 0; i < NI; ++i) {
-              const int r = wn * 64 + 32 * i + (lane & 31);
-              bf[i] = lds_frag(Bi + r * 32 + ((ch ^ pswz(r)) << 3));
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-              const int r = wm * 128 + 32 * j + (lane & 31);
-              af[j] = lds_frag(Ai + r * 32 + ((ch ^ pswz(r)) << 3));
-            }
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-#pragma unroll
-              for (int i = 0; i < NI; ++i)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
-          }
-        } else {
-          const int ch = lane >> 4;
-          bf16x8 bf[NI], af[NJ];
-#pragma unroll
-          for (int i = 0; i < NI; ++i) {
-            const int r = wn * 64 + 16 * i + (lane & 15);
-            bf[i] = lds_frag(Bi + r * 32 + ((ch ^ pswz(r)) << 3));
-          }
-#pragma unroll
-          for (int j = 0; j < NJ; ++j) {
-            const int r = wm * 128 + 16 * j + (lane & 15);
-            af[j] = lds_frag(Ai + r * 32 + ((ch ^ pswz(r)) << 3));
-          }
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-#pragma unroll
-            for (int i = 0; i < NI; ++i)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[i], af[j], acc[i][j], 0, 0, 0);
-        }
-      }
-      buf ^= 1;
-    }
-    // ---- epilogue through the last K-tile's buffer (64 KiB; the other holds the next prefetch)
-    raw_barrier();  // every wave is done reading it
-    gemm_epilogue<MF, EPI>(acc, smem + (buf ^ 1) * 2 * PHASE + w * (64 * 64), g, brs, tm, tn, wm, wn, lane);
-    epi_pend = 1;
-  }
-}
 }  // namespace
 
 namespace pllm {
 
 static int g_gemm_mfma = 16;
 static int g_gemm_group_m = 4;
-static int g_gemm_phased = 0;  // 0 single-phase, 1 phased (gemm_tn_ph_kernel), 2 single-phase ASYM DMA
+// 0: every wave issues its DMA pieces; 2: the asymmetric DMA (waves 0-3 issue all).  Measured and
+// removed (profiles/r3_gemm_tn.md): 1 = two k32 phases per K-tile with counted vmcnt across raw
+// barriers (3-12 % slower), 3 = one wave per SIMD with 128x128 per wave and the DMA pinned between
+// MFMA groups (hipBLASLt's geometry; 4-18 % slower, its fused epilogues up to 40 % slower)
+static int g_gemm_phased = 0;
 void gemm_set_config(int mfma, int group_m, int phased) {
   if (mfma == 16 || mfma == 32) g_gemm_mfma = mfma;
   if (group_m > 0) g_gemm_group_m = group_m;
@@ -500,9 +340,7 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
   const int tiles = ntiles < num_cus() ? ntiles : num_cus();  // persistent grid: one workgroup per CU
 #define PLLM_GEMM_CASE(MFV, E)                                                       \
   do {                                                                               \
-    if (g_gemm_phased == 1)                                                          \
-      hipLaunchKernelGGL((gemm_tn_ph_kernel<MFV, E>), dim3(tiles), dim3(GNT), 0, st, a); \
-    else if (g_gemm_phased == 2)                                                     \
+    if (g_gemm_phased == 2)                                                          \
       hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, true>), dim3(tiles), dim3(GNT), 0, st, a); \
     else                                                                             \
       hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, false>), dim3(tiles), dim3(GNT), 0, st, a); \

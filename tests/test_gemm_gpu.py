@@ -37,7 +37,7 @@ SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192), 
           (16640, 1032, 320)]
 
 
-@pytest.mark.parametrize("phased", [0, 1, 2])
+@pytest.mark.parametrize("phased", [0, 2])
 @pytest.mark.parametrize("mf", [32, 16])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
@@ -67,7 +67,7 @@ def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
         torch.ops.pllm.gemm_set_config(16, 4, 0)
 
 
-@pytest.mark.parametrize("phased", [0, 1, 2])
+@pytest.mark.parametrize("phased", [0, 2])
 @pytest.mark.parametrize("mf", [32, 16])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("f32_bias_grad", [True, False])
