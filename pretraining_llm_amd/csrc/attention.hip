@@ -1044,7 +1044,38 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // Q / dO tile chunks: as in the forward, chunk i of a thread is row c / CPR2, column chunk
   // (c % CPR2) + (i odd ? CPR2 : 0), c = tid + NT * (i / 2): both RoPE partners in one thread
   constexpr int QPAIR = (BQ * CPR2 + NT - 1) / NT;
-  u32x4 qr[2 * QPAIR], dor[2 * QPAIR];
+  // QDMA (no in-kernel RoPE): the Q / dO tiles go HBM/L2 -> LDS by buffer_load ... lds, issued
+  // right after the sub-block phase (the dQ task reads neither image) and waited at the next
+  // iteration's top: no staging registers, no ds_write pass, one barrier less per iteration.
+  // Pieces of 1 KiB = QRP rows; lane l fills row blk * QRP + l / CPR at chunk position l % CPR,
+  // which holds logical chunk (l % CPR) ^ I::f(row) (the image's swizzle, applied to the source)
+  constexpr bool QDMA = ROPE == 0;
+  constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW;
+  static_assert(2 * QNP % C::NW == 0, "Q/dO pieces per wave");
+  u32x4 qr[QDMA ? 1 : 2 * QPAIR], dor[QDMA ? 1 : 2 * QPAIR];
+  uint32_t qvo[QPPW];
+#pragma unroll
+  for (int k = 0; k < QPPW; ++k) {
+    const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
+    qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
+  }
+  const unsigned lds_q = (unsigned)(uintptr_t)Ql, lds_o = (unsigned)(uintptr_t)Ol;
+  auto qdma = [&](int it) {
+    const int h = hk * G + it / per_head;
+    const int q0 = (qb_start + it % per_head) * BQ;
+    const int rows = a.T - q0;
+    const i32x4v qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
+                             (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
+    const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
+                             (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
+    const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform piece numbers: scalar descriptors
+#pragma unroll
+    for (int k = 0; k < QPPW; ++k) {
+      const int pc = wu * QPPW + k, img = pc / QNP, blk = pc % QNP;
+      blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
+    }
+  };
   float rc = 0.f;
   auto gload = [&](int it) {
     const int h = hk * G + it / per_head;
@@ -1058,7 +1089,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     int tl = tid;
     asm volatile("" : "+v"(tl));
 #pragma unroll
-    for (int i = 0; i < 2 * QPAIR; ++i) {
+    for (int i = 0; i < (QDMA ? 0 : 2 * QPAIR); ++i) {
       const int c = tl + NT * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
       if (c < BQ * CPR2) {
         qr[i] = buf_ld16(qrs, (uint32_t)(row * (int)a.q_st + col * 8) * 2u);
@@ -1120,7 +1151,19 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // VALU arbitration to its older SIMD partner otherwise (MI355X_MICROARCH.md, 'Two waves
   // per SIMD' item 4)
   if (C::NW == 8 && w >= 4) __builtin_amdgcn_s_setprio(1);
-  if (total > 0) gload(0);
+  if constexpr (QDMA) {
+    if (total > 0) {
+      // row constants of iteration 0 (their load retired by this write), then its Q / dO DMA
+      gload(0);
+      if (tid < 2 * BQ) {
+        const bool live = qb_start * BQ + (tid & (BQ - 1)) < a.T;
+        rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
+      }
+      qdma(0);
+    }
+  } else if (total > 0) {
+    gload(0);
+  }
   // (head, query block) of iteration it, advanced incrementally (no integer division per step)
   int h = hk * G, qbi = qb_start;
 #if PLLM_BWD_STAMPS
@@ -1147,10 +1190,14 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     // wait left inside the staging branches made hipcc assume loads still in flight at the
     // join and wait vmcnt(0) again before the next prefetch -- on the fresh dQ stores
     vm_wait_all();
-    __syncthreads();  // previous iteration's readers of Q/dO/dS are done
+    __syncthreads();  // previous iteration's readers of Q/dO/dS are done (QDMA: this one's tiles landed)
     PLLM_BSTAMP(0);
+    if constexpr (QDMA) {
+      flush_dq();
+      if (it + 1 < total) gload(it + 1);  // the next iteration's row constants
+    }
 #pragma unroll
-    for (int i = 0; i < 2 * QPAIR; i += 2) {
+    for (int i = 0; i < (QDMA ? 0 : 2 * QPAIR); i += 2) {
       const int c = tid + NT * (i / 2), row = c / CPR2, col = c % CPR2;
       if (c < BQ * CPR2) {
         if (ROPE == 1 && q0 + row < a.T) {
@@ -1161,14 +1208,16 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         I::st_pair(Ol, row, col, dor[i], dor[i + 1]);
       }
     }
-    if (tid < 2 * BQ) {
-      const bool live = q0 + (tid & (BQ - 1)) < a.T;
-      rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
+    if constexpr (!QDMA) {
+      if (tid < 2 * BQ) {
+        const bool live = q0 + (tid & (BQ - 1)) < a.T;
+        rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
+      }
+      flush_dq();
+      __syncthreads();
+      PLLM_BSTAMP(1);
+      if (it + 1 < total) gload(it + 1);
     }
-    flush_dq();
-    __syncthreads();
-    PLLM_BSTAMP(1);
-    if (it + 1 < total) gload(it + 1);
     PLLM_BSTAMP(2);
 #if PLLM_BWD_STAGGER > 0
     // diagnostic: delay the second half of the workgroup (the SIMD partners of waves 0-3)
@@ -1307,6 +1356,18 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     }
     PLLM_BSTAMP(3);
     __syncthreads();
+    if constexpr (QDMA) {
+      if (it + 1 < total) {
+        // every wave is past its Q / dO / row-constant reads: the next tile's row constants (their
+        // load retired by this write, before the DMA below is in flight), then its Q / dO DMA
+        if (tid < 2 * BQ) {
+          const int qn = (qbi + 1 == nqb ? qb_start : qbi + 1) * BQ;
+          const bool live = qn + (tid & (BQ - 1)) < a.T;
+          rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
+        }
+        qdma(it + 1);
+      }
+    }
     PLLM_BSTAMP(4);
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
