@@ -155,6 +155,18 @@ struct Img {
   }
 };
 
+// The fused-role backward's dS^T image [keys][128 queries] (256-B rows): chunk ch of row r at
+// ch ^ fs(r), fs linear in r's bits 0..2 (4, 9, 2).  Conflict-free both for the dQ task's
+// ds_read_b64_tr_b16 (4 consecutive rows x 4 aligned chunks -> 16 distinct positions) and for the
+// 16-B dS stores, whose 8-lane ds_write_b128 groups are 8 consecutive rows at one chunk (bank =
+// address mod 128 B: fs mod 8 is a permutation over any 8 aligned rows).  Img<128>'s swizzle gave
+// the former 8-B dS stores a 2-way conflict on every store (16 rows per ds_write_b64 group onto
+// 8 slots mod 128 B): ~64 conflict cycles per wave and iteration (profiles/r3_pmc_attn_*_bwd.md).
+struct ImgS {
+  static PLLM_DEV int f(int r) { return ((r & 1) ? 4 : 0) ^ ((r & 2) ? 9 : 0) ^ ((r & 4) ? 2 : 0); }
+  static PLLM_DEV int off(int r, int col) { return r * 128 + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+};
+
 // ============================================================================
 // forward
 // ============================================================================
@@ -962,7 +974,8 @@ template <int D, int ROPE>
 __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_bwd_kernel(AttnBwdArgs a) {
   using C = BwdCfg<D>;
   using I = Img<D>;
-  using IS = Img<C::BQ>;  // dS^T image [keys][BQ]
+  static_assert(C::BQ == 128, "dS^T image");
+  using IS = ImgS;  // dS^T image [keys][BQ]
   constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR, KH = C::KH;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
@@ -1145,7 +1158,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // them (scratch reloads with vmcnt(0) inside the sub-blocks, serialising the Q/dO prefetch).
   const int fq = I::off(r, 8 * hh);
   const int ft0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
-  const int fs0 = IS::off(w * 32 * KH + r, 4 * hh);
+  const int fs0 = IS::off(w * 32 * KH + r, 8 * hh);
 
   // static priority for the second-dispatched half of an 8-wave workgroup: it loses every
   // VALU arbitration to its older SIMD partner otherwise (MI355X_MICROARCH.md, 'Two waves
@@ -1243,8 +1256,8 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       for (int kh = 0; kh < KH; ++kh) {
         if (kh < live) continue;
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<u32x2*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + g) << 3))) = u32x2{0u, 0u};
+        for (int k = 0; k < 4; k += 2)
+          *reinterpret_cast<u32x4*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + k) << 3))) = u32x4{0u, 0u, 0u, 0u};
       }
       // MASKED is a compile-time property of the code path: a uniform run-time test per
       // element made hipcc emit one basic block per exponential (16 scalar branches per
@@ -1328,16 +1341,30 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
             }
           }
         }
-        // dS^T image: the lane's key rows, 4 consecutive queries per 8-byte store -- dwords
-        // 2(g&1), 2(g&1)+1 of the packed fragment sf[g/2] (no second conversion)
+        // dS^T image: the lane's key rows.  The lane holds queries 8g + 4hh + (0..3) (dwords
+        // 2(g&1), 2(g&1)+1 of the packed fragment sf[g/2]); v_permlane32_swap of the group pairs
+        // (g, g+1) across the half-waves gives each lane 8 consecutive queries (8g + 8hh .. +7, g
+        // even): one 16-B store per pair on the ImgS swizzle, conflict-free
 #pragma unroll
-        for (int kh = 0; kh < NL; ++kh)
+        for (int kh = 0; kh < NL; ++kh) {
+          u32x2 v[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const u32x4 w4 = __builtin_bit_cast(u32x4, sf[kh][g >> 1]);
-            const u32x2 v2 = {w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
-            *reinterpret_cast<u32x2*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + g) << 3))) = v2;
+            v[g] = u32x2{w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
           }
+#pragma unroll
+          for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(v[k][d], v[k + 1][d], false, false);
+              v[k][d] = sw[0];
+              v[k + 1][d] = sw[1];
+            }
+            *reinterpret_cast<u32x4*>(Sl + 32 * kh * BQ + (fs ^ ((4 * j + k) << 3))) =
+                u32x4{v[k][0], v[k][1], v[k + 1][0], v[k + 1][1]};
+          }
+        }
         // keep the scheduler from overlapping consecutive sub-blocks (their live ranges
         // together exceed the 256 registers of two waves per SIMD)
         __builtin_amdgcn_sched_barrier(0);
