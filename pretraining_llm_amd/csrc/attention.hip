@@ -1513,7 +1513,8 @@ template <int D, int ROPE>
 __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   using C = RsCfg<D>;
   using I = Img<D>;
-  using IS = Img<C::BQ>;
+  static_assert(C::BQ == 128, "dS^T image");
+  using IS = ImgS;  // dS^T image (16-B stores after a half-wave swap: conflict-free, see ImgS)
   constexpr int NT = C::NT, BK = C::BK, BQ = C::BQ, NQB = C::NQB, CPR = C::CPR;
   constexpr int NKS = D / 16, NDB = D / 32;
   __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
@@ -1618,7 +1619,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
   // stores fs ^ ((4 j + g) << 3)
   const int fq = I::off(r, 8 * hh);
   const int ft0 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft8 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
-  const int fs0 = IS::off(grp * 32 + r, 4 * hh);
+  const int fs0 = IS::off(grp * 32 + r, 8 * hh);
 
   // dQ fragment blocks of an iteration are STORED one iteration late, right after the next
   // iteration's Q/dO staging: vmcnt counts stores too (gfx9 has no separate store counter), so
@@ -1726,8 +1727,8 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
         }
       } else if (!roleA) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g)
-          *reinterpret_cast<u32x2*>(Sl + (fs ^ ((4 * j + g) << 3))) = u32x2{0u, 0u};
+        for (int k = 0; k < 4; k += 2)
+          *reinterpret_cast<u32x4*>(Sl + (fs ^ ((4 * j + k) << 3))) = u32x4{0u, 0u, 0u, 0u};
       }
       __syncthreads();  // P of sub-block j handed over
       if (live) {
@@ -1747,12 +1748,23 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
           }
           f0 = pack_frag(x, 0);
           f1 = pack_frag(x, 1);
-          // dS^T image from the packed fragments (dwords 2(g&1), 2(g&1)+1 of f[g/2])
+          // dS^T image from the packed fragments (dwords 2(g&1), 2(g&1)+1 of f[g/2]): group pairs
+          // swapped across the half-waves, one 16-B store of 8 consecutive queries per pair
+          u32x2 v[4];
 #pragma unroll
           for (int g = 0; g < 4; ++g) {
             const u32x4 w4 = __builtin_bit_cast(u32x4, g < 2 ? f0 : f1);
-            const u32x2 v2 = {w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
-            *reinterpret_cast<u32x2*>(Sl + (fs ^ ((4 * j + g) << 3))) = v2;
+            v[g] = u32x2{w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
+          }
+#pragma unroll
+          for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const auto sw = __builtin_amdgcn_permlane32_swap(v[k][d], v[k + 1][d], false, false);
+              v[k][d] = sw[0];
+              v[k + 1][d] = sw[1];
+            }
+            *reinterpret_cast<u32x4*>(Sl + (fs ^ ((4 * j + k) << 3))) = u32x4{v[k][0], v[k][1], v[k + 1][0], v[k + 1][1]};
           }
         }
         // dV^T += dO^T P (A) / dK^T += Q^T dS (B): A operands by transposed reads
