@@ -38,11 +38,26 @@ def main():
     ap.add_argument("--group", type=int, default=4)
     ap.add_argument("--fused", action="store_true", help="also time the fused MLP epilogues")
     ap.add_argument("--phased", type=int, default=0)
+    ap.add_argument("--swiglu", action="store_true",
+                    help="only the llama SwiGLU backward: gemm_tn epilogue 5 vs hipBLASLt + swiglu_bwd")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
     P = torch.ops.pllm
     P.gemm_set_config(args.mf, args.group, args.phased)
+    if args.swiglu:
+        # llama-1.3B B16 T2048 (C 2048, F 5504) and B8: dA[M, F] = dy[M, C] @ W_down[C, F] -> [dg | du]
+        for M, F_, C in ((32768, 5504, 2048), (16384, 5504, 2048)):
+            dy = torch.randn(M, C, device="cuda").bfloat16()
+            wdt = (torch.randn(F_, C, device="cuda") / C ** 0.5).bfloat16()  # W_down^T shadow [F, C]
+            gu = torch.randn(M, 2 * F_, device="cuda").bfloat16()
+            fused = timeit(lambda: P.gemm_tn(dy, wdt, None, 5, gu))
+            unf = timeit(lambda: P.swiglu_bwd(dy @ wdt.t(), gu))
+            dg = timeit(lambda: dy @ wdt.t())
+            print(json.dumps({"M": M, "F": F_, "C": C, "mf": args.mf, "fused_swiglu_bwd_us": round(fused, 1),
+                              "blas_plus_swiglu_bwd_us": round(unf, 1), "blas_dgrad_us": round(dg, 1)}), flush=True)
+            del dy, wdt, gu
+        return
     for M, N, K in SHAPES:
         a = torch.randn(M, K, device="cuda").bfloat16()
         w = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()

@@ -204,14 +204,15 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 // a [M, K] (row stride lda), b [N, K] contiguous -> [out [M, N], aux]:
 // epi 0: out = a b^T (+ bias); 1: out = gelu(pre), aux = pre = a b^T + bias; 2: out = relu(a b^T + bias);
 // 3 / 4: out = (a b^T) * gelu'(aux) / * (aux > 0), and when bias_acc is given its column sums are
-// added into it (the producing layer's bias gradient, bf16 or fp32)
+// added into it (the producing layer's bias gradient, bf16 or fp32); 5: aux = [gate | up] [M, 2N],
+// out = [dgate | dup] [M, 2N] with d = a b^T the SwiGLU output's gradient (swiglu_bwd fused)
 std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
                             const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_acc) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_tn: a [M, K], b [N, K]");
   TORCH_CHECK(a.stride(1) == 1 && b.is_contiguous(), "gemm_tn: K-contiguous operands");
-  TORCH_CHECK(epi >= 0 && epi <= 4, "gemm_tn: epi 0..4");
+  TORCH_CHECK(epi >= 0 && epi <= 5, "gemm_tn: epi 0..5");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(K % 64 == 0 && K > 0, "gemm_tn: K must be a positive multiple of 64, got ", K);
   TORCH_CHECK(N % 8 == 0 && a.stride(0) % 8 == 0, "gemm_tn: N and lda must be multiples of 8");
@@ -227,7 +228,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     TORCH_CHECK((reinterpret_cast<uintptr_t>(bias->data_ptr()) & 7) == 0, "gemm_tn: bias 8-byte aligned");
     TORCH_CHECK(epi <= 2, "gemm_tn: bias only in the forward epilogues");
   }
-  Tensor out = at::empty({M, N}, a.options());
+  Tensor out = at::empty({M, epi == 5 ? 2 * N : N}, a.options());
   Tensor aux_out = at::empty({epi == 1 ? M : 0, N}, a.options());
   pllm::GemmArgs g{};
   g.A = (const uint16_t*)a.data_ptr();
@@ -236,7 +237,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   g.bias = bias ? (const uint16_t*)bias->data_ptr() : nullptr;
   g.lda = a.stride(0);
   g.ldb = K;
-  g.ldc = N;
+  g.ldc = epi == 5 ? 2 * N : N;
   g.M = (int)M;
   g.N = (int)N;
   g.K = (int)K;
@@ -244,6 +245,14 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   if (epi == 1) {
     g.aux = (uint16_t*)aux_out.data_ptr();
     g.ldaux = N;
+  } else if (epi == 5) {
+    TORCH_CHECK(aux.has_value(), "gemm_tn: epi 5 needs aux = [gate | up]");
+    check_bf16(*aux, "aux");
+    TORCH_CHECK(aux->dim() == 2 && aux->size(0) == M && aux->size(1) == 2 * N && aux->stride(1) == 1 &&
+                    aux->stride(0) % 8 == 0, "gemm_tn: aux [M, 2N]");
+    check_aligned16(*aux, "aux");
+    g.aux = (uint16_t*)aux->data_ptr();
+    g.ldaux = aux->stride(0);
   } else if (epi >= 3) {
     TORCH_CHECK(aux.has_value(), "gemm_tn: epi 3 / 4 need aux");
     check_bf16(*aux, "aux");
@@ -257,7 +266,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   }
   bool of32 = false;
   if (bias_acc) {
-    TORCH_CHECK(epi >= 3, "gemm_tn: bias_acc only with epi 3 / 4");
+    TORCH_CHECK(epi == 3 || epi == 4, "gemm_tn: bias_acc only with epi 3 / 4");
     of32 = check_grad(*bias_acc, "bias_acc");
     TORCH_CHECK(bias_acc->numel() == N && bias_acc->is_contiguous(), "gemm_tn: bias_acc [N]");
   }

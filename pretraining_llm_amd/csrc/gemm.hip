@@ -23,7 +23,9 @@
 //    128x64 tile back as rows and writes / reads global memory in whole 128-B rows;
 //  * epilogues (EPI): 0 plain (+bias), 1 GELU (C = gelu(pre), aux = pre = acc + bias),
 //    2 ReLU (C = relu(acc + bias)), 3 GELU backward (aux = pre in, C = acc * gelu'(pre)),
-//    4 ReLU backward (aux = relu output in, C = acc * (aux > 0)); 3 / 4 also write the column
+//    4 ReLU backward (aux = relu output in, C = acc * (aux > 0)), 5 SwiGLU backward (aux = the
+//    up-projection's [gate | up] output [M, 2N] in, C = [dgate | dup] [M, 2N]: the llama MLP's
+//    down-projection data gradient fused with swiglu_bwd_kernel); 3 / 4 also write the column
 //    sums of C per (tile row, wave row) to an fp32 slab for the bias gradient (fixed order,
 //    deterministic).  Every value that the unfused path rounds to bf16 is rounded here too
 //    (pre before the activation, the data gradient before the activation backward).
@@ -75,8 +77,13 @@ PLLM_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // passes of 64 rows; 8-B granule g of row r at g ^ (r & 15)) -> rows read back as 16 B per lane,
 // whole 128-B rows per 8 lanes -> epilogue op -> global by unconditional buffer ops (out-of-range
 // lanes get an offset past the descriptor), exactly kEpiOps<MF, EPI> vector-memory instructions
+// (EPI 5 issues 64: vmcnt's field holds at most 63, and waiting for one op more is still exact)
 template <int MF, int EPI>
-constexpr int kEpiOps = EPI == 1 ? 32 + (MF == 32 ? 8 : 4) : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
+constexpr int kEpiOps = EPI == 5 ? 63
+                        : EPI == 1 ? 32 + (MF == 32 ? 8 : 4)
+                                   : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
+
+PLLM_DEV float swiglu_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // (acc columns fragments [I0, I0 + NIE) are the wave's 64 columns)
 template <int MF, int EPI, int I0 = 0, typename Acc, int NIA, int NJ>
@@ -89,9 +96,11 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
   const int M = g.M, N = g.N;
   const int m0 = tm * GT, n0 = tn * GT, ncol0 = n0 + wn * 64;
     const int rows_ok = min(GT, M - m0);
-  const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, N);
+  // EPI 5: C and aux rows hold two N-wide halves ([dgate | dup], [gate | up])
+  constexpr int W2 = EPI == 5 ? 2 : 1;
+  const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, W2 * N);
   const __amdgpu_buffer_rsrc_t ars = rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)m0 * g.ldaux : g.C, rows_ok,
-                                               g.ldaux, N);
+                                               g.ldaux, W2 * N);
   const int rsub = lane >> 3, c8 = lane & 7;
   const int col = ncol0 + 8 * c8;
   const bool col_ok = col < N;
@@ -152,6 +161,21 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
         for (int e = 0; e < 8; ++e) f[e] = EPI == 1 ? gelu_f(f[e]) : fmaxf(f[e], 0.f);
         if constexpr (EPI == 1) bst16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff, v);
         bst16(crs, off, pack8(f));
+      } else if constexpr (EPI == 5) {
+        // d = the bf16-rounded data gradient of the SwiGLU output (as swiglu_bwd_kernel reads it)
+        float d[8], gt[8], up[8], dg[8], du[8];
+        unpack8(v, d);
+        const uint32_t ao = col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff;
+        unpack8(buf_ld16(ars, ao), gt);
+        unpack8(buf_ld16(ars, col_ok ? ao + (uint32_t)N * 2u : kOff), up);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float sg = swiglu_sigmoid(gt[e]);
+          du[e] = d[e] * (gt[e] * sg);
+          dg[e] = d[e] * up[e] * sg * (1.f + gt[e] * (1.f - sg));
+        }
+        bst16(crs, off, pack8(dg));
+        bst16(crs, col_ok ? off + (uint32_t)N * 2u : kOff, pack8(du));
       } else {
         float f[8], a[8];
         unpack8(v, f);
@@ -168,7 +192,7 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
-  if constexpr (EPI >= 3) {
+  if constexpr (EPI == 3 || EPI == 4) {
     // lanes l, l + 8, ..., l + 56 hold the same 8 columns; rows past M contributed zeros
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -351,7 +375,8 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
     case 1: PLLM_GEMM_CASE(MFV, 1); break; \
     case 2: PLLM_GEMM_CASE(MFV, 2); break; \
     case 3: PLLM_GEMM_CASE(MFV, 3); break; \
-    default: PLLM_GEMM_CASE(MFV, 4); break; \
+    case 4: PLLM_GEMM_CASE(MFV, 4); break; \
+    default: PLLM_GEMM_CASE(MFV, 5); break; \
   }
   if (g_gemm_mfma == 16) {
     PLLM_GEMM_EPIS(16)

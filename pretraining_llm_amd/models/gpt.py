@@ -161,6 +161,10 @@ class MLP(nn.Module):
             # activation in the GEMM epilogues (csrc/gemm.hip)
             return ops.fused_mlp(x, self.hidden.weight, self.hidden.bias, self.proj.weight, self.proj.bias,
                                  self.kind, out_bias_ext=fuse_out_bias)
+        if self.kind == "swiglu" and ops.fused_swiglu_ok(x, self.hidden.weight, self.hidden.bias,
+                                                          self.proj.weight, self.proj.bias):
+            # SwiGLU backward in the down-projection's data-gradient epilogue (csrc/gemm.hip)
+            return ops.fused_swiglu_mlp(x, self.hidden.weight, self.proj.weight)
         fuse_act = ops._hip(x) and self.kind in ("gelu", "relu") and self.hidden.bias is not None \
             and torch.is_grad_enabled()
         h = ops.linear(x, self.hidden.weight, self.hidden.bias, bias_grad_external=fuse_act)

@@ -340,6 +340,70 @@ def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False):
     return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext)
 
 
+def fused_swiglu_ok(x, w1, b1, w2, b2) -> bool:
+    """The fused SwiGLU (llama) MLP: no biases, on the HIP training path (PLLM_FUSED_MLP != 0)."""
+    if not FUSED_MLP or b1 is not None or b2 is not None or not torch.is_grad_enabled():
+        return False
+    if not (_hip_op("linear", x) and _hip_op("act", x) and w1.requires_grad):
+        return False
+    C, F2 = x.shape[-1], w1.shape[0]
+    return (C % 64 == 0 and F2 % 16 == 0 and x.numel() > 0 and tuple(w1.shape) == (F2, C)
+            and tuple(w2.shape) == (C, F2 // 2) and w1.is_contiguous() and w2.is_contiguous()
+            and _aligned16(w1) and _aligned16(w2))
+
+
+class _FusedSwiGLUMLPFn(torch.autograd.Function):
+    """y = (silu(g) * u) W2^T with [g | u] = x W1^T (the llama MLP), the SwiGLU backward fused into
+    the down-projection's data-gradient GEMM:
+
+    forward   gu = x W1^T (hipBLASLt), a = swiglu(gu) (swiglu_fwd_kernel), y = a W2^T (hipBLASLt)
+    backward  dW2 += dy^T a
+              [dg | du] = swiglu'(gu, dy W2)   one gemm_tn launch (epilogue 5) through W2's
+                                               transposed shadow: no swiglu_bwd pass over the
+                                               [tokens, 2F] activations
+              dx = [dg | du] W1, dW1 += [dg | du]^T x
+    Same roundings as the unfused path (dy W2 rounded to bf16 before the SwiGLU backward).
+    Reference MLP: /root/reference/src/models/mlp.py:24-26 (the llama preset's SwiGLU variant)."""
+
+    @staticmethod
+    def forward(ctx, x, w1, w2):
+        C = x.shape[-1]
+        x2 = x.reshape(-1, C)
+        gu = F.linear(x2, w1)
+        a = _ops().swiglu_fwd(gu)
+        ctx.save_for_backward(x2, gu, a)
+        ctx.params = (w1, w2)
+        ctx.xshape = x.shape
+        return F.linear(a, w2).view(*x.shape[:-1], C)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, gu, a = ctx.saved_tensors
+        w1, w2 = ctx.params
+        ctx.params = None
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        tgt = _acc_target(w2)
+        dw2 = _weight_grad(dy2, a, tgt)
+        if tgt is not None:
+            _notify(w2)
+        w2t = getattr(w2, "_pllm_wT", None)
+        if w2t is None or getattr(w2, "_pllm_wT_ver", None) != w2._version:
+            w2t = w2.t().contiguous()
+        dgu = _ops().gemm_tn(dy2, w2t, None, 5, gu, None)[0]
+        dx = _dgrad(dgu, w1) if ctx.needs_input_grad[0] else None
+        tgt = _acc_target(w1)
+        dw1 = _weight_grad(dgu, x2, tgt)
+        if tgt is not None:
+            _notify(w1)
+        if dx is not None:
+            dx = dx.view(ctx.xshape)
+        return dx, dw1, dw2
+
+
+def fused_swiglu_mlp(x, w1, w2):
+    return _FusedSwiGLUMLPFn.apply(x, w1, w2)
+
+
 _ACT_IDS = {None: 0, "gelu": 1, "relu": 2}
 
 

@@ -57,7 +57,7 @@ def register() -> None:
     @_reg("gemm_tn")
     def _(a, b, bias, epi, aux=None, bias_acc=None):
         M, N = a.shape[0], b.shape[0]
-        return a.new_empty((M, N)), a.new_empty((M if epi == 1 else 0, N))
+        return a.new_empty((M, 2 * N if epi == 5 else N)), a.new_empty((M if epi == 1 else 0, N))
 
     @_reg("act_fwd")
     def _(x, op):

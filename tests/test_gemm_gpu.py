@@ -150,3 +150,65 @@ def test_fused_mlp_matches_unfused(kind, ext, fwd, monkeypatch):
             continue
         assert a is not None, n
         assert _rel(a, b) < 2e-2, (n, _rel(a, b))
+
+
+def _silu(x):
+    return x * torch.sigmoid(x)
+
+
+@pytest.mark.parametrize("mf", [32, 16])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (300, 520, 128), (777, 264, 192), (4160, 1376, 256)])
+def test_gemm_tn_swiglu_backward_epilogue(M, N, K, mf):
+    """epi 5: [dgate | dup] = swiglu'([gate | up], dy W2) in the data-gradient GEMM's epilogue
+    vs fp32 math on the bf16-rounded data gradient (what swiglu_bwd_kernel reads)."""
+    torch.manual_seed(7)
+    dy = (0.3 * torch.randn(M, K, device=DEV)).bfloat16()
+    wt = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    gu = torch.randn(M, 2 * N, device=DEV).bfloat16()
+    d = (dy.float() @ wt.float().t()).bfloat16().float()
+    g, u = gu.float()[:, :N], gu.float()[:, N:]
+    sg = torch.sigmoid(g)
+    ref = torch.cat([d * u * sg * (1 + g * (1 - sg)), d * _silu(g)], dim=1)
+    torch.ops.pllm.gemm_set_config(mf, 4, 0)
+    try:
+        out, aux = torch.ops.pllm.gemm_tn(dy, wt, None, 5, gu)
+        assert out.shape == (M, 2 * N) and aux.numel() == 0
+        assert _rel(out[:, :N], ref[:, :N]) < 1e-2, _rel(out[:, :N], ref[:, :N])
+        assert _rel(out[:, N:], ref[:, N:]) < 1e-2, _rel(out[:, N:], ref[:, N:])
+        # bit-identical to the unfused kernel pair it replaces (same bf16 roundings)
+        unfused = torch.ops.pllm.swiglu_bwd(torch.ops.pllm.gemm_tn(dy, wt, None, 0)[0], gu)
+        assert (out.float() - unfused.float()).abs().max().item() <= 2 ** -6 * unfused.float().abs().max().item()
+        assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 5, gu)[0], out)  # deterministic
+    finally:
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
+
+
+def test_fused_swiglu_mlp_matches_unfused():
+    """ops.fused_swiglu_mlp (SwiGLU backward in the down-projection's data-gradient epilogue) vs
+    hipBLASLt GEMMs + the swiglu kernels."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(13)
+    C, Fh = 256, 704
+    x0 = torch.randn(4, 128, C, device=DEV).bfloat16()
+    w1 = (torch.randn(2 * Fh, C, device=DEV) / C ** 0.5).bfloat16()
+    w2 = (torch.randn(C, Fh, device=DEV) / Fh ** 0.5).bfloat16()
+    dy = torch.randn(4, 128, C, device=DEV).bfloat16()
+
+    def run(fused):
+        ps = [t.clone().requires_grad_() for t in (x0, w1, w2)]
+        x, W1, W2 = ps
+        with torch.enable_grad():
+            if fused:
+                assert ops.fused_swiglu_ok(x, W1, None, W2, None)
+                y = ops.fused_swiglu_mlp(x, W1, W2)
+            else:
+                y = ops.linear(ops.swiglu(ops.linear(x, W1)), W2)
+            y.backward(dy)
+        return y.detach(), [p.grad for p in ps]
+
+    yf, gf = run(True)
+    yu, gu = run(False)
+    assert torch.equal(yf, yu)
+    for n, a, b in zip(["x", "w1", "w2"], gf, gu):
+        assert a is not None, n
+        assert _rel(a, b) < 1e-2, (n, _rel(a, b))
