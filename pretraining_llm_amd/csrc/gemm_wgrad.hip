@@ -38,6 +38,7 @@
 //    192 KiB of LDS reads per stage (profiles/r2_wgrad_4wave_negative.jsonl) -- LDS read volume is not
 //    the limiter; the second wave per SIMD covering the per-stage barrier / DMA latency is worth more.
 // Requires M % 64 == 0 and P, Q multiples of 8 (checked by the host binding).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -63,6 +64,9 @@ constexpr bool kWgradLoaders = PLLM_WGRAD_LOADERS != 0;
 #define PLLM_WGRAD_BUFLDS 1  // buffer_load ... lds (SRD + 32-bit offsets) instead of global_load_lds
 #endif
 constexpr bool kWgradBufLds = PLLM_WGRAD_BUFLDS != 0;
+#ifndef PLLM_WGRAD_XCD_ALIGN
+#define PLLM_WGRAD_XCD_ALIGN 0  // 1: wgrad_plan prefers slice counts giving every XCD whole slices (measured slower in the step)
+#endif
 #ifndef PLLM_WGRAD_STAGGER
 #define PLLM_WGRAD_STAGGER 0  // n > 0: waves 4-7 (the SIMD partners of 0-3) issue the next stage's DMA before k-step n
 #endif
@@ -519,6 +523,10 @@ void wgrad_set_mfma(int mf) {
   g_wgrad_asym = mf == 0 || mf >= 100;
 }
 
+// A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices
+static int g_wgrad_force_s = 0;
+void wgrad_force_slices(int s) { g_wgrad_force_s = s > 0 ? s : 0; }
+
 void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   // Split-K slice count from a cost model: rounds of 256 workgroups (one per CU) x stages per
   // slice x ~2.0 us per 256x256x64 stage, plus -- for S > 1 -- the fp32 slab traffic (S slabs
@@ -541,6 +549,27 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
       best = s;
     }
   }
+  // XCD alignment: xcd_remap deals each XCD a contiguous 1/8 of the work items, and a slice's items
+  // share its dY / X panels through that XCD's L2.  With a one-round grid and S % 8 == 0 every XCD
+  // holds whole slices; otherwise slices straddle XCDs and their panels are fetched twice.  Measured
+  // (bench/wgrad_slices.py, profiles/r3s3_wgrad_slices.jsonl): GPT-2 QKV (27 tiles) S = 8 226 us vs
+  // the model's S = 9 260 us in isolation -- but the whole GPT-2 step ran 0.2 ms SLOWER with it
+  // (57.82-57.86 vs 58.02-58.08 ms, same box A/B/A/B), so it is off (PLLM_WGRAD_XCD_ALIGN=1 to build it).
+  {
+    int al = 0;
+    double al_t = 1e30;
+    for (int s = 8; s <= 64 && kst / s >= 8; s += 8) {
+      if (ntiles * s > 256) break;
+      const int st_per = (kst + s - 1) / s;
+      const double t = (double)st_per * 2.0e-6 + (double)P * Q * 4.0 * (2 * s + 1) / 4.0e12;
+      if (t < al_t) {
+        al_t = t;
+        al = s;
+      }
+    }
+    if (PLLM_WGRAD_XCD_ALIGN && al > 0 && al_t <= best_t * 1.15) best = al;
+  }
+  if (g_wgrad_force_s > 0) best = std::min(g_wgrad_force_s, std::max(1, kst));
   int st_per = (kst + best - 1) / best;
   *slice = st_per * BKM;
   *S = (kst + st_per - 1) / st_per;

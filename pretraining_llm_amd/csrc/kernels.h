@@ -121,6 +121,7 @@ int gemm_colsum_groups(int M);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad_set_mfma(int mf);
+void wgrad_force_slices(int s);
 void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool out_f32, bool accumulate, hipStream_t st);
 
