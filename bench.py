@@ -60,7 +60,10 @@ def parse(argv=None):
     ap.add_argument("--grad-clip", type=float, default=1.0)
     ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
     ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
-    ap.add_argument("--cuda-graph", action="store_true", help="replay the whole step as one captured hipGraph")
+    ap.add_argument("--cuda-graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
+                    help="replay the whole step as one captured hipGraph (the Trainer's TORCH_COMPILE default); "
+                         "auto: on for one GPU on the HIP path (+0.5 %%, profiles/r3s3_graph_ab.txt), off with "
+                         "N > 1 ranks (RCCL collectives are not captured in the bench) and for ZeRO")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: functional rehearsal on gloo (fp32, tiny shapes); never a measurement")
     ap.add_argument("--verbose", action="store_true")
@@ -169,6 +172,9 @@ def main(argv=None):
         opt.zero_grad()
         return loss
 
+    if args.cuda_graph == "auto":
+        args.cuda_graph = "1" if (world == 1 and not cpu and args.backend == "auto" and not args.zero) else "0"
+    args.cuda_graph = args.cuda_graph == "1"
     if args.cuda_graph:
         from pretraining_llm_amd.train.graph import GraphedTrainStep
         engine.timer.enabled = False  # no event records inside a captured graph
