@@ -168,8 +168,12 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
 }
 
 // ---------------------------------------------------------------- weight-gradient GEMM
-// out[P, Q] (+)= dy[M, P]^T @ x[M, Q]; accumulates into out_acc if given, else returns a new tensor
-Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out_acc) {
+// out[P, Q] (+)= dy[M, P]^T @ x[M, Q]; accumulates into out_acc if given, else returns a new tensor.
+// bias_acc (requires out_acc): the bias gradient column sums of dy are added into it too -- inside the
+// GEMM when its kernel can (wgrad_kernel's all-ones MFMAs), else by the bias_grad kernels
+Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc);
+Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out_acc,
+             const std::optional<Tensor>& bias_acc) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy [M,P], x [M,Q]");
@@ -192,11 +196,24 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   int S = 1, slice = 1;
   pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
   Tensor part = at::empty({S > 1 ? S : 0, P, Q}, dy.options().dtype(at::kFloat));
+  bool bf32 = false;
+  Tensor bpart;
+  if (bias_acc) {
+    TORCH_CHECK(out_acc.has_value(), "wgrad: bias_acc needs out_acc");
+    bf32 = check_grad(*bias_acc, "bias_acc");
+    TORCH_CHECK(bias_acc->numel() == P && bias_acc->is_contiguous(), "wgrad: bias_acc [P]");
+    check_aligned16(*bias_acc, "bias_acc");
+    bpart = at::empty({S, P}, dy.options().dtype(at::kFloat));
+  }
+  bool fused_b = false;
   if (M > 0)
-    pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
-                S > 1 ? part.data_ptr<float>() : nullptr, out.data_ptr(), of32, out_acc.has_value(), cur_stream());
+    fused_b = pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
+                          S > 1 ? part.data_ptr<float>() : nullptr, out.data_ptr(), of32, out_acc.has_value(),
+                          cur_stream(), bias_acc ? bpart.data_ptr<float>() : nullptr,
+                          bias_acc ? bias_acc->data_ptr() : nullptr, bf32);
   else if (!out_acc)
     out.zero_();
+  if (bias_acc && M > 0 && !fused_b) bias_grad(dy.is_contiguous() ? dy : dy.contiguous(), bias_acc);
   return out_acc ? at::empty({0}, dy.options()) : out;
 }
 
@@ -933,7 +950,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms) -> (Tensor, Tensor, Tensor)");
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
-  m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None) -> (Tensor, Tensor)");
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1) -> ()",
         [](int64_t mf, int64_t gm, int64_t ph) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph); });

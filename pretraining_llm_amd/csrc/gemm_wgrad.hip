@@ -115,7 +115,7 @@ template <int MF, bool OF32, bool ASYM>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part, void* __restrict__ out,
-                                                   int accumulate) {
+                                                   int accumulate, float* __restrict__ bpart) {
   constexpr int QUADS = BKM / 4;  // row-quads per image
   // 1-KiB pieces per wave and stage; ASYM: waves 0-3 issue all 64 (16 each) and waves 4-7 none,
   // so each SIMD's partner wave computes while the loader wave is stuck issuing its burst
@@ -199,6 +199,14 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
 #pragma unroll
       for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
 
+  // Fused bias gradient (bpart != null, MF = 16): the column sums of dY over the slice's tokens,
+  // db[p] = sum_m dY[m, p], as MFMAs against an all-ones B fragment -- out[p][q'] = sum_m dY[m, p] for
+  // every q' -- run by the workgroups of the first Q tile only, each wave taking 2 of the 8 A
+  // fragments of its 128-row half (+2 MFMAs per 32; exact fp32 sums of the bf16 inputs, fixed
+  // order).  Replaces a separate column-sum pass over dY (the QKV projection's bias gradient).
+  const bool do_b = MF == 16 && bpart != nullptr && (t % tiles_q) == 0;
+  f32x4 bacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
 #if PLLM_WGRAD_STAMPS
   uint64_t st_acc[4] = {0, 0, 0, 0};
   uint64_t ts_prev = __builtin_amdgcn_s_memtime();
@@ -277,6 +285,13 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
         for (int i = 0; i < 8; ++i)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
+        if constexpr (MF == 16) {
+          if (do_b) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+              if ((i >> 1) == wq) bacc[i & 1] = mfma16(af[i], ones, bacc[i & 1]);
+          }
+        }
       }
     }
   }
@@ -294,6 +309,17 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
     return MF == 32 ? p0 + wp * 128 + 32 * i + acc_row(e, hh) : p0 + wp * 128 + 16 * i + 4 * (lane >> 4) + e;
   };
   auto qcol = [&](int j) { return MF == 32 ? q0 + wq * 64 + 32 * j + r : q0 + wq * 64 + 16 * j + (lane & 15); };
+  if (do_b && (lane & 15) == 0) {
+    // column 0 of the all-ones product: rows p0 + wp 128 + 16 i + 4 (lane / 16) + e, i = 2 wq + k;
+    // slice s's partial row of the fp32 [S][P] slab (summed in slice order by wgrad_reduce_kernel)
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int p = p0 + wp * 128 + 16 * (2 * wq + k) + 4 * (lane >> 4) + e;
+        if (p < P) bpart[(int64_t)s * P + p] = bacc[k][e];
+      }
+  }
   if (S == 1) {
     // single slice: add the tile straight into the gradient
 #pragma unroll
@@ -575,11 +601,21 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
   *S = (kst + st_per - 1) / st_per;
 }
 
-void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool out_f32, bool accumulate, hipStream_t st) {
+int wgrad_bias_slices(int M, int P, int Q) {
+  int S, slice;
+  wgrad_plan(M, P, Q, &S, &slice);
+  return S;
+}
+
+bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
+           bool out_f32, bool accumulate, hipStream_t st, float* bpart, void* bout, bool bout_f32) {
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
+  const int mfma = g_wgrad_mfma != 0 ? g_wgrad_mfma : (P >= 16384 ? 32 : 16);
+  // the bias gradient rides along only on the 16x16x32 kernel (see wgrad_kernel)
+  const bool fuse_b = bpart != nullptr && bout != nullptr && mfma == 16 && !kWgradLoaders;
+  float* const bp = fuse_b ? bpart : nullptr;
 #define PLLM_WGRAD_LAUNCH(MFV, OF)                                                                              \
   do {                                                                                                         \
     if (kWgradLoaders)                                                                                         \
@@ -588,12 +624,11 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
     else                                                                                                       \
       if (g_wgrad_asym)                                                                                        \
         hipLaunchKernelGGL((wgrad_kernel<MFV, OF, true>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
-                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
+                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp);     \
       else                                                                                                     \
         hipLaunchKernelGGL((wgrad_kernel<MFV, OF, false>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
-                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
+                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp);     \
   } while (0)
-  const int mfma = g_wgrad_mfma != 0 ? g_wgrad_mfma : (P >= 16384 ? 32 : 16);
   if (mfma == 16) {
     if (out_f32) PLLM_WGRAD_LAUNCH(16, true);
     else PLLM_WGRAD_LAUNCH(16, false);
@@ -614,11 +649,17 @@ void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wg_stamps), z, sizeof(z));
   }
 #endif
-  if (S == 1) return;
+  if (fuse_b) {  // bias gradient: the [S][P] partial rows summed in slice order into bout
+    const dim3 bg((unsigned)((P / 8 + 255) / 256));
+    if (bout_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);
+    else hipLaunchKernelGGL(wgrad_reduce_kernel<false>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);
+  }
+  if (S == 1) return fuse_b;
   const int64_t PQ = (int64_t)P * Q;
   const dim3 rg((unsigned)((PQ / 8 + 255) / 256));
   if (out_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rg, dim3(256), 0, st, part, S, PQ, out, (int)accumulate);
   else hipLaunchKernelGGL(wgrad_reduce_kernel<false>, rg, dim3(256), 0, st, part, S, PQ, out, (int)accumulate);
+  return fuse_b;
 }
 
 }  // namespace pllm

@@ -122,8 +122,12 @@ int gemm_colsum_groups(int M);
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);
 void wgrad_set_mfma(int mf);
 void wgrad_force_slices(int s);
-void wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
-           bool out_f32, bool accumulate, hipStream_t st);
+// bpart / bout (optional): also the bias gradient db[P] (+)= column sums of dY, through an fp32 [S][P]
+// workspace (S = wgrad_bias_slices); returns whether it was computed (16x16x32 kernel only)
+int wgrad_bias_slices(int M, int P, int Q);
+bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
+           bool out_f32, bool accumulate, hipStream_t st, float* bpart = nullptr, void* bout = nullptr,
+           bool bout_f32 = false);
 
 // transpose.hip: desc int64 [n][6] = (src, dst, rows, cols, first tile, tiles per row band)
 int transpose_tiles(int R, int C);

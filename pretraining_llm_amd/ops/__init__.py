@@ -113,9 +113,16 @@ class _LinearFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = _dgrad(dy, weight)
         dy2 = dy.reshape(-1, dy.shape[-1])
+        # the bias gradient rides along the weight-gradient GEMM when both go into flat targets
+        btgt = None
+        if (ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext and ctx.needs_input_grad[1]
+                and not WGRAD_STREAM and FUSED_WGRAD_BIAS):
+            btgt = _acc_target(ctx.b)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             tgt = _acc_target(ctx.w)
+            if tgt is None:
+                btgt = None
             if WGRAD_STREAM and tgt is not None and dy2.is_cuda:
                 main, side = torch.cuda.current_stream(), _side_stream(dy2.device)
                 side.wait_stream(main)
@@ -125,10 +132,12 @@ class _LinearFn(torch.autograd.Function):
                 x2.record_stream(side)
                 dw = None
             else:
-                dw = _weight_grad(dy2, x2, tgt)
+                dw = _weight_grad(dy2, x2, tgt, btgt)
             if tgt is not None:
                 _notify(ctx.w)
-        if ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext:
+        if btgt is not None:
+            _notify(ctx.b)
+        elif ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext:
             tgt = _acc_target(ctx.b)
             if tgt is not None:
                 _ops().bias_grad(dy2.contiguous(), tgt)
@@ -160,6 +169,10 @@ WGRAD_BLAS_SHAPES = {(16384, 6144, 2048), (16384, 2048, 5504), (16384, 50304, 20
 # MI355X: +1.5 % on one box, -0.8 % on another, and sporadic 2.5-3x slower runs on back-to-back
 # processes (never seen with it off), so it stays off by default.
 WGRAD_STREAM = _os.environ.get("PLLM_WGRAD_STREAM", "0") == "1"
+# A linear layer's bias gradient computed inside its weight-gradient GEMM (csrc/gemm_wgrad.hip: MFMAs
+# against an all-ones operand by the first Q-tile's workgroups) instead of a separate column-sum pass
+# over dy (the GPT-2 QKV projection); PLLM_WGRAD_BIAS=0 for the separate pass
+FUSED_WGRAD_BIAS = _os.environ.get("PLLM_WGRAD_BIAS", "1") == "1"
 _SIDE_STREAMS = {}
 
 
@@ -191,8 +204,10 @@ def _dgrad(dy, weight):
     return dy @ weight
 
 
-def _weight_grad(dy2, x2, tgt):
-    """dW = dy2^T @ x2, added into ``tgt`` (bf16 or fp32) when given (returns None) else returned."""
+def _weight_grad(dy2, x2, tgt, btgt=None):
+    """dW = dy2^T @ x2, added into ``tgt`` (bf16 or fp32) when given (returns None) else returned.
+    ``btgt`` (with ``tgt``): the bias gradient (column sums of dy2) is added into it as well -- on the
+    hand-written kernel inside the GEMM (its all-ones MFMAs), else by the bias_grad kernels."""
     hip_ok = dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.shape[0] % 64 == 0
     f32_tgt = tgt is not None and tgt.dtype == torch.float32 and dy2.dtype != torch.float32
     # an fp32 gradient target always takes the hand-written kernel (fp32 read-add-write epilogue)
@@ -201,9 +216,11 @@ def _weight_grad(dy2, x2, tgt):
     if use_hip:
         dy2, x2 = dy2.contiguous(), x2.contiguous()
         if tgt is not None:
-            _ops().wgrad(dy2, x2, tgt.view(dy2.shape[1], x2.shape[1]))
+            _ops().wgrad(dy2, x2, tgt.view(dy2.shape[1], x2.shape[1]), btgt)
             return None
         return _ops().wgrad(dy2, x2)
+    if btgt is not None:
+        _ops().bias_grad(dy2.contiguous(), btgt)
     if tgt is not None:
         if f32_tgt:
             tgt.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32) if dy2.is_cuda

@@ -49,7 +49,7 @@ def register() -> None:
         return dy.new_empty((dy.shape[-1],))
 
     @_reg("wgrad")
-    def _(dy, x, out_acc=None):
+    def _(dy, x, out_acc=None, bias_acc=None):
         if out_acc is not None:
             return dy.new_empty((0,))
         return dy.new_empty((dy.shape[1], x.shape[1]))

@@ -595,6 +595,39 @@ def test_wgrad_kernel(M, P, Q):
         torch.ops.pllm.wgrad(dy[:M - 8], x[:M - 8])  # token count must be a multiple of 64
 
 
+@pytest.mark.parametrize("M,P,Q", [(2048, 200, 136), (4096, 768, 768), (2048, 512, 2304), (1024, 4096, 4096),
+                                   (8192, 2304, 768)])
+@pytest.mark.parametrize("bias_f32", [True, False])
+def test_wgrad_fused_bias_grad(M, P, Q, bias_f32):
+    """wgrad(..., bias_acc): the bias gradient (column sums of dy) added inside the weight-gradient GEMM
+    (all-ones MFMAs; split-K partial rows summed in slice order) or, on the 32x32x16 kernel, by the
+    bias_grad kernels -- against fp64 sums; the weight gradient itself is unchanged."""
+    torch.manual_seed(17)
+    dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
+    x = torch.randn(M, Q, device=DEV).bfloat16()
+    w0 = torch.randn(P, Q, device=DEV)
+    try:
+        for variant in (0, 16, 116, 132):
+            torch.ops.pllm.wgrad_set_mfma(variant)
+            b0 = torch.randn(P, device=DEV)
+            b0 = b0 if bias_f32 else b0.bfloat16()
+            acc, bacc = w0.clone(), b0.clone()
+            torch.ops.pllm.wgrad(dy, x, acc, bacc)
+            ref_b = b0.double() + dy.double().sum(0)
+            tol = 1e-6 if bias_f32 else 1e-2
+            assert _rel(bacc.double(), ref_b) < tol, (variant, _rel(bacc.double(), ref_b))
+            acc2 = w0.clone()
+            torch.ops.pllm.wgrad(dy, x, acc2)
+            assert torch.equal(acc, acc2), variant  # the GEMM result does not change
+            bacc2 = b0.clone()
+            torch.ops.pllm.wgrad(dy, x, w0.clone(), bacc2)
+            assert torch.equal(bacc, bacc2), variant  # deterministic
+    finally:
+        torch.ops.pllm.wgrad_set_mfma(0)
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.wgrad(dy, x, None, torch.zeros(P, device=DEV))  # bias_acc needs out_acc
+
+
 def test_graphed_train_step_matches_eager():
     """A hipGraph-captured step (fwd, bwd, clip, AdamW, zero_grad) reproduces eager steps."""
     from pretraining_llm_amd.models import GPT, get_preset
