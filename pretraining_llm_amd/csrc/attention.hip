@@ -1952,7 +1952,7 @@ static void attn_bwd_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
   const int nkb = (a.S + BwdCfg<D>::BK - 1) / BwdCfg<D>::BK;
-  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  if (!a.delta_ready) hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   // key blocks in passes of at most a.nkb_pass (bounded slab workspace)
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {
@@ -1988,7 +1988,7 @@ static void attn_bwd_rs_t(AttnBwdArgs a, hipStream_t st) {
   const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
   const int nkb = (a.S + C::BK - 1) / C::BK;
   const int red_grid = a.B * a.H * a.nqt;  // one workgroup per 32-query tile
-  hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  if (!a.delta_ready) hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {
     a.kb0 = kb0;

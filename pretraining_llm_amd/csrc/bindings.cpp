@@ -224,12 +224,12 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 // added into it (the producing layer's bias gradient, bf16 or fp32); 5: aux = [gate | up] [M, 2N],
 // out = [dgate | dup] [M, 2N] with d = a b^T the SwiGLU output's gradient (swiglu_bwd fused)
 std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias, int64_t epi,
-                            const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_acc) {
+                            const std::optional<Tensor>& aux, const std::optional<Tensor>& bias_acc, int64_t T) {
   check_bf16(a, "a");
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_tn: a [M, K], b [N, K]");
   TORCH_CHECK(a.stride(1) == 1 && b.is_contiguous(), "gemm_tn: K-contiguous operands");
-  TORCH_CHECK(epi >= 0 && epi <= 5, "gemm_tn: epi 0..5");
+  TORCH_CHECK(epi >= 0 && epi <= 6, "gemm_tn: epi 0..6");
   const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
   TORCH_CHECK(K % 64 == 0 && K > 0, "gemm_tn: K must be a positive multiple of 64, got ", K);
   TORCH_CHECK(N % 8 == 0 && a.stride(0) % 8 == 0, "gemm_tn: N and lda must be multiples of 8");
@@ -246,7 +246,8 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     TORCH_CHECK(epi <= 2, "gemm_tn: bias only in the forward epilogues");
   }
   Tensor out = at::empty({M, epi == 5 ? 2 * N : N}, a.options());
-  Tensor aux_out = at::empty({epi == 1 ? M : 0, N}, a.options());
+  Tensor aux_out = epi == 6 ? at::empty({T > 0 ? M / T : 0, N / 64, T}, a.options().dtype(at::kFloat))
+                            : at::empty({epi == 1 ? M : 0, N}, a.options());
   pllm::GemmArgs g{};
   g.A = (const uint16_t*)a.data_ptr();
   g.B = (const uint16_t*)b.data_ptr();
@@ -262,6 +263,17 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   if (epi == 1) {
     g.aux = (uint16_t*)aux_out.data_ptr();
     g.ldaux = N;
+  } else if (epi == 6) {
+    TORCH_CHECK(aux.has_value(), "gemm_tn: epi 6 needs aux = the attention output [M, N]");
+    check_bf16(*aux, "aux");
+    TORCH_CHECK(aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N && aux->stride(1) == 1 &&
+                    aux->stride(0) % 8 == 0, "gemm_tn: aux [M, N]");
+    TORCH_CHECK(T > 0 && M % T == 0 && N % 64 == 0, "gemm_tn: epi 6 needs T | M and 64 | N (head dim 64)");
+    check_aligned16(*aux, "aux");
+    g.aux = (uint16_t*)aux->data_ptr();
+    g.ldaux = aux->stride(0);
+    g.delta = aux_out.data_ptr<float>();
+    g.T = (int)T;
   } else if (epi == 5) {
     TORCH_CHECK(aux.has_value(), "gemm_tn: epi 5 needs aux = [gate | up]");
     check_bf16(*aux, "aux");
@@ -864,7 +876,7 @@ int64_t attn_bwd_ws_bytes() {
 // dq/dk/dv are written into caller-provided views (e.g. slices of a packed dQKV buffer)
 void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor& v, const Tensor& o, const Tensor& lse,
               Tensor& dq, Tensor& dk, Tensor& dv, bool causal, double scale, const std::optional<Tensor>& rope_cos,
-              const std::optional<Tensor>& rope_sin, bool rope_in) {
+              const std::optional<Tensor>& rope_sin, bool rope_in, const std::optional<Tensor>& delta_in) {
   const int64_t D = q.size(3);
   TORCH_CHECK(pllm::attn_supported_head_dim((int)D), "attention: head dim must be 32, 64 or 128");
   for (auto& pr : std::vector<std::pair<const Tensor*, const char*>>{
@@ -876,7 +888,11 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   TORCH_CHECK(lse.scalar_type() == at::kFloat && lse.is_contiguous() && lse.numel() == B * H * T, "lse shape");
   check_rope(rope_cos, rope_sin, S, D);
   auto f32 = q.options().dtype(at::kFloat);
-  Tensor delta = at::empty({B, H, T}, f32);
+  // delta_in: rowsum(dO * O) already computed (the output projection's gemm_tn epilogue 6)
+  if (delta_in)
+    TORCH_CHECK(delta_in->scalar_type() == at::kFloat && delta_in->is_contiguous() && delta_in->numel() == B * H * T,
+                "attn_bwd: delta [B, H, T] fp32");
+  Tensor delta = delta_in ? *delta_in : at::empty({B, H, T}, f32);
   // per-key-block bf16 dQ partial slabs (attention.hip: plain stores + ordered fp32 reduce, no
   // atomics), run in passes of at most `per` key blocks: the workspace is bounded by
   // PLLM_ATTN_BWD_WS_MB (default 4096 MiB: one pass for every shipped config -- passes split the
@@ -925,6 +941,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.scale = (float)scale;
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
+  a.delta_ready = delta_in ? 1 : 0;
   static const bool bstamps = std::getenv("PLLM_BWD_STAMPS") != nullptr;
   Tensor bst;
   if (bstamps && D <= 64) {  // diagnostic, with a PLLM_BWD_STAMPS=1 build of attention.hip
@@ -951,7 +968,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
-  m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None) -> (Tensor, Tensor)");
+  m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1) -> ()",
         [](int64_t mf, int64_t gm, int64_t ph) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph); });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
@@ -977,7 +994,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("sample(Tensor logits, float temperature, int seed) -> Tensor");
   m.def("attn_fwd(Tensor q, Tensor k, Tensor v, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None) -> Tensor[]");
   m.def("attn_decode(Tensor q, Tensor k, Tensor v, float scale, Tensor? seqlen=None) -> Tensor");
-  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, bool rope_in=True) -> ()");
+  m.def("attn_bwd(Tensor dout, Tensor q, Tensor k, Tensor v, Tensor o, Tensor lse, Tensor(a!) dq, Tensor(b!) dk, Tensor(c!) dv, bool causal, float scale, Tensor? rope_cos=None, Tensor? rope_sin=None, bool rope_in=True, Tensor? delta=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(pllm, CUDA, m) {

@@ -25,7 +25,10 @@
 //    2 ReLU (C = relu(acc + bias)), 3 GELU backward (aux = pre in, C = acc * gelu'(pre)),
 //    4 ReLU backward (aux = relu output in, C = acc * (aux > 0)), 5 SwiGLU backward (aux = the
 //    up-projection's [gate | up] output [M, 2N] in, C = [dgate | dup] [M, 2N]: the llama MLP's
-//    down-projection data gradient fused with swiglu_bwd_kernel); 3 / 4 also write the column
+//    down-projection data gradient fused with swiglu_bwd_kernel), 6 attention-output projection data
+//    gradient (aux = the attention output O [M, N] in, C = dO = acc, plus delta[b, h, t] = sum over
+//    the 64 columns of head h of dO * O: the attention backward's row constants, so its
+//    attn_bwd_pre_kernel pass over dO and O disappears; head dim 64); 3 / 4 also write the column
 //    sums of C per (tile row, wave row) to an fp32 slab for the bias gradient (fixed order,
 //    deterministic).  Every value that the unfused path rounds to bf16 is rounded here too
 //    (pre before the activation, the data gradient before the activation backward).
@@ -80,6 +83,7 @@ PLLM_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
 // (EPI 5 issues 64: vmcnt's field holds at most 63, and waiting for one op more is still exact)
 template <int MF, int EPI>
 constexpr int kEpiOps = EPI == 5 ? 63
+                        : EPI == 6 ? 48
                         : EPI == 1 ? 32 + (MF == 32 ? 8 : 4)
                                    : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
 
@@ -101,6 +105,10 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
   const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, W2 * N);
   const __amdgpu_buffer_rsrc_t ars = rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)m0 * g.ldaux : g.C, rows_ok,
                                                g.ldaux, W2 * N);
+  // EPI 6: delta [M / T, N / 64, T] fp32 (whole buffer; offsets past it drop the store)
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.delta != nullptr ? g.delta : (float*)g.C), (short)0, EPI == 6 ? (int)(4ll * M * N / 64) : 0,
+      0x00020000);
   const int rsub = lane >> 3, c8 = lane & 7;
   const int col = ncol0 + 8 * c8;
   const bool col_ok = col < N;
@@ -161,6 +169,24 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
         for (int e = 0; e < 8; ++e) f[e] = EPI == 1 ? gelu_f(f[e]) : fmaxf(f[e], 0.f);
         if constexpr (EPI == 1) bst16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff, v);
         bst16(crs, off, pack8(f));
+      } else if constexpr (EPI == 6) {
+        // dO stored as is; its bf16 values times O summed over the wave's 64 columns = one head
+        bst16(crs, off, v);
+        float d[8], o[8];
+        unpack8(v, d);
+        unpack8(buf_ld16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff), o);
+        float sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) sum = __builtin_fmaf(d[e], o[e], sum);
+        // the row's 8 lanes (c8 = 0..7, consecutive lanes) in a fixed butterfly order
+        sum += __shfl_xor(sum, 1, 64);
+        sum += __shfl_xor(sum, 2, 64);
+        sum += __shfl_xor(sum, 4, 64);
+        const int m = m0 + rt;
+        const int bq = m / g.T, tq = m - bq * g.T, hd = ncol0 >> 6;
+        const uint32_t doff = (c8 == 0 && m < M && col_ok)
+                                  ? (uint32_t)((((int64_t)bq * (N >> 6) + hd) * g.T + tq) * 4) : kOff;
+        __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), drs, doff, 0, 0);
       } else if constexpr (EPI == 5) {
         // d = the bf16-rounded data gradient of the SwiGLU output (as swiglu_bwd_kernel reads it)
         float d[8], gt[8], up[8], dg[8], du[8];
@@ -376,7 +402,8 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
     case 2: PLLM_GEMM_CASE(MFV, 2); break; \
     case 3: PLLM_GEMM_CASE(MFV, 3); break; \
     case 4: PLLM_GEMM_CASE(MFV, 4); break; \
-    default: PLLM_GEMM_CASE(MFV, 5); break; \
+    case 5: PLLM_GEMM_CASE(MFV, 5); break; \
+    default: PLLM_GEMM_CASE(MFV, 6); break; \
   }
   if (g_gemm_mfma == 16) {
     PLLM_GEMM_EPIS(16)

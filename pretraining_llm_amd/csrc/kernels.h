@@ -50,6 +50,7 @@ struct AttnBwdArgs {
   float scale, scale_log2;
   int causal;
   unsigned long long* stamps;  // diagnostic builds only (PLLM_BWD_STAMPS): per-wave phase cycles
+  int delta_ready;             // 1: delta already holds rowsum(dO * O) (gemm_tn epilogue 6): no pre-pass
 };
 
 namespace pllm {
@@ -114,6 +115,8 @@ struct GemmArgs {
   int64_t lda, ldb, ldc, ldaux;
   int M, N, K;
   int group_m;  // set by gemm_tn
+  float* delta;  // epilogue 6: [M / T, N / 64, T] row sums of C * aux per 64-column head
+  int T;         // epilogue 6: rows per sequence
 };
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 void gemm_set_config(int mfma, int group_m, int phased);  // phased: 0 single-phase, 1 gemm_tn_ph_kernel, 2 asym DMA

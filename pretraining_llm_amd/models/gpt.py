@@ -73,6 +73,11 @@ class Attention(nn.Module):
     def forward(self, x, rope=None, fuse_out_bias: bool = False):
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         cos, sin = rope if rope is not None else (None, None)
+        if self.proj is not None and ops.attn_proj_ok(qkv, self.n_head, self.n_kv_head, self.proj.weight,
+                                                      self.proj.bias):
+            # the projection's data gradient also emits the attention backward's row constants
+            return ops.attention_proj(qkv, self.n_head, self.n_kv_head, self.proj.weight, self.proj.bias,
+                                      rope_cos=cos, rope_sin=sin, bias_grad_external=fuse_out_bias)
         y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is not None:
             y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)

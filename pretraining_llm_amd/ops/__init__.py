@@ -636,6 +636,100 @@ class _FlashAttnPacked(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None
 
 
+class _AttnProjFn(torch.autograd.Function):
+    """``attention_packed`` followed by the output projection y = O W_o^T (+ b_o).  The backward runs
+    the projection's data gradient through the fused-epilogue GEMM (csrc/gemm.hip epilogue 6), which
+    also emits the attention backward's row constants delta = rowsum(dO * O) per (batch, head,
+    query) while dO is in registers, so the attn_bwd_pre_kernel pass over dO and O is gone.  Head
+    dim 64 (a wave's 64 output columns are one head).  Same math as _FlashAttnPacked + _LinearFn."""
+
+    @staticmethod
+    def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin, w, b, bias_ext):
+        B, T, W = qkv.shape
+        D = W // (H + 2 * Hkv)
+        q, k, v = _split_qkv(qkv, H, Hkv, D)
+        qk = None
+        if cos is not None and _ROPE_PREPASS:
+            qk = _ops().rope_qk(qkv, cos, sin, H + 2 * Hkv, H + Hkv, T)
+            q = qk[..., : H * D].view(B, T, H, D)
+            k = qk[..., H * D:].view(B, T, Hkv, D)
+            o, lse = _ops().attn_fwd(q, k, v, causal, scale)
+        else:
+            o, lse = _ops().attn_fwd(q, k, v, causal, scale, cos, sin)
+        ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
+        ctx.cfg = (H, Hkv, D, causal, scale)
+        ctx.w, ctx.b, ctx.bias_ext = w, b, bias_ext
+        return F.linear(o.view(B, T, H * D), w, b)
+
+    @staticmethod
+    def backward(ctx, dy):
+        qkv, qk, o, lse, cos, sin = ctx.saved_tensors
+        H, Hkv, D, causal, scale = ctx.cfg
+        w, b = ctx.w, ctx.b
+        ctx.w = ctx.b = None
+        B, T, _ = qkv.shape
+        dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
+        o2 = o.view(B * T, H * D)
+        # projection weight / bias gradients (as _LinearFn.backward)
+        dw = db = None
+        need_b = b is not None and ctx.needs_input_grad[8] and not ctx.bias_ext
+        if ctx.needs_input_grad[7]:
+            tgt = _acc_target(w)
+            btgt = _acc_target(b) if (need_b and tgt is not None and FUSED_WGRAD_BIAS) else None
+            dw = _weight_grad(dy2, o2, tgt, btgt)
+            if tgt is not None:
+                _notify(w)
+            if btgt is not None:
+                _notify(b)
+                need_b = False
+        if need_b:
+            bt = _acc_target(b)
+            if bt is not None:
+                _ops().bias_grad(dy2, bt)
+                _notify(b)
+            else:
+                db = _ops().bias_grad(dy2)
+        # dO and delta from one GEMM through W_o's transposed shadow
+        wt = getattr(w, "_pllm_wT", None)
+        if wt is None or getattr(w, "_pllm_wT_ver", None) != w._version:
+            wt = w.t().contiguous()
+        do2, delta = _ops().gemm_tn(dy2, wt, None, 6, o2, None, T)
+        q, k, v = _split_qkv(qkv, H, Hkv, D)
+        if qk is not None:
+            q = qk[..., : H * D].view(B, T, H, D)
+            k = qk[..., H * D:].view(B, T, Hkv, D)
+        dqkv = torch.empty_like(qkv)
+        dq, dk, dv = _split_qkv(dqkv, H, Hkv, D)
+        _attn_ws(qkv.device)
+        _ops().attn_bwd(do2.view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin, qk is None,
+                        delta)
+        return dqkv, None, None, None, None, None, None, dw, db, None
+
+
+# PLLM_ATTN_PROJ_FUSED=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
+FUSED_ATTN_PROJ = os.environ.get("PLLM_ATTN_PROJ_FUSED", "1") == "1"
+
+
+def attn_proj_ok(qkv, n_head: int, n_kv_head: int, w, b) -> bool:
+    """The fused attention + output projection path (_AttnProjFn): HIP training path, head dim 64."""
+    if not FUSED_ATTN_PROJ or not torch.is_grad_enabled() or not (_hip_op("attn", qkv) and _hip_op("linear", qkv)):
+        return False
+    B, T, W = qkv.shape
+    D = W // (n_head + 2 * n_kv_head)
+    C_out = w.shape[0]
+    return (D == 64 and B * T > 0 and tuple(w.shape) == (C_out, n_head * D) and C_out % 64 == 0
+            and w.is_contiguous() and _aligned16(w) and (b is None or b.is_contiguous()))
+
+
+def attention_proj(qkv, n_head: int, n_kv_head: int, w, b, causal: bool = True, scale: Optional[float] = None,
+                   rope_cos=None, rope_sin=None, bias_grad_external: bool = False):
+    """``linear(attention_packed(qkv, ...), w, b)`` with the fused backward (see _AttnProjFn)."""
+    D = qkv.shape[-1] // (n_head + 2 * n_kv_head)
+    scale = scale if scale is not None else 1.0 / math.sqrt(D)
+    ext = bool(bias_grad_external and b is not None and not (_TORCH_OPS & {"norm", "act"}))
+    return _AttnProjFn.apply(qkv, n_head, n_kv_head, causal, scale, rope_cos, rope_sin, w, b, ext)
+
+
 _ATTN_WS_MB = [None]
 
 

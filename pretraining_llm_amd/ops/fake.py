@@ -55,8 +55,10 @@ def register() -> None:
         return dy.new_empty((dy.shape[1], x.shape[1]))
 
     @_reg("gemm_tn")
-    def _(a, b, bias, epi, aux=None, bias_acc=None):
+    def _(a, b, bias, epi, aux=None, bias_acc=None, T=0):
         M, N = a.shape[0], b.shape[0]
+        if epi == 6:  # dO and delta [M / T, N / 64, T] fp32
+            return a.new_empty((M, N)), a.new_empty((M // T, N // 64, T), dtype=torch.float32)
         return a.new_empty((M, 2 * N if epi == 5 else N)), a.new_empty((M if epi == 1 else 0, N))
 
     @_reg("act_fwd")
@@ -138,7 +140,7 @@ def register() -> None:
         return q.new_empty(q.shape)
 
     @_reg("attn_bwd")
-    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, rope_cos=None, rope_sin=None, rope_in=True):
+    def _(dout, q, k, v, o, lse, dq, dk, dv, causal, scale, rope_cos=None, rope_sin=None, rope_in=True, delta=None):
         return None
 
     @_reg("gemv")

@@ -212,3 +212,58 @@ def test_fused_swiglu_mlp_matches_unfused():
     for n, a, b in zip(["x", "w1", "w2"], gf, gu):
         assert a is not None, n
         assert _rel(a, b) < 1e-2, (n, _rel(a, b))
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 256, 12), (3, 200, 4), (1, 1024, 16)])
+def test_gemm_tn_attn_delta_epilogue(B, T, H):
+    """epi 6: dO = dy W_o (as epi 0, bitwise) plus delta[b, h, t] = sum_d dO * O per 64-wide head,
+    against fp64 math on the bf16 dO (what attn_bwd_pre_kernel reads)."""
+    torch.manual_seed(19)
+    C = H * 64
+    M = B * T
+    dy = (0.5 * torch.randn(M, C, device=DEV)).bfloat16()
+    wt = (torch.randn(C, C, device=DEV) / C ** 0.5).bfloat16()  # W_o^T shadow [H*D, C_out]
+    o = torch.randn(M, C, device=DEV).bfloat16()
+    do, delta = torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)
+    assert delta.shape == (B, H, T) and delta.dtype == torch.float32
+    assert torch.equal(do, torch.ops.pllm.gemm_tn(dy, wt, None, 0)[0])
+    ref = (do.double() * o.double()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
+    assert _rel(delta.double(), ref) < 1e-6, _rel(delta.double(), ref)
+    assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)[1], delta)  # deterministic
+
+
+@pytest.mark.parametrize("bias", [True, False])
+@pytest.mark.parametrize("ext", [False, True])
+def test_attn_proj_fused_matches_unfused(bias, ext):
+    """ops.attention_proj (projection dgrad + delta in one GEMM, attention backward without its
+    delta pass) vs attention_packed + linear."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(23)
+    B, T, H, D = 2, 256, 4, 64
+    C = H * D
+    qkv0 = (0.5 * torch.randn(B, T, 3 * C, device=DEV)).bfloat16()
+    w0 = (torch.randn(C, C, device=DEV) / C ** 0.5).bfloat16()
+    b0 = (0.1 * torch.randn(C, device=DEV)).bfloat16() if bias else None
+    dy = torch.randn(B, T, C, device=DEV).bfloat16()
+
+    def run(fused):
+        ps = [t.clone().requires_grad_() if t is not None else None for t in (qkv0, w0, b0)]
+        qkv, w, b = ps
+        with torch.enable_grad():
+            if fused:
+                assert ops.attn_proj_ok(qkv, H, H, w, b)
+                y = ops.attention_proj(qkv, H, H, w, b, bias_grad_external=ext)
+            else:
+                y = ops.linear(ops.attention_packed(qkv, H, H), w, b, bias_grad_external=ext)
+            y.backward(dy)
+        return y.detach(), [p.grad if p is not None else None for p in ps]
+
+    yf, gf = run(True)
+    yu, gu = run(False)
+    assert torch.equal(yf, yu)
+    for n, a, c in zip(["qkv", "w", "b"], gf, gu):
+        if c is None:
+            assert a is None, n
+            continue
+        assert a is not None, n
+        assert _rel(a, c) < 1e-2, (n, _rel(a, c))
