@@ -125,6 +125,24 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
   }
 #pragma unroll
   for (int hf = 0; hf < 2; ++hf) {
+    // the half's aux rows (EPI >= 3), all 8 (16 for EPI 5) loads issued before the LDS pack: their
+    // latency overlaps the pack and each other instead of one load -> use round trip per row
+    // block (kEpiOps unchanged: the same instructions, reordered)
+    // (two groups of 4 row blocks: group 1's loads go out as group 0's rows are processed; a fully
+    // unrolled 8-block loop spilled)
+    u32x4 anx[4], anx2[4];
+    auto aload = [&](int grp) {
+      if constexpr (EPI >= 3) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int rt = wm * 128 + hf * 64 + 8 * (4 * grp + k) + rsub;
+          const uint32_t ao = col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff;
+          anx[k] = buf_ld16(ars, ao);
+          if constexpr (EPI == 5) anx2[k] = buf_ld16(ars, col_ok ? ao + (uint32_t)N * 2u : kOff);
+        }
+      }
+    };
+    aload(0);
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
 #pragma unroll
@@ -152,8 +170,18 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
     // one wave writes and reads its own region: LDS executes a wave's accesses in order
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-    for (int it = 0; it < 8; ++it) {
+#pragma unroll 1
+    for (int grp = 0; grp < 2; ++grp) {
+    u32x4 apre[4], apre2[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      apre[k] = anx[k];
+      apre2[k] = anx2[k];
+    }
+    if (grp == 0) aload(1);
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int it = 4 * grp + kk;
       const int r = 8 * it + rsub;
       const int s = r & 15;
       u32x4 v = *reinterpret_cast<const u32x4*>(tile + r * 64 + ((((2 * c8) ^ s) & ~1) << 2));
@@ -174,7 +202,7 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
         bst16(crs, off, v);
         float d[8], o[8];
         unpack8(v, d);
-        unpack8(buf_ld16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff), o);
+        unpack8(apre[kk], o);
         float sum = 0.f;
 #pragma unroll
         for (int e = 0; e < 8; ++e) sum = __builtin_fmaf(d[e], o[e], sum);
@@ -191,9 +219,8 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
         // d = the bf16-rounded data gradient of the SwiGLU output (as swiglu_bwd_kernel reads it)
         float d[8], gt[8], up[8], dg[8], du[8];
         unpack8(v, d);
-        const uint32_t ao = col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff;
-        unpack8(buf_ld16(ars, ao), gt);
-        unpack8(buf_ld16(ars, col_ok ? ao + (uint32_t)N * 2u : kOff), up);
+        unpack8(apre[kk], gt);
+        unpack8(apre2[kk], up);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float sg = swiglu_sigmoid(gt[e]);
@@ -205,7 +232,7 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
       } else {
         float f[8], a[8];
         unpack8(v, f);
-        unpack8(buf_ld16(ars, col_ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kOff), a);
+        unpack8(apre[kk], a);
 #pragma unroll
         for (int e = 0; e < 8; ++e) f[e] = EPI == 3 ? f[e] * gelu_df(a[e]) : (a[e] > 0.f ? f[e] : 0.f);
         const u32x4 o = pack8(f);
@@ -215,6 +242,7 @@ PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pll
         for (int e = 0; e < 8; ++e) csum[e] += f[e];
       }
     }
+    }  // grp
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
   }
