@@ -386,7 +386,10 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
 namespace pllm {
 
 static int g_gemm_mfma = 16;
-static int g_gemm_group_m = 4;
+#ifndef PLLM_GEMM_GROUP_M
+#define PLLM_GEMM_GROUP_M 4  // m-tiles per tile group (L2 reuse of the B panels; A/B builds)
+#endif
+static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
 // 0: every wave issues its DMA pieces; 2: the asymmetric DMA (waves 0-3 issue all).  Measured and
 // removed (profiles/r3_gemm_tn.md): 1 = two k32 phases per K-tile with counted vmcnt across raw
 // barriers (3-12 % slower), 3 = one wave per SIMD with 128x128 per wave and the DMA pinned between
