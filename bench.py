@@ -61,9 +61,12 @@ def parse(argv=None):
     ap.add_argument("--no-tuned-gemm", action="store_true", help="use the libraries' default GEMM heuristics")
     ap.add_argument("--tune-missing", action="store_true", help="TunableOp-tune GEMM shapes missing from the table")
     ap.add_argument("--cuda-graph", nargs="?", const="1", default="auto", choices=["auto", "0", "1"],
-                    help="replay the whole step as one captured hipGraph (the Trainer's TORCH_COMPILE default); "
-                         "auto: on for one GPU on the HIP path (+0.5 %%, profiles/r3s3_graph_ab.txt), off with "
-                         "N > 1 ranks (RCCL collectives are not captured in the bench) and for ZeRO")
+                    help="replay the whole step as one captured hipGraph; auto: the Trainer's own policy "
+                         "(train/graph.py graph_step_policy): on for one GPU on the HIP path (+0.5 %%, "
+                         "profiles/r3s3_graph_ab.txt), off with N > 1 ranks unless --graph-collectives, off for ZeRO")
+    ap.add_argument("--graph-collectives", action="store_true",
+                    help="with N > 1 and --cuda-graph auto: capture the RCCL all-reduces inside the step's hipGraph "
+                         "(opt-in, as the Trainer's graph_collectives=True; default: eager hook-overlapped step)")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: functional rehearsal on gloo (fp32, tiny shapes); never a measurement")
     ap.add_argument("--verbose", action="store_true")
@@ -173,7 +176,11 @@ def main(argv=None):
         return loss
 
     if args.cuda_graph == "auto":
-        args.cuda_graph = "1" if (world == 1 and not cpu and args.backend == "auto" and not args.zero) else "0"
+        from pretraining_llm_amd.train.graph import graph_step_policy
+        ok, _why = graph_step_policy(cuda=not cpu, world=world, dist_backend=di.backend if world > 1 else None,
+                                     zero=bool(args.zero), hip_ops=args.backend == "auto" and bool(getattr(opt, "use_hip", False)),
+                                     graph_collectives=args.graph_collectives)
+        args.cuda_graph = "1" if ok else "0"
     args.cuda_graph = args.cuda_graph == "1"
     if args.cuda_graph:
         from pretraining_llm_amd.train.graph import GraphedTrainStep
@@ -240,6 +247,7 @@ def main(argv=None):
             "config": {"model": args.model, "global_batch": B * world, "seq_len": T,
                        "parallelism": f"dp{world}" + ("-zero1" if args.zero else ""), "micro_batch_per_gpu": B, "backend": args.backend,
                        "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph),
+                       "step_mode": "graph" if args.cuda_graph else "eager",
                        "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev))),
                        "checkpointed_blocks": int(model.checkpointed_blocks(torch.empty(B, T, device=dev)))},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),

@@ -203,11 +203,20 @@ class ShardedFlatAdamW(FlatAdamW):
         first = [p for m in (model.token_embed, getattr(model, "position_embed", None)) if m is not None
                  for p in m.parameters()]
         hooks.append(model.register_forward_pre_hook(lambda _m, _a: self.wait_params(first)))
-        for blk in list(getattr(model, "attn_blocks", [])) + [getattr(model, "layer_norm", None)]:
+        head = [p for p in (getattr(model, "head_weight", None), getattr(model, "head_bias", None)) if p is not None]
+        final_norm = getattr(model, "layer_norm", None)
+        for blk in list(getattr(model, "attn_blocks", [])) + [final_norm]:
             if blk is None:
                 continue
             ps = list(blk.parameters())
+            if blk is final_norm:
+                # the LM head (+ fused CE, which also produces the head's gradient) runs INSIDE
+                # GPT.forward right after the final norm, before the model's forward hook fires:
+                # its buckets (the buffer's tail, gathered last) must be waited for here
+                ps = ps + head
             hooks.append(blk.register_forward_pre_hook(lambda _m, _a, ps=ps: self.wait_params(ps)))
+        if final_norm is None and head:
+            hooks.append(model.register_forward_pre_hook(lambda _m, _a: self.wait_params(head)))
         hooks.append(model.register_forward_hook(lambda _m, _a, _o: self.wait_params()))
         return hooks
 

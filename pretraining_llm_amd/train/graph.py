@@ -19,8 +19,42 @@ step over the fp32 accumulated gradient scaled by 1/accum.  The static inputs ar
 from __future__ import annotations
 
 import contextlib
+from typing import Optional, Tuple
 
 import torch
+
+
+def graph_step_policy(*, cuda: bool, world: int, dist_backend: Optional[str], zero: bool = False,
+                      model_parallel: bool = False, loss_scaling: bool = False, bf16: bool = True,
+                      hip_ops: bool = True, graph_collectives: bool = False) -> Tuple[bool, Optional[str]]:
+    """THE decision whether a training step is replayed as one captured hipGraph, shared by
+    ``Trainer`` (TORCH_COMPILE default) and ``bench.py`` (``--cuda-graph auto``) so the path the
+    driver's multi-GPU bench measures is the path ``torchrun scripts/train_transformer.py`` runs.
+
+    Returns ``(use_graph, reason_if_not)``.  With more than one rank the default is the EAGER
+    step: the bucketed RCCL all-reduces are launched from the backward hooks on RCCL's own stream
+    and overlap the rest of the backward.  Capturing those collectives inside the graph is an
+    explicit opt-in (``graph_collectives=True``): it cannot be exercised on a one-GPU box (two
+    RCCL ranks cannot share a device), so it is not the default of any launch path."""
+    if not cuda:
+        return False, "not a GPU run"
+    if zero:
+        return False, "ZeRO-1 (collectives inside the optimizer step)"
+    if model_parallel:
+        return False, "tensor / context parallelism"
+    if loss_scaling:
+        return False, "loss scaling (host-side skip decision)"
+    if not bf16:
+        return False, "non-bf16 dtype (the graphed step runs the bf16 HIP kernels)"
+    if not hip_ops:
+        return False, "stock torch ops backend (PLLM_TORCH_OPS / set_backend)"
+    if world > 1:
+        if dist_backend != "nccl":
+            return False, f"dist backend {dist_backend} (collectives cannot be captured)"
+        if not graph_collectives:
+            return False, ("world > 1: eager step with hook-launched RCCL buckets (the bench's multi-GPU path); "
+                           "graph_collectives=True captures the collectives too")
+    return True, None
 
 
 class GraphedTrainStep:

@@ -80,7 +80,12 @@ class Trainer:
         self.device = self.di.device
         seed = int(self.cfg.get("seed", 1337))
         torch.manual_seed(seed)  # identical init on every rank (then broadcast for certainty)
-        if self.cfg.get("deterministic", False):
+        from ..utils import memory as _mem
+        det = bool(self.cfg.get("deterministic", False))
+        # workspace budgets (CE chunk rows, attention dQ slabs) decided once, not per call from the
+        # free HBM; deterministic: pinned to their fixed caps (utils/memory.py)
+        _mem.freeze_budgets(pin_caps=det)
+        if det:
             # every hand-written kernel already reduces in a fixed order (attention dQ slabs,
             # split-K wgrad slabs, sorted embedding backward); this pins torch's own ops too
             torch.use_deterministic_algorithms(True, warn_only=True)
@@ -148,14 +153,15 @@ class Trainer:
         self.use_graph = False
         self.fwd = self.model
         if self.compile and self.device.type == "cuda":
-            why = ("ZeRO-1 (collectives inside the optimizer step)"
-                   if int(self.cfg.get("zero_stage", 0)) >= 1 else "tensor / context parallelism"
-                   if self.pg.model_parallel else "loss scaling (host-side skip decision)" if self.scaler.enabled
-                   else f"dtype={dtype_name} (the graphed step runs the bf16 HIP kernels)"
-                   if self.dtype != torch.bfloat16 else "stock torch ops backend (PLLM_TORCH_OPS / set_backend)"
-                   if not self._hip_step_ok() else "dist backend gloo (collectives cannot be captured)"
-                   if dist.is_initialized() and dist.get_backend() != "nccl" else None)
-            if why is None:
+            # the same policy bench.py applies (train/graph.py): at world > 1 the eager step with
+            # hook-launched RCCL buckets unless graph_collectives=True
+            from .graph import graph_step_policy
+            ok, why = graph_step_policy(
+                cuda=True, world=self.di.world_size, dist_backend=dist.get_backend() if dist.is_initialized() else None,
+                zero=int(self.cfg.get("zero_stage", 0)) >= 1, model_parallel=self.pg.model_parallel,
+                loss_scaling=self.scaler.enabled, bf16=self.dtype == torch.bfloat16, hip_ops=self._hip_step_ok(),
+                graph_collectives=bool(self.cfg.get("graph_collectives", False)))
+            if ok:
                 self.use_graph = True
                 if self.di.is_master:
                     self.log(f"TORCH_COMPILE: whole training step captured as a hipGraph (grad_accum_steps={self.accum})")
@@ -163,6 +169,7 @@ class Trainer:
                 self.log(f"TORCH_COMPILE: hipGraph step disabled for this configuration ({why}); running eagerly")
         elif self.compile:
             self.fwd = torch.compile(self.model, backend=self.cfg.get("compile_backend", "inductor"))
+        self.step_mode = "graph" if self.use_graph else "eager"
         self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
         self.train_loader = self._loader(self.cfg["train_path"], seed, 0)
         vp = self.cfg.get("val_path") or self.cfg.get("dev_path")

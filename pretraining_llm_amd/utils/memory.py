@@ -31,13 +31,40 @@ def free_hbm_bytes(device: torch.device) -> int:
     return int(free + max(0, slack))
 
 
+# Budget policy.  The chunking a budget selects changes the fp32 grouping of some sums (e.g. the
+# LM-head weight gradient accumulates per CE chunk), so a budget re-read from the free HBM on every
+# call makes same-seed runs depend on the memory state.  ``freeze_budgets()`` (the Trainer calls
+# it) computes each budget once, at its first use, and keeps it; ``freeze_budgets(pin_caps=True)``
+# (``deterministic=True``) pins every budget to its cap, independent of the device's state.
+_policy = {"mode": "live"}   # live | frozen | caps
+_frozen: dict = {}
+
+
+def freeze_budgets(pin_caps: bool = False) -> None:
+    _policy["mode"] = "caps" if pin_caps else "frozen"
+    _frozen.clear()
+
+
+def live_budgets() -> None:
+    _policy["mode"] = "live"
+    _frozen.clear()
+
+
 def workspace_budget(device: torch.device, cap_bytes: int, fraction: float, floor_bytes: int,
                      free_fn: Optional[Callable[[torch.device], int]] = None) -> int:
-    """``fraction`` x free HBM, clamped to [floor_bytes, cap_bytes] (CPU: the cap)."""
-    if device.type != "cuda" and free_fn is None:
+    """``fraction`` x free HBM, clamped to [floor_bytes, cap_bytes] (CPU: the cap); see the policy
+    above for the frozen / pinned modes."""
+    mode = _policy["mode"]
+    if mode == "caps" or (device.type != "cuda" and free_fn is None):
         return int(cap_bytes)
+    key = (str(device), int(cap_bytes), float(fraction), int(floor_bytes))
+    if mode == "frozen" and key in _frozen:
+        return _frozen[key]
     free = (free_fn or free_hbm_bytes)(device)
-    return int(max(floor_bytes, min(cap_bytes, fraction * free)))
+    b = int(max(floor_bytes, min(cap_bytes, fraction * free)))
+    if mode == "frozen":
+        _frozen[key] = b
+    return b
 
 
 # defaults: caps = the budgets measured to keep every shipped config in one chunk / pass

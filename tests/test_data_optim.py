@@ -140,6 +140,7 @@ def test_workspace_budgets_follow_free_hbm():
     from pretraining_llm_amd.utils import memory as M
     dev = torch.device("cuda", 0)
     GiB = 2 ** 30
+    M.live_budgets()  # a Trainer built by an earlier test froze them
     assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 200 * GiB) == M.CE_CAP
     assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 8 * GiB) == 2 * GiB
     assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 0) == M.CE_FLOOR
@@ -148,3 +149,13 @@ def test_workspace_budgets_follow_free_hbm():
     assert _ce_chunk_rows(N, V, M.CE_CAP) == N                     # one chunk with a roomy device
     r = _ce_chunk_rows(N, V, 2 * GiB)                               # a fuller device: 4 chunks
     assert r % 64 == 0 and -(-N // r) == 4 and r * V * 2 <= 2 * GiB + 64 * V * 2
+    # frozen at first use (the Trainer's default) / pinned to the cap (deterministic=True)
+    try:
+        M.freeze_budgets()
+        first = M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 8 * GiB)
+        later = M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 1 * GiB)
+        assert first == later == 2 * GiB
+        M.freeze_budgets(pin_caps=True)
+        assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 1 * GiB) == M.CE_CAP
+    finally:
+        M.live_budgets()

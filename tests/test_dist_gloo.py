@@ -168,6 +168,7 @@ def test_bench_self_launches_ranks_cpu():
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "dp2" and rec["config"]["global_batch"] == 4
     c = rec["comm"]
     assert c["world"] == 2 and c["hook_launched_buckets"]
+    assert rec["config"]["step_mode"] == "eager" and not rec["config"]["cuda_graph"]
     # multi-GPU diagnostics: per-rank step times, the RCCL environment the run had (set before
     # the process group existed), exposed-communication fields (HIP events: None on CPU)
     assert c["rank_step_ms_min"] <= c["rank_step_ms_max"] and abs(c["rank_step_ms_max"] - rec["ms_per_step"]) < 1e-2
@@ -206,3 +207,27 @@ def test_byte_tokenizer_renders_non_byte_ids():
     ids = t.encode("héllo") + [1234, 50256] + t.encode("!")
     assert t.decode(ids) == "héllo<|1234|><|50256|>!"
     assert t.decode(t.encode("plain")) == "plain"
+
+
+def test_trainer_and_bench_share_the_step_policy():
+    """the Trainer's world > 1 step and ``bench.py --gpus N`` must be the same path.
+    Both decide through ``train/graph.py: graph_step_policy``; at world > 1 on RCCL the default
+    is the eager step with hook-launched buckets (capture is the ``graph_collectives`` opt-in),
+    at world 1 the hipGraph step."""
+    import inspect
+    import sys
+    from pretraining_llm_amd.train import graph as g
+    from pretraining_llm_amd.train import trainer as tr
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    assert "graph_step_policy(" in inspect.getsource(tr.Trainer.__init__)
+    assert "graph_step_policy(" in inspect.getsource(bench.main)
+    for world in (2, 4, 8):
+        ok, why = g.graph_step_policy(cuda=True, world=world, dist_backend="nccl")
+        assert not ok and "eager" in why
+        assert g.graph_step_policy(cuda=True, world=world, dist_backend="nccl", graph_collectives=True)[0]
+        assert not g.graph_step_policy(cuda=True, world=world, dist_backend="gloo", graph_collectives=True)[0]
+    assert g.graph_step_policy(cuda=True, world=1, dist_backend=None) == (True, None)
+    assert not g.graph_step_policy(cuda=True, world=1, dist_backend=None, zero=True)[0]
+    assert not g.graph_step_policy(cuda=False, world=1, dist_backend=None)[0]

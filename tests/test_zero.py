@@ -24,9 +24,12 @@ def _free_port():
     return port
 
 
-def _cfg():
+def _cfg(untied=False):
     from pretraining_llm_amd.models import get_preset
-    return get_preset("gpt2-tiny").replace(vocab_size=256, context_length=32, n_embed=64, n_head=2)
+    cfg = get_preset("gpt2-tiny").replace(vocab_size=256, context_length=32, n_embed=64, n_head=2)
+    # untied biased LM head (the reference architecture's head): its parameters sit at the buffer's
+    # tail, i.e. in the bucket whose all-gather step() issues last
+    return cfg.replace(tie_embeddings=False, head_bias=True) if untied else cfg
 
 
 def _train(model_opt_engine, data, rank, steps, accum=1):
@@ -51,7 +54,7 @@ class _null:
         return False
 
 
-def _worker(rank, world, port, outdir, accum):
+def _worker(rank, world, port, outdir, accum, untied=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(1)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -59,7 +62,7 @@ def _worker(rank, world, port, outdir, accum):
     from pretraining_llm_amd.parallel.dp import DataParallelEngine
     from pretraining_llm_amd.parallel.zero import ShardedFlatAdamW, ZeroDataParallelEngine
     from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
-    cfg = _cfg()
+    cfg = _cfg(untied)
     g = torch.Generator().manual_seed(7)
     data = torch.randint(0, 256, (2 * world * accum, 33), generator=g)
     kw = dict(lr=1e-2, weight_decay=0.1, decay_filter=no_decay_1d, max_grad_norm=0.5)
@@ -78,9 +81,22 @@ def _worker(rank, world, port, outdir, accum):
     # the step leaves its bucket all-gathers pending; the next forward waits for each bucket at
     # its first use (pre-hooks), so no blanket wait ends the step
     pending_after_step = len(o_z._gathers)
+    # the LM head runs inside GPT.forward right after the final norm: its buckets must no longer be
+    # pending when the final norm starts (hooks run in registration order: this one after ZeRO's)
+    head = [p for p in (m_z.head_weight, m_z.head_bias) if p is not None]
+    head_buckets = set(o_z._buckets_of(head))
+    seen = {}
+
+    def probe(_m, _a):
+        seen.setdefault("head_pending", bool(head_buckets & set(o_z._gathers)))
+
+    h = m_z.layer_norm.register_forward_pre_hook(probe)
     with torch.no_grad():
-        m_z(data[:2, :-1], data[:2, 1:])
-    out_lazy = {"pending_after_step": pending_after_step, "pending_after_fwd": len(o_z._gathers)}
+        _, loss_z = m_z(data[:2, :-1], data[:2, 1:])
+        _, loss_ref = m_ref(data[:2, :-1], data[:2, 1:])
+    h.remove()
+    out_lazy = {"pending_after_step": pending_after_step, "pending_after_fwd": len(o_z._gathers),
+                "head_pending_at_norm": seen["head_pending"], "fwd_loss_diff": abs(loss_z.item() - loss_ref.item())}
     out = {**out_lazy, "diff": (o_ref.flat_param[:o_ref.total] - o_z.flat_param[:o_ref.total]).abs().max().item(),
            "shard_frac": o_z.master.numel() / o_z.total, "nbuckets": len(o_z.buckets)}
     sd_ref, sd_z = o_ref.state_dict(), o_z.state_dict()  # collective for the sharded one
@@ -110,9 +126,9 @@ def _worker(rank, world, port, outdir, accum):
     dist.destroy_process_group()
 
 
-def _run(world, accum=1):
+def _run(world, accum=1, untied=False):
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_worker, args=(world, _free_port(), d, accum), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), d, accum, untied), nprocs=world, join=True)
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
 
 
@@ -126,6 +142,8 @@ def _check(res, world):
         assert r["nbuckets"] > 2
         assert len(set(r["replicas"])) == 1
         assert r["pending_after_step"] == r["nbuckets"] and r["pending_after_fwd"] == 0, r
+        assert not r["head_pending_at_norm"], r
+        assert r["fwd_loss_diff"] < 1e-4, r
 
 
 def test_zero1_matches_replicated_world2():
@@ -134,3 +152,8 @@ def test_zero1_matches_replicated_world2():
 
 def test_zero1_matches_replicated_world3_accum():
     _check(_run(3, accum=2), 3)
+
+
+def test_zero1_untied_head_world2():
+    # the untied LM head's bucket used to be waited for only after GPT.forward returned
+    _check(_run(2, untied=True), 2)
