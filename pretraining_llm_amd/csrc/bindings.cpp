@@ -969,8 +969,8 @@ TORCH_LIBRARY(pllm, m) {
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
-  m.def("gemm_set_config(int mfma, int group_m, int phased=-1) -> ()",
-        [](int64_t mf, int64_t gm, int64_t ph) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph); });
+  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1) -> ()",
+        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc); });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });

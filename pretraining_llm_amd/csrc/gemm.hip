@@ -394,11 +394,15 @@ static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
 // removed (profiles/r3_gemm_tn.md): 1 = two k32 phases per K-tile with counted vmcnt across raw
 // barriers (3-12 % slower), 3 = one wave per SIMD with 128x128 per wave and the DMA pinned between
 // MFMA groups (hipBLASLt's geometry; 4-18 % slower, its fused epilogues up to 40 % slower)
+// 4: the ping-pong kernel of gemm_pp.hip (two wave groups one barrier apart, counted waits)
 static int g_gemm_phased = 0;
-void gemm_set_config(int mfma, int group_m, int phased) {
+// CUs the persistent grids leave free, for RCCL kernels overlapping the backward (world > 1)
+static int g_gemm_reserve = 0;
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus) {
   if (mfma == 16 || mfma == 32) g_gemm_mfma = mfma;
   if (group_m > 0) g_gemm_group_m = group_m;
   if (phased >= 0) g_gemm_phased = phased;
+  if (reserve_cus >= 0) g_gemm_reserve = reserve_cus;
 }
 
 int gemm_colsum_groups(int M) { return 2 * ((M + GT - 1) / GT); }
@@ -418,7 +422,13 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
   a.group_m = g_gemm_group_m;
   const int ntiles = ((a.M + GT - 1) / GT) * ((a.N + GT - 1) / GT);
   if (ntiles == 0) return;
-  const int tiles = ntiles < num_cus() ? ntiles : num_cus();  // persistent grid: one workgroup per CU
+  // persistent grid: one workgroup per CU, minus the CUs reserved for concurrent collectives
+  const int ctas = num_cus() - g_gemm_reserve > 8 ? num_cus() - g_gemm_reserve : 8;
+  if (g_gemm_phased == 4) {
+    gemm_tn_pp(a, epi, ctas, st);
+    return;
+  }
+  const int tiles = ntiles < ctas ? ntiles : ctas;
 #define PLLM_GEMM_CASE(MFV, E)                                                       \
   do {                                                                               \
     if (g_gemm_phased == 2)                                                          \

@@ -1,0 +1,442 @@
+// Ping-pong TN GEMM with fused epilogues on gfx950 MFMA (round 4):
+//     C[M, N] = epi( A[M, K] . B[N, K]^T )          (bf16 in, fp32 accumulate, bf16 out)
+// Same contract and epilogues as gemm_tn_kernel (csrc/gemm.hip, which stays as the A/B
+// reference); a structurally different main loop, built for the measured bottleneck of that
+// kernel: its waves parked 36 % of the time on the one barrier + vmcnt(0) per 64-deep K-tile
+// (profiles/r3_gemm_tn.md: MFMA busy 41 % vs hipBLASLt's 52 %).  Reference math: the MLP and
+// attention projections of /root/reference/src/models/mlp.py:24-26 and attention.py:29-31.
+//
+// Design (cdna_hip_programming.md §5 "8-phase", T3/T4/T5; MI355X_MICROARCH.md "Two waves per
+// SIMD"):
+//  * 256x256 output tile per 512-thread workgroup, persistent over tiles (grouped order, XCD-aware
+//    block remap); wave (wr, wc) owns rows wr*128 + [0,128) and columns wc*64 + [0,64): 8 x 4
+//    MFMA 16x16x32 accumulators (128 fp32 per lane);
+//  * a 64-deep K-tile is 4 PHASES, each one 64x32 quadrant of the wave's tile (16 MFMAs); the
+//    two wave groups (waves 0-3 = rows 0-127, waves 4-7 = rows 128-255; one wave of each on every
+//    SIMD) run one barrier apart (group 1 takes an extra s_barrier up front), so on every SIMD one
+//    wave issues its 16 MFMAs while its partner reads the next quadrant's fragments and issues its
+//    share of the next K-tile's DMA: the matrix pipe alternates between the two waves instead of
+//    idling at a shared barrier;
+//  * K-tile s+1 is DMA'd (buffer_load ... lds, 1 KiB pieces, XOR-swizzled images through the
+//    per-lane SOURCE address) during K-tile s's four phases, in the order of first use (A rows of
+//    both groups' first quadrant, B columns of the first quadrant, B columns of the second, A rows
+//    of the second): every piece has >= 3 phases to land, and each phase waits with a COUNTED
+//    vmcnt(4) (never 0 in the main loop) before its barrier;
+//  * one VGPR offset per operand and piece parity; a piece's row offset goes into the buffer
+//    descriptor's base (scalar), so the DMA plan costs 4 VGPRs instead of one per piece (the
+//    spill that sank the round-3 one-wave-per-SIMD variant);
+//  * the B image rows are permuted inside each 32-row block (image row 16h + 4g + r <- column
+//    8g + 4h + r) so that the accumulators of column tiles 2p and 2p+1 hold 8 CONSECUTIVE output
+//    columns per lane: the epilogue stores 16 B per lane straight from registers (no LDS round
+//    trip), with bias / GELU / ReLU / GELU' / ReLU' / SwiGLU' / attention-delta math on the way.
+// Requires K % 64 == 0, N % 8 == 0, lda / ldc / ldaux % 8 == 0 (checked by the binding).
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int PT = 256;            // output tile (M and N)
+constexpr int PBK = 64;            // K per K-tile
+constexpr int PNT = 512;           // 8 waves
+constexpr int PIMG = PT * PBK;     // elements of one operand image [256][64]
+constexpr int PSLOT = 2 * PIMG;    // A image then B image: 64 KiB
+constexpr uint32_t kPOff = 0x80000000u;  // a byte offset past every descriptor built here
+
+PLLM_DEV bf16x8 ldsf(const uint16_t* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
+PLLM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+PLLM_DEV void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int N>
+PLLM_DEV void pp_vmwait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// grouped tile order: GROUP_M m-tiles x all n-tiles, m fastest inside a group
+PLLM_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int per_group = gm * tiles_n;
+  const int grp = t / per_group, first_m = grp * gm, gsize = min(gm, tiles_m - first_m);
+  tm = first_m + (t % per_group) % gsize;
+  tn = (t % per_group) / gsize;
+}
+
+// the epilogue's vector-memory instructions issued after its last wait (its C / aux stores):
+// a lower bound is what the counted waits of the next tile's first two phases need
+template <int EPI>
+constexpr int kPPEpiStores = (EPI == 5 || EPI == 1) ? 32 : 16;
+
+PLLM_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+}
+PLLM_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
+PLLM_DEV float pp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+
+// ---------------------------------------------------------------------------------------------
+// Epilogue of one 256x256 tile, straight from the accumulators.  Lane (r16 = lane & 15,
+// g = lane >> 4) holds, for row tile j and column pair p, output row wr*128 + 16j + r16 and the 8
+// columns wc*64 + 32p + 8g + [0, 8): acc[2p][j][0..3] then acc[2p+1][j][0..3].
+template <int EPI>
+PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc, int lane) {
+  const int M = g.M, N = g.N;
+  const int m0 = tm * PT, n0 = tn * PT;
+  const int rows_ok = min(PT, M - m0);
+  constexpr int W2 = EPI == 5 ? 2 : 1;  // EPI 5: C and aux rows hold two N-wide halves
+  const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)m0 * g.ldc, rows_ok, g.ldc, W2 * N);
+  const __amdgpu_buffer_rsrc_t ars =
+      rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)m0 * g.ldaux : g.C, rows_ok, g.ldaux, W2 * N);
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int colw = n0 + wc * 64 + 8 * g4;  // + 32 p
+  const bool cok0 = colw < N, cok1 = colw + 32 < N;
+  float bias[2][8];
+  if constexpr (EPI <= 2) {
+    const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.bias != nullptr ? g.bias : g.A), (short)0, g.bias != nullptr ? N * 2 : 0, 0x00020000);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bool ok = p == 0 ? cok0 : cok1;
+      unpack8(buf_ld16(brs, ok ? (uint32_t)(colw + 32 * p) * 2u : kPOff), bias[p]);
+    }
+  }
+  float csum[2][8];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) csum[p][e] = 0.f;
+  const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(g.delta != nullptr ? g.delta : (float*)g.C), (short)0, EPI == 6 ? (int)(4ll * M * N / 64) : 0,
+      0x00020000);
+  // aux rows (EPI >= 3) one row tile ahead: the loads of tile j + 1 fly while tile j is processed,
+  // and the scheduling barrier at the end of each tile keeps the compiler from hoisting all 16-32
+  // loads to the top, where the 128 accumulators are still live (that spilled)
+  constexpr int NAX = EPI >= 3 ? (EPI == 5 ? 4 : 2) : 0;
+  u32x4 axc[NAX > 0 ? NAX : 1], axn[NAX > 0 ? NAX : 1];
+  auto aux_load = [&](int j, u32x4* dst) {
+    if constexpr (NAX > 0) {
+      const int rt = wr * 128 + 16 * j + r16;
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const bool ok = p == 0 ? cok0 : cok1;
+        const uint32_t aoff = ok ? (uint32_t)(((int64_t)rt * g.ldaux + colw + 32 * p) * 2) : kPOff;
+        dst[p] = buf_ld16(ars, aoff);
+        if constexpr (EPI == 5) dst[2 + p] = buf_ld16(ars, ok ? aoff + (uint32_t)N * 2u : kPOff);
+      }
+    }
+  };
+  aux_load(0, axc);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int rt = wr * 128 + 16 * j + r16;  // row within the tile
+    if (j + 1 < 8) aux_load(j + 1, axn);
+    float dsum = 0.f;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bool ok = p == 0 ? cok0 : cok1;
+      const int col = colw + 32 * p;
+      const uint32_t off = ok ? (uint32_t)(((int64_t)rt * g.ldc + col) * 2) : kPOff;
+      const uint32_t aoff = ok ? (uint32_t)(((int64_t)rt * g.ldaux + col) * 2) : kPOff;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[e] = acc[2 * p][j][e];
+        v[4 + e] = acc[2 * p + 1][j][e];
+      }
+      if constexpr (EPI == 0) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[p][e];
+        pp_st16(crs, off, pack8(v));
+      } else if constexpr (EPI == 1) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bias[p][e];
+        const u32x4 pre = pack8(v);
+        float f[8];
+        unpack8(pre, f);  // the activation reads the bf16-rounded pre-activation
+#pragma unroll
+        for (int e = 0; e < 8; ++e) f[e] = gelu_f(f[e]);
+        pp_st16(ars, aoff, pre);
+        pp_st16(crs, off, pack8(f));
+      } else if constexpr (EPI == 2) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e] + bias[p][e], 0.f);
+        pp_st16(crs, off, pack8(v));
+      } else if constexpr (EPI == 3 || EPI == 4) {
+        float a[8];
+        unpack8(axc[p], a);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = bfr(v[e]);  // the unfused path's bf16 data gradient
+          v[e] = EPI == 3 ? d * gelu_df(a[e]) : (a[e] > 0.f ? d : 0.f);
+        }
+        const u32x4 o = pack8(v);
+        pp_st16(crs, off, o);
+        unpack8(o, v);  // the bias gradient sums the bf16-rounded values, like act_bwd_colsum
+#pragma unroll
+        for (int e = 0; e < 8; ++e) csum[p][e] += v[e];
+        __builtin_amdgcn_sched_barrier(0);  // one 8-column group of GELU' math at a time
+      } else if constexpr (EPI == 5) {
+        float gt[8], up[8], dg[8], du[8];
+        unpack8(axc[p], gt);
+        unpack8(axc[2 + p], up);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float d = bfr(v[e]);
+          const float sg = pp_sigmoid(gt[e]);
+          du[e] = d * (gt[e] * sg);
+          dg[e] = d * up[e] * sg * (1.f + gt[e] * (1.f - sg));
+        }
+        pp_st16(crs, off, pack8(dg));
+        pp_st16(crs, ok ? off + (uint32_t)N * 2u : kPOff, pack8(du));
+      } else {  // EPI 6: dO stored; delta = sum over the wave's 64 columns (one head) of dO * O
+        const u32x4 o = pack8(v);
+        pp_st16(crs, off, o);
+        float d[8], oo[8];
+        unpack8(o, d);
+        unpack8(axc[p], oo);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dsum = __builtin_fmaf(d[e], oo[e], dsum);
+      }
+    }
+    if constexpr (EPI == 6) {
+      // the row's 4 lane groups (g = 0..3: lanes r16, r16 + 16, + 32, + 48) in a fixed order
+      dsum += __shfl_xor(dsum, 16, 64);
+      dsum += __shfl_xor(dsum, 32, 64);
+      const int m = m0 + rt;
+      const int bq = m / g.T, tq = m - bq * g.T, hd = (n0 + wc * 64) >> 6;
+      const uint32_t doff = (g4 == 0 && m < M && cok0)
+                                ? (uint32_t)((((int64_t)bq * (N >> 6) + hd) * g.T + tq) * 4) : kPOff;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dsum), drs, doff, 0, 0);
+    }
+    if constexpr (NAX > 0) {
+#pragma unroll
+      for (int x = 0; x < NAX; ++x) axc[x] = axn[x];
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (EPI == 3 || EPI == 4) {
+    // lanes r16 = 0..15 of a lane group hold the same 8 columns; rows past M contributed zeros
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        float s = csum[p][e];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        csum[p][e] = s;
+      }
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.colpart + (int64_t)(2 * tm + wr) * N), (short)0, N * 4, 0x00020000);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const bool ok = (p == 0 ? cok0 : cok1) && r16 == 0;
+      const uint32_t po = ok ? (uint32_t)(colw + 32 * p) * 4u : kPOff;
+      pp_st16(prs, po, __builtin_bit_cast(u32x4, f32x4{csum[p][0], csum[p][1], csum[p][2], csum[p][3]}));
+      pp_st16(prs, ok ? po + 16u : kPOff,
+              __builtin_bit_cast(u32x4, f32x4{csum[p][4], csum[p][5], csum[p][6], csum[p][7]}));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+struct PPCtx {
+  const pllm::GemmArgs* g;
+  int w, wr, wc, lane;
+  unsigned lds;           // byte address of the LDS array
+  uint32_t vA[2], vB[2];  // per-lane DMA source offsets, even / odd piece
+  unsigned rdA[2], rdB[2];  // per-lane LDS byte offsets of the fragment reads (k32 = 0, 1), slot 0
+};
+
+// DMA of piece group PH (2 pieces per wave) of K-tile kt of tile (tm, tn) into LDS slot sl.
+// PH 0: A rows 0-63 of both row halves, 1: B image rows of column pair 0 of every wave,
+// 2: B column pair 1, 3: A rows 64-127 of both halves.  valid = false: zero-range descriptors
+// (same instruction count, so the counted waits stay exact; nothing reads that slot again).
+template <int PH>
+PLLM_DEV void pp_issue(const PPCtx& c, int tm, int tn, int kt, int sl, bool valid) {
+  // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
+  const pllm::GemmArgs& g = *c.g;
+  constexpr bool isA = PH == 0 || PH == 3;
+  const int w = c.w;
+  const int blk0 = PH == 0 ? 2 * w + 8 * (w >> 2)
+                   : PH == 3 ? 8 + 2 * w + 8 * (w >> 2)
+                   : PH == 1 ? 8 * (w >> 1) + 2 * (w & 1)
+                             : 4 + 8 * (w >> 1) + 2 * (w & 1);
+  const int64_t ld = isA ? g.lda : g.ldb;
+  const int rows_ok = isA ? min(PT, g.M - tm * PT) : min(PT, g.N - tn * PT);
+  const uint16_t* base = (isA ? g.A + (int64_t)tm * PT * g.lda : g.B + (int64_t)tn * PT * g.ldb) + kt * PBK;
+  const int kleft2 = (g.K - kt * PBK) * 2;
+  const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG)) * 2u;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int blk = blk0 + q;
+    const int prow0 = isA ? 8 * blk : 32 * (blk >> 2) + 16 * (blk & 1) + 4 * ((blk >> 1) & 1);
+    const int left = rows_ok - prow0;
+    const uint32_t bytes = (valid && left > 0) ? (uint32_t)((int64_t)(left - 1) * ld * 2 + kleft2) : 0u;
+    const i32x4v srd = srd_of(base + (int64_t)prow0 * ld, bytes);
+    blds16(srd, isA ? c.vA[q] : c.vB[q], lds0 + 1024u * (unsigned)blk);
+  }
+}
+
+// One phase of a K-tile: the LOAD segment (fragment reads for this phase's quadrant, the next
+// K-tile's piece group PH, the counted wait), a barrier, the MFMA segment (16 MFMAs), a barrier.
+// VM: the vmcnt of the wait (4 in steady state; 4 + the epilogue's stores in the first two
+// phases of a tile).
+template <int PH, bool FIRST, int VM>
+PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
+                       const uint16_t* slotp, int ntm, int ntn, int nkt, int nsl, bool nvalid) {
+  const int wr = c.wr, wc = c.wc;
+  const char* sb = reinterpret_cast<const char*>(slotp);
+  // ---- LOAD segment
+  if constexpr (PH == 0 || PH == 2) {
+    const int jh = PH == 0 ? 0 : 1;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        fa[k][jj] = ldsf(reinterpret_cast<const uint16_t*>(
+            sb + c.rdA[k] + (unsigned)((wr * 128 + 16 * (4 * jh + jj)) * PBK * 2)));
+  }
+  if constexpr (PH == 0 || PH == 1) {
+    const int p = PH;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+        fb[p][k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
+            sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
+  }
+  pp_issue<PH>(c, ntm, ntn, nkt, nsl, nvalid);
+  pp_vmwait<VM>();
+  pp_barrier();
+  // ---- MFMA segment: quadrant (rows half jh, column pair p)
+  {
+    constexpr int jh = PH >= 2 ? 1 : 0;
+    constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii) {
+          f32x4& a = acc[2 * p + ii][4 * jh + jj];
+          if (FIRST && k == 0) a = mfma16(fb[p][k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
+          else a = mfma16(fb[p][k][ii], fa[k][jj], a);
+        }
+    __builtin_amdgcn_s_setprio(0);
+  }
+  pp_barrier();
+}
+
+template <bool FIRST, int EPI>
+PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
+                       const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid) {
+  const uint16_t* slotp = smem + (s & 1) * PSLOT;
+  const int nsl = (s + 1) & 1;
+  constexpr int VE = FIRST ? 4 + kPPEpiStores<EPI> : 4;
+  pp_phase<0, FIRST, VE>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
+  pp_phase<1, FIRST, VE>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
+  pp_phase<2, FIRST, 4>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
+  pp_phase<3, FIRST, 4>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
+  // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads)
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT];
+  const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + PT - 1) / PT, ntiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int lid = xcd_remap(blockIdx.x, G);
+  if (lid >= ntiles) return;
+  PPCtx c;
+  c.g = &g;
+  const int tid = threadIdx.x, lane = tid & 63;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+  c.lane = lane;
+  c.lds = (unsigned)(uintptr_t)smem;
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    // lane l of a piece fills image row 8 * blk + l / 8 at 16-B position l % 8, which holds
+    // logical chunk (l % 8) ^ swz(row), swz(row) = (row >> 1) & 7 = (4 * (blk & 1) + l / 16) & 7
+    const int ch = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);
+    c.vA[par] = (uint32_t)(((int64_t)(lane >> 3) * g.lda + ch * 8) * 2);
+    const int prow = 8 * ((lane >> 5) & 1) + ((lane >> 3) & 3);  // B column permutation, per-lane part
+    c.vB[par] = (uint32_t)(((int64_t)prow * g.ldb + ch * 8) * 2);
+  }
+  {
+    // fragment reads: image row (16-aligned base) + r16, chunk 4 k32 + g, swizzled by (r16 >> 1) & 7
+    const int r16 = lane & 15, g4 = lane >> 4;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const unsigned off = (unsigned)(r16 * PBK + ((((4 * k + g4) ^ ((r16 >> 1) & 7))) << 3)) * 2u;
+      c.rdA[k] = off;
+      c.rdB[k] = off;
+    }
+  }
+  const int S = g.K / PBK;
+  int tm, tn;
+  pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
+  // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
+  pp_issue<0>(c, tm, tn, 0, 0, true);
+  pp_issue<1>(c, tm, tn, 0, 0, true);
+  pp_issue<2>(c, tm, tn, 0, 0, true);
+  pp_issue<3>(c, tm, tn, 0, 0, true);
+  pp_vmwait<0>();
+  pp_barrier();
+  if (c.wr == 1) pp_barrier();  // the stagger: rows 128-255 run one barrier behind rows 0-127
+
+  f32x4 acc[4][8];
+  bf16x8 fa[2][4];
+  bf16x8 fb[2][2][2];
+  int s = 0;
+  for (int t = lid; t < ntiles; t += G) {
+    pp_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    const bool more = t + G < ntiles;
+    int tm2 = tm, tn2 = tn;
+    if (more) pp_tile(t + G, tiles_m, tiles_n, g.group_m, tm2, tn2);
+    // K-tile kt's DMA carries K-tile kt + 1, or the next tile's K-tile 0 after the last one.
+    // K-tile 0 is peeled (its MFMAs start the accumulators from zero): no path reaches an
+    // accumulating body without passing it, so the accumulators are dead after the epilogue
+    {
+      const bool last = S == 1;
+      pp_ktile<true, EPI>(c, acc, fa, fb, smem, s, last ? tm2 : tm, last ? tn2 : tn, last ? 0 : 1, !last || more);
+      ++s;
+    }
+    for (int kt = 1; kt < S; ++kt, ++s) {
+      const bool last = kt + 1 == S;
+      pp_ktile<false, EPI>(c, acc, fa, fb, smem, s, last ? tm2 : tm, last ? tn2 : tn, last ? 0 : kt + 1,
+                           !last || more);
+    }
+    // the epilogue runs in this wave's next LOAD slot: beside the partner group's MFMAs
+    pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
+  }
+  if (c.wr == 0) pp_barrier();  // balance the stagger
+}
+
+}  // namespace
+
+namespace pllm {
+
+void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
+  const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + PT - 1) / PT);
+  if (ntiles == 0) return;
+  const int grid = ntiles < ctas ? ntiles : ctas;
+  switch (epi) {
+    case 0: hipLaunchKernelGGL((gemm_pp_kernel<0>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 1: hipLaunchKernelGGL((gemm_pp_kernel<1>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((gemm_pp_kernel<2>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 3: hipLaunchKernelGGL((gemm_pp_kernel<3>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((gemm_pp_kernel<4>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 5: hipLaunchKernelGGL((gemm_pp_kernel<5>), dim3(grid), dim3(PNT), 0, st, a); break;
+    default: hipLaunchKernelGGL((gemm_pp_kernel<6>), dim3(grid), dim3(PNT), 0, st, a); break;
+  }
+}
+
+}  // namespace pllm

@@ -119,7 +119,10 @@ struct GemmArgs {
   int T;         // epilogue 6: rows per sequence
 };
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
-void gemm_set_config(int mfma, int group_m, int phased);  // phased: 0 single-phase, 1 gemm_tn_ph_kernel, 2 asym DMA
+// phased: 0 single-phase, 2 asym DMA, 4 ping-pong kernel (gemm_pp.hip); reserve_cus >= 0: CUs left
+// free by the persistent grids (collectives in flight), -1 keeps the current setting
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1);
+void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
 int gemm_colsum_groups(int M);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
 void wgrad_plan(int M, int P, int Q, int* S, int* slice);

@@ -37,8 +37,11 @@ SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192), 
           (16640, 1032, 320)]
 
 
-@pytest.mark.parametrize("phased", [0, 2])
-@pytest.mark.parametrize("mf", [32, 16])
+# phased 4 = the ping-pong kernel (csrc/gemm_pp.hip; its MFMA shape is fixed, mf is ignored)
+KERNELS = [(16, 0), (32, 0), (16, 2), (32, 2), (16, 4)]
+
+
+@pytest.mark.parametrize("mf,phased", KERNELS)
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
     torch.manual_seed(3)
@@ -67,8 +70,7 @@ def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
         torch.ops.pllm.gemm_set_config(16, 4, 0)
 
 
-@pytest.mark.parametrize("phased", [0, 2])
-@pytest.mark.parametrize("mf", [32, 16])
+@pytest.mark.parametrize("mf,phased", KERNELS)
 @pytest.mark.parametrize("M,N,K", SHAPES)
 @pytest.mark.parametrize("f32_bias_grad", [True, False])
 def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad, phased):
@@ -156,9 +158,9 @@ def _silu(x):
     return x * torch.sigmoid(x)
 
 
-@pytest.mark.parametrize("mf", [32, 16])
+@pytest.mark.parametrize("mf,phased", [(32, 0), (16, 0), (16, 4)])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 768), (300, 520, 128), (777, 264, 192), (4160, 1376, 256)])
-def test_gemm_tn_swiglu_backward_epilogue(M, N, K, mf):
+def test_gemm_tn_swiglu_backward_epilogue(M, N, K, mf, phased):
     """epi 5: [dgate | dup] = swiglu'([gate | up], dy W2) in the data-gradient GEMM's epilogue
     vs fp32 math on the bf16-rounded data gradient (what swiglu_bwd_kernel reads)."""
     torch.manual_seed(7)
@@ -169,7 +171,7 @@ def test_gemm_tn_swiglu_backward_epilogue(M, N, K, mf):
     g, u = gu.float()[:, :N], gu.float()[:, N:]
     sg = torch.sigmoid(g)
     ref = torch.cat([d * u * sg * (1 + g * (1 - sg)), d * _silu(g)], dim=1)
-    torch.ops.pllm.gemm_set_config(mf, 4, 0)
+    torch.ops.pllm.gemm_set_config(mf, 4, phased)
     try:
         out, aux = torch.ops.pllm.gemm_tn(dy, wt, None, 5, gu)
         assert out.shape == (M, 2 * N) and aux.numel() == 0
@@ -214,8 +216,9 @@ def test_fused_swiglu_mlp_matches_unfused():
         assert _rel(a, b) < 1e-2, (n, _rel(a, b))
 
 
+@pytest.mark.parametrize("phased", [0, 4])
 @pytest.mark.parametrize("B,T,H", [(2, 256, 12), (3, 200, 4), (1, 1024, 16)])
-def test_gemm_tn_attn_delta_epilogue(B, T, H):
+def test_gemm_tn_attn_delta_epilogue(B, T, H, phased):
     """epi 6: dO = dy W_o (as epi 0, bitwise) plus delta[b, h, t] = sum_d dO * O per 64-wide head,
     against fp64 math on the bf16 dO (what attn_bwd_pre_kernel reads)."""
     torch.manual_seed(19)
@@ -224,12 +227,16 @@ def test_gemm_tn_attn_delta_epilogue(B, T, H):
     dy = (0.5 * torch.randn(M, C, device=DEV)).bfloat16()
     wt = (torch.randn(C, C, device=DEV) / C ** 0.5).bfloat16()  # W_o^T shadow [H*D, C_out]
     o = torch.randn(M, C, device=DEV).bfloat16()
-    do, delta = torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)
-    assert delta.shape == (B, H, T) and delta.dtype == torch.float32
-    assert torch.equal(do, torch.ops.pllm.gemm_tn(dy, wt, None, 0)[0])
-    ref = (do.double() * o.double()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
-    assert _rel(delta.double(), ref) < 1e-6, _rel(delta.double(), ref)
-    assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)[1], delta)  # deterministic
+    torch.ops.pllm.gemm_set_config(16, 4, phased)
+    try:
+        do, delta = torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)
+        assert delta.shape == (B, H, T) and delta.dtype == torch.float32
+        assert torch.equal(do, torch.ops.pllm.gemm_tn(dy, wt, None, 0)[0])
+        ref = (do.double() * o.double()).view(B, T, H, 64).sum(-1).permute(0, 2, 1)
+        assert _rel(delta.double(), ref) < 1e-6, _rel(delta.double(), ref)
+        assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)[1], delta)  # deterministic
+    finally:
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
 
 
 @pytest.mark.parametrize("bias", [True, False])
@@ -267,3 +274,44 @@ def test_attn_proj_fused_matches_unfused(bias, ext):
             continue
         assert a is not None, n
         assert _rel(a, c) < 1e-2, (n, _rel(a, c))
+
+
+@pytest.mark.parametrize("phased", [0, 4])
+@pytest.mark.parametrize("reserve", [0, 32, 240])
+def test_gemm_tn_reserved_cus(phased, reserve):
+    """reserve_cus caps the persistent grid (CUs left to RCCL kernels during an overlapped backward):
+    more tiles per workgroup, the same result bit for bit."""
+    torch.manual_seed(29)
+    M, N, K = 4096, 2304, 768
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    torch.ops.pllm.gemm_set_config(16, 4, phased, 0)
+    try:
+        ref = torch.ops.pllm.gemm_tn(a, b, bias, 1)
+        torch.ops.pllm.gemm_set_config(16, 4, phased, reserve)
+        out = torch.ops.pllm.gemm_tn(a, b, bias, 1)
+        assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
+        assert _rel(out[1], a.float() @ b.float().t() + bias.float()) < 5e-3
+    finally:
+        torch.ops.pllm.gemm_set_config(16, 4, 0, 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(65536, 768, 768), (65536, 3072, 768), (8192, 2304, 3072)])
+def test_gemm_pp_large_shapes(M, N, K):
+    """The ping-pong kernel at training shapes (many tiles per workgroup) vs fp32 math and vs the
+    round-3 kernel (same bf16 rounding: identical up to fp32 summation order)."""
+    torch.manual_seed(31)
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    try:
+        torch.ops.pllm.gemm_set_config(16, 4, 4)
+        out = torch.ops.pllm.gemm_tn(a, b, None, 0)[0]
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        old = torch.ops.pllm.gemm_tn(a, b, None, 0)[0]
+    finally:
+        torch.ops.pllm.gemm_set_config(16, 4, 0)
+    rows = torch.randint(0, M, (512,), device=DEV)
+    ref = a[rows].float() @ b.float().t()
+    assert _rel(out[rows], ref) < 5e-3
+    assert (out.float() - old.float()).abs().max().item() <= 2 ** -6 * old.float().abs().max().item()
