@@ -33,6 +33,20 @@
 #include "common.h"
 #include "kernels.h"
 
+// Ablation builds (scripts/build_variant.py gemm_pp.hip x.so -DPLLM_PP_EXP=n; numerics WRONG):
+// bit 0: the epilogue computes but stores nothing; bit 1: the main loop issues no DMA (stale LDS);
+// bit 2: non-temporal stores; bit 3: sc1 (write-through, line dropped from L2) stores; bit 4: the
+// waits of the two K-tiles after an epilogue leave its stores outstanding (races the DMA: timing
+// only); bit 5: odd workgroups sleep ~half a tile before starting (desynchronised epilogues);
+// bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third tile, 6 points per phase, and
+// its second epilogue) written over the start of C (diagnostic: bench/gemm_pp_stamps.py).
+#ifndef PLLM_PP_EXP
+#define PLLM_PP_EXP 0
+#endif
+constexpr bool kPPStamps = (PLLM_PP_EXP & 64) != 0;
+constexpr bool kPPStaticPrio = (PLLM_PP_EXP & 128) != 0;  // bit 7: waves 4-7 at priority 1, no flips
+constexpr int kPPStampN = 52;  // per wave
+
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -72,7 +86,11 @@ template <int EPI>
 constexpr int kPPEpiStores = (EPI == 5 || EPI == 1) ? 32 : 16;
 
 PLLM_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
-  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
+  if constexpr (PLLM_PP_EXP & 1) {
+    asm volatile("" ::"v"(v), "v"(off));
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, (PLLM_PP_EXP & 4) ? 2 : (PLLM_PP_EXP & 8) ? 16 : 0);
+  }
 }
 PLLM_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
 PLLM_DEV float pp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
@@ -248,38 +266,56 @@ struct PPCtx {
   const pllm::GemmArgs* g;
   int w, wr, wc, lane;
   unsigned lds;           // byte address of the LDS array
-  uint32_t vA[2], vB[2];  // per-lane DMA source offsets, even / odd piece
+  bool stamp;             // kPPStamps: this workgroup records
+  uint64_t* stamp_at;     // kPPStamps: this wave's stamp area (in the LDS array)
+  uint32_t vo[4][2];      // per-lane DMA source offsets of this wave's 8 pieces (group, piece)
   unsigned rdA[2], rdB[2];  // per-lane LDS byte offsets of the fragment reads (k32 = 0, 1), slot 0
 };
 
-// DMA of piece group PH (2 pieces per wave) of K-tile kt of tile (tm, tn) into LDS slot sl.
-// PH 0: A rows 0-63 of both row halves, 1: B image rows of column pair 0 of every wave,
-// 2: B column pair 1, 3: A rows 64-127 of both halves.  valid = false: zero-range descriptors
-// (same instruction count, so the counted waits stay exact; nothing reads that slot again).
-template <int PH>
-PLLM_DEV void pp_issue(const PPCtx& c, int tm, int tn, int kt, int sl, bool valid) {
-  // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
-  const pllm::GemmArgs& g = *c.g;
-  constexpr bool isA = PH == 0 || PH == 3;
-  const int w = c.w;
-  const int blk0 = PH == 0 ? 2 * w + 8 * (w >> 2)
-                   : PH == 3 ? 8 + 2 * w + 8 * (w >> 2)
-                   : PH == 1 ? 8 * (w >> 1) + 2 * (w & 1)
-                             : 4 + 8 * (w >> 1) + 2 * (w & 1);
-  const int64_t ld = isA ? g.lda : g.ldb;
-  const int rows_ok = isA ? min(PT, g.M - tm * PT) : min(PT, g.N - tn * PT);
-  const uint16_t* base = (isA ? g.A + (int64_t)tm * PT * g.lda : g.B + (int64_t)tn * PT * g.ldb) + kt * PBK;
-  const int kleft2 = (g.K - kt * PBK) * 2;
-  const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG)) * 2u;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int blk = blk0 + q;
-    const int prow0 = isA ? 8 * blk : 32 * (blk >> 2) + 16 * (blk & 1) + 4 * ((blk >> 1) & 1);
-    const int left = rows_ok - prow0;
-    const uint32_t bytes = (valid && left > 0) ? (uint32_t)((int64_t)(left - 1) * ld * 2 + kleft2) : 0u;
-    const i32x4v srd = srd_of(base + (int64_t)prow0 * ld, bytes);
-    blds16(srd, isA ? c.vA[q] : c.vB[q], lds0 + 1024u * (unsigned)blk);
+PLLM_DEV void pp_stamp(const PPCtx& c, int idx) {
+  if constexpr (kPPStamps) {
+    if (c.stamp && idx >= 0) {
+      const uint64_t t = __builtin_amdgcn_s_memtime();
+      if (c.lane == 0) c.stamp_at[idx] = t;
+    }
   }
+}
+
+// Descriptors of the DMA target K-tile's A and B panels (256 rows from the K-tile's first column,
+// range-checked: rows past M / N read zeros); valid = false: empty ranges (the same instructions
+// issue, so the counted waits stay exact; nothing reads that slot again).  Built once per K-tile:
+// the pieces differ only in their per-lane offsets (PPCtx::vo), which hold the row.
+struct PPSrd {
+  i32x4v a, b;
+};
+PLLM_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
+  const pllm::GemmArgs& g = *c.g;
+  const int ra = min(PT, g.M - tm * PT), rb = min(PT, g.N - tn * PT);
+  const int64_t kleft2 = (int64_t)(g.K - kt * PBK) * 2;
+  const uint32_t ba = valid ? (uint32_t)((int64_t)(ra - 1) * g.lda * 2 + kleft2) : 0u;
+  const uint32_t bb = valid ? (uint32_t)((int64_t)(rb - 1) * g.ldb * 2 + kleft2) : 0u;
+  return {srd_of(g.A + (int64_t)tm * PT * g.lda + kt * PBK, ba), srd_of(g.B + (int64_t)tn * PT * g.ldb + kt * PBK, bb)};
+}
+
+// DMA piece group PH (2 pieces per wave) of the target K-tile into LDS slot sl, in the order of
+// first use: 0 = B image rows of column pair 0 of every wave (read in the PREVIOUS K-tile's
+// phase 3), 1 = A rows 0-63 of both row halves, 2 = B column pair 1, 3 = A rows 64-127.
+template <int PH>
+PLLM_DEV int pp_blk0(int w) {
+  return PH == 0 ? 8 * (w >> 1) + 2 * (w & 1)
+         : PH == 1 ? 2 * w + 8 * (w >> 2)
+         : PH == 2 ? 4 + 8 * (w >> 1) + 2 * (w & 1)
+                   : 8 + 2 * w + 8 * (w >> 2);
+}
+template <int PH>
+PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
+  // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
+  constexpr bool isA = PH == 1 || PH == 3;
+  const int blk0 = pp_blk0<PH>(c.w);
+  const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG) + blk0 * 512) * 2u;
+  if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
+#pragma unroll
+  for (int q = 0; q < 2; ++q) blds16(isA ? srd.a : srd.b, c.vo[PH][q], lds0 + 1024u * (unsigned)q);
 }
 
 // One phase of a K-tile: the LOAD segment (fragment reads for this phase's quadrant, the next
@@ -288,11 +324,13 @@ PLLM_DEV void pp_issue(const PPCtx& c, int tm, int tn, int kt, int sl, bool vali
 // phases of a tile).
 template <int PH, bool FIRST, int VM>
 PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
-                       const uint16_t* slotp, int ntm, int ntn, int nkt, int nsl, bool nvalid) {
+                       const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl, int sk) {
   const int wr = c.wr, wc = c.wc;
-  const char* sb = reinterpret_cast<const char*>(slotp);
-  // ---- LOAD segment
+  const int st0 = sk < 0 ? -1 : 24 * sk + 6 * PH;  // stamp indices of this phase (kPPStamps)
+  pp_stamp(c, st0);
+  // ---- LOAD segment: 8 / 4 / 8 / 4 fragment reads (PH 3 reads the NEXT K-tile's column pair 0)
   if constexpr (PH == 0 || PH == 2) {
+    const char* sb = reinterpret_cast<const char*>(slotp);
     const int jh = PH == 0 ? 0 : 1;
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -300,9 +338,9 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
       for (int jj = 0; jj < 4; ++jj)
         fa[k][jj] = ldsf(reinterpret_cast<const uint16_t*>(
             sb + c.rdA[k] + (unsigned)((wr * 128 + 16 * (4 * jh + jj)) * PBK * 2)));
-  }
-  if constexpr (PH == 0 || PH == 1) {
-    const int p = PH;
+  } else {
+    const char* sb = reinterpret_cast<const char*>(PH == 1 ? slotp : nslotp);
+    const int p = PH == 1 ? 1 : 0;
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -310,14 +348,18 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
         fb[p][k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
             sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
   }
-  pp_issue<PH>(c, ntm, ntn, nkt, nsl, nvalid);
+  pp_stamp(c, st0 < 0 ? -1 : st0 + 1);
+  pp_issue<PH>(c, srd, nsl);
+  pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
   pp_vmwait<VM>();
+  pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
   pp_barrier();
-  // ---- MFMA segment: quadrant (rows half jh, column pair p)
+  pp_stamp(c, st0 < 0 ? -1 : st0 + 4);
+  // ---- MFMA segment: quadrant (rows half jh, column pair p): (0,0) (0,1) (1,0) (1,1)
   {
     constexpr int jh = PH >= 2 ? 1 : 0;
-    constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
-    __builtin_amdgcn_s_setprio(1);
+    constexpr int p = PH & 1;
+    if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -328,8 +370,9 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
           if (FIRST && k == 0) a = mfma16(fb[p][k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
           else a = mfma16(fb[p][k][ii], fa[k][jj], a);
         }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(0);
   }
+  pp_stamp(c, st0 < 0 ? -1 : st0 + 5);
   pp_barrier();
 }
 
@@ -338,17 +381,23 @@ PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
                        const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid) {
   const uint16_t* slotp = smem + (s & 1) * PSLOT;
   const int nsl = (s + 1) & 1;
+  const uint16_t* nslotp = smem + nsl * PSLOT;
+  const PPSrd srd = pp_srds(c, ntm, ntn, nkt, nvalid);  // the DMA carries the next K-tile
   constexpr int VE = FIRST ? 4 + kPPEpiStores<EPI> : 4;
-  pp_phase<0, FIRST, VE>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
-  pp_phase<1, FIRST, VE>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
-  pp_phase<2, FIRST, 4>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
-  pp_phase<3, FIRST, 4>(c, acc, fa, fb, slotp, ntm, ntn, nkt, nsl, nvalid);
+  constexpr int VL = (PLLM_PP_EXP & 16) && FIRST ? VE : 4;
+  // kPPStamps: the third tile's K-tile 0 (right after an epilogue) and its K-tile S / 2
+  const int S = c.g->K / PBK;
+  const int sk = !kPPStamps ? -1 : s == 2 * S ? 0 : s == 2 * S + S / 2 ? 1 : -1;
+  pp_phase<0, FIRST, VE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
+  pp_phase<1, FIRST, VE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
+  pp_phase<2, FIRST, VL>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
+  pp_phase<3, FIRST, VL>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
 }
 
 template <int EPI>
 __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads)
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT];
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
   const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + PT - 1) / PT, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
@@ -361,14 +410,30 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   c.wc = c.w & 3;
   c.lane = lane;
   c.lds = (unsigned)(uintptr_t)smem;
+  c.stamp = kPPStamps && blockIdx.x == 0;
+  c.stamp_at = reinterpret_cast<uint64_t*>(smem + 2 * PSLOT) + kPPStampN * c.w;
+  {
+    // per-lane source offsets of this wave's pieces: lane l of piece blk fills image row
+    // 8 * blk + l / 8 at 16-B position l % 8, which holds logical chunk (l % 8) ^ swz(row),
+    // swz(row) = (row >> 1) & 7 = (4 * (blk & 1) + l / 16) & 7; B image rows are permuted inside
+    // each 32-row block (image row 16h + 4g + r <- column 8g + 4h + r)
+    const int prow = 8 * ((lane >> 5) & 1) + ((lane >> 3) & 3);  // B permutation, per-lane part
+    auto voA = [&](int blk) {
+      const int ch = (lane & 7) ^ ((4 * (blk & 1) + (lane >> 4)) & 7);
+      return (uint32_t)(((int64_t)(8 * blk + (lane >> 3)) * g.lda + ch * 8) * 2);
+    };
+    auto voB = [&](int blk) {
+      const int ch = (lane & 7) ^ ((4 * (blk & 1) + (lane >> 4)) & 7);
+      const int row = 32 * (blk >> 2) + 16 * (blk & 1) + 4 * ((blk >> 1) & 1) + prow;
+      return (uint32_t)(((int64_t)row * g.ldb + ch * 8) * 2);
+    };
 #pragma unroll
-  for (int par = 0; par < 2; ++par) {
-    // lane l of a piece fills image row 8 * blk + l / 8 at 16-B position l % 8, which holds
-    // logical chunk (l % 8) ^ swz(row), swz(row) = (row >> 1) & 7 = (4 * (blk & 1) + l / 16) & 7
-    const int ch = (lane & 7) ^ ((4 * par + (lane >> 4)) & 7);
-    c.vA[par] = (uint32_t)(((int64_t)(lane >> 3) * g.lda + ch * 8) * 2);
-    const int prow = 8 * ((lane >> 5) & 1) + ((lane >> 3) & 3);  // B column permutation, per-lane part
-    c.vB[par] = (uint32_t)(((int64_t)prow * g.ldb + ch * 8) * 2);
+    for (int q = 0; q < 2; ++q) {
+      c.vo[0][q] = voB(pp_blk0<0>(c.w) + q);
+      c.vo[1][q] = voA(pp_blk0<1>(c.w) + q);
+      c.vo[2][q] = voB(pp_blk0<2>(c.w) + q);
+      c.vo[3][q] = voA(pp_blk0<3>(c.w) + q);
+    }
   }
   {
     // fragment reads: image row (16-aligned base) + r16, chunk 4 k32 + g, swizzled by (r16 >> 1) & 7
@@ -381,20 +446,40 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     }
   }
   const int S = g.K / PBK;
+  if constexpr ((PLLM_PP_EXP & 32) != 0) {
+    if (lid & 1)
+      for (int i = 0; i < S * 24; ++i) __builtin_amdgcn_s_sleep(63);  // ~1.5k cycles per K-tile
+  }
   int tm, tn;
   pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
   // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
-  pp_issue<0>(c, tm, tn, 0, 0, true);
-  pp_issue<1>(c, tm, tn, 0, 0, true);
-  pp_issue<2>(c, tm, tn, 0, 0, true);
-  pp_issue<3>(c, tm, tn, 0, 0, true);
+  {
+    const PPSrd srd = pp_srds(c, tm, tn, 0, true);
+    pp_issue<0>(c, srd, 0);
+    pp_issue<1>(c, srd, 0);
+    pp_issue<2>(c, srd, 0);
+    pp_issue<3>(c, srd, 0);
+  }
   pp_vmwait<0>();
   pp_barrier();
   if (c.wr == 1) pp_barrier();  // the stagger: rows 128-255 run one barrier behind rows 0-127
+  if constexpr (kPPStaticPrio) {
+    if (c.wr == 1) __builtin_amdgcn_s_setprio(1);  // the younger half keeps priority (no flips)
+  }
 
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
   bf16x8 fb[2][2][2];
+  {
+    // K-tile 0's column pair 0 (every later K-tile's is read in its predecessor's phase 3)
+    const char* sb = reinterpret_cast<const char*>(smem);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+        fb[0][k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
+            sb + c.rdB[k] + (unsigned)((PIMG + (c.wc * 64 + 16 * ii) * PBK) * 2)));
+  }
   int s = 0;
   for (int t = lid; t < ntiles; t += G) {
     pp_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
@@ -415,9 +500,23 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
                            !last || more);
     }
     // the epilogue runs in this wave's next LOAD slot: beside the partner group's MFMAs
+    const bool st_epi = kPPStamps && t == lid + G;  // the second tile's epilogue
+    pp_stamp(c, st_epi ? 48 : -1);
     pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
+    pp_stamp(c, st_epi ? 49 : -1);
   }
   if (c.wr == 0) pp_barrier();  // balance the stagger
+  if constexpr (kPPStamps) {
+    if (c.stamp) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void*)g.C, (short)0, 1 << 30, 0x00020000);
+      if (lane < kPPStampN) {
+        const uint64_t v = c.stamp_at[lane];
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), crs,
+                                              (uint32_t)((c.w * kPPStampN + lane) * 8), 0, 0);
+      }
+    }
+  }
 }
 
 }  // namespace

@@ -25,6 +25,9 @@ _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO_PATH = os.environ.get("PLLM_SO") or os.path.join(_HERE, "_C.so")  # PLLM_SO: A/B builds
 
 _lock = threading.Lock()
+# fused-epilogue TN GEMM main loops (gemm_set_config's `phased`): csrc/gemm_pp.hip's ping-pong
+# kernel, csrc/gemm.hip's round-3 persistent kernel
+GEMM_KERNELS = {"pp": 4, "r3": 0}
 _loaded = False
 _err: str | None = None
 
@@ -46,6 +49,13 @@ def load(raise_on_error: bool = False) -> bool:
                 # PLLM_WGRAD_VARIANT: weight-gradient kernel variant for A/B runs (csrc/gemm_wgrad.hip)
                 if os.environ.get("PLLM_WGRAD_VARIANT"):
                     torch.ops.pllm.wgrad_set_mfma(int(os.environ["PLLM_WGRAD_VARIANT"]))
+                # PLLM_GEMM_KERNEL=pp|r3: main loop of the fused-epilogue TN GEMM (ops.gemm_config);
+                # PLLM_GEMM_RESERVE_CUS=n: CUs its persistent grid leaves to concurrent RCCL kernels
+                kern = os.environ.get("PLLM_GEMM_KERNEL")
+                res = os.environ.get("PLLM_GEMM_RESERVE_CUS")
+                if kern or res:
+                    torch.ops.pllm.gemm_set_config(0, 0, GEMM_KERNELS.get(kern, -1) if kern else -1,
+                                                   int(res) if res else -1)
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box
