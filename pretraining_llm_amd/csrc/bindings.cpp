@@ -290,7 +290,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     check_aligned16(*aux, "aux");
     g.aux = (uint16_t*)aux->data_ptr();
     g.ldaux = aux->stride(0);
-    part = at::empty({pllm::gemm_colsum_groups((int)M), N}, a.options().dtype(at::kFloat));
+    part = at::empty({pllm::gemm_colsum_groups((int)M, (int)K), N}, a.options().dtype(at::kFloat));
     g.colpart = part.data_ptr<float>();
   }
   bool of32 = false;
@@ -302,7 +302,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   if (M > 0) {
     pllm::gemm_tn(g, (int)epi, cur_stream());
     if (bias_acc)
-      pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M), (int)N, bias_acc->data_ptr(), of32, true,
+      pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M, (int)K), (int)N, bias_acc->data_ptr(), of32, true,
                        cur_stream());
   }
   return {out, aux_out};  // a (Tensor, Tensor) tuple: functionalization rejects Tensor[] beside an (a!) arg

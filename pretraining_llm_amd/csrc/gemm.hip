@@ -405,7 +405,13 @@ void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus) {
   if (reserve_cus >= 0) g_gemm_reserve = reserve_cus;
 }
 
-int gemm_colsum_groups(int M) { return 2 * ((M + GT - 1) / GT); }
+// column-sum partial rows of the EPI 3 / 4 bias gradient: 2 per tile row here, 4 (one per
+// accumulator quadrant row half and wave row) in the ping-pong kernel's quadrant epilogues
+// the ping-pong kernel serves a call when selected, with >= 2 K-tiles and (epilogue 6) 16 | T
+bool gemm_uses_pp(int K, int epi, int T) { return g_gemm_phased == 4 && K >= 128 && (epi != 6 || T % 16 == 0); }
+int gemm_colsum_groups(int M, int K) {
+  return gemm_uses_pp(K, 3, 0) ? gemm_pp_colsum_groups(M) : 2 * ((M + GT - 1) / GT);
+}
 
 static int num_cus() {
   static int n = 0;
@@ -424,7 +430,7 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
   if (ntiles == 0) return;
   // persistent grid: one workgroup per CU, minus the CUs reserved for concurrent collectives
   const int ctas = num_cus() - g_gemm_reserve > 8 ? num_cus() - g_gemm_reserve : 8;
-  if (g_gemm_phased == 4) {
+  if (gemm_uses_pp(a.K, epi, a.T)) {
     gemm_tn_pp(a, epi, ctas, st);
     return;
   }

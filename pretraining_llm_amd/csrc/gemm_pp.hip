@@ -28,18 +28,24 @@
 //  * the B image rows are permuted inside each 32-row block (image row 16h + 4g + r <- column
 //    8g + 4h + r) so that the accumulators of column tiles 2p and 2p+1 hold 8 CONSECUTIVE output
 //    columns per lane: the epilogue stores 16 B per lane straight from registers (no LDS round
-//    trip), with bias / GELU / ReLU / GELU' / ReLU' / SwiGLU' / attention-delta math on the way.
+//    trip), with bias / GELU / ReLU / GELU' / ReLU' / SwiGLU' / attention-delta math on the way;
+//  * the epilogue is NOT a burst at the end of a tile (measured: 128 KiB of stores per CU, issued
+//    by every CU at once, parked both wave groups ~4.5k cycles per tile -- 20 % of the kernel at
+//    K = 768): the previous tile's epilogue runs one accumulator QUADRANT per phase inside the
+//    next tile's first K-tile, each quadrant just before that phase's MFMAs overwrite it; its
+//    bias / aux rows come through a per-wave 4 KiB LDS area by DMA issued one phase ahead, and
+//    every wait is a count that leaves the stores outstanding (no load of the main loop is issued
+//    by the compiler, so no compiler wait drains them).  EPI 5 (SwiGLU backward, 8 KiB of aux per
+//    wave and quadrant) keeps the end-of-tile epilogue.
 // Requires K % 64 == 0, N % 8 == 0, lda / ldc / ldaux % 8 == 0 (checked by the binding).
 #include "common.h"
 #include "kernels.h"
 
 // Ablation builds (scripts/build_variant.py gemm_pp.hip x.so -DPLLM_PP_EXP=n; numerics WRONG):
 // bit 0: the epilogue computes but stores nothing; bit 1: the main loop issues no DMA (stale LDS);
-// bit 2: non-temporal stores; bit 3: sc1 (write-through, line dropped from L2) stores; bit 4: the
-// waits of the two K-tiles after an epilogue leave its stores outstanding (races the DMA: timing
-// only); bit 5: odd workgroups sleep ~half a tile before starting (desynchronised epilogues);
-// bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third tile, 6 points per phase, and
-// its second epilogue) written over the start of C (diagnostic: bench/gemm_pp_stamps.py).
+// bit 2: non-temporal stores; bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third
+// tile, 6 points per phase) written over the start of C (diagnostic: bench/gemm_pp_stamps.py);
+// bit 7: waves 4-7 at static priority 1 instead of per-segment flips.
 #ifndef PLLM_PP_EXP
 #define PLLM_PP_EXP 0
 #endif
@@ -80,16 +86,26 @@ PLLM_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn)
   tn = (t % per_group) / gsize;
 }
 
-// the epilogue's vector-memory instructions issued after its last wait (its C / aux stores):
-// a lower bound is what the counted waits of the next tile's first two phases need
+// EPI 5's end-of-tile epilogue: the vector-memory instructions it issues after its last wait
+// (its stores); a lower bound is what the counted waits of the next tile's first phases need
+constexpr int kPPEpi5Stores = 32;
+// quadrant epilogues (every EPI but 5): DMA ops of the bias / aux rows of one quadrant, and the
+// stores of one quadrant epilogue (C, the EPI 1 pre-activation, the EPI 3 / 4 column-sum
+// partials, the EPI 6 delta on the second column pair)
 template <int EPI>
-constexpr int kPPEpiStores = (EPI == 5 || EPI == 1) ? 32 : 16;
+constexpr bool kQuadEpi = EPI != 5;
+template <int EPI>
+constexpr int kAuxN = EPI <= 2 ? 1 : 4;
+template <int EPI>
+constexpr int kStQ(int q) {
+  return EPI == 1 ? 8 : (EPI == 3 || EPI == 4) ? 6 : EPI == 6 ? ((q & 1) ? 8 : 4) : 4;
+}
 
 PLLM_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
   if constexpr (PLLM_PP_EXP & 1) {
     asm volatile("" ::"v"(v), "v"(off));
   } else {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, (PLLM_PP_EXP & 4) ? 2 : (PLLM_PP_EXP & 8) ? 16 : 0);
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, (PLLM_PP_EXP & 4) ? 2 : 0);
   }
 }
 PLLM_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
@@ -261,15 +277,24 @@ PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, i
   }
 }
 
+
 // ---------------------------------------------------------------------------------------------
 struct PPCtx {
   const pllm::GemmArgs* g;
   int w, wr, wc, lane;
   unsigned lds;           // byte address of the LDS array
+  uint16_t* aux;          // this wave's 4 KiB bias / aux staging area (after the two K-tile slots)
   bool stamp;             // kPPStamps: this workgroup records
   uint64_t* stamp_at;     // kPPStamps: this wave's stamp area (in the LDS array)
-  uint32_t vo[4][2];      // per-lane DMA source offsets of this wave's 8 pieces (group, piece)
+  uint32_t vo[2][2];      // per-lane DMA source offsets of this wave's pieces of groups 0 (A) / 1 (B)
+                          // (groups 3 / 2 are the same rows + 64 (A) / + 32 (B): descriptor base)
+  uint32_t vaux;          // per-lane source offset of the aux DMA (row lane / 4, 16-B chunk lane % 4)
   unsigned rdA[2], rdB[2];  // per-lane LDS byte offsets of the fragment reads (k32 = 0, 1), slot 0
+};
+
+struct PPEpi {  // the tile whose (quadrant) epilogue is in flight
+  int tm, tn;
+  bool valid;   // false: the kernel's first tile has no predecessor (stores go nowhere)
 };
 
 PLLM_DEV void pp_stamp(const PPCtx& c, int idx) {
@@ -298,67 +323,298 @@ PLLM_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
 }
 
 // DMA piece group PH (2 pieces per wave) of the target K-tile into LDS slot sl, in the order of
-// first use: 0 = B image rows of column pair 0 of every wave (read in the PREVIOUS K-tile's
-// phase 3), 1 = A rows 0-63 of both row halves, 2 = B column pair 1, 3 = A rows 64-127.
+// first use: 0 = A rows 0-63 of both row halves, 1 = B image rows of column pair 0 of every wave,
+// 2 = B column pair 1, 3 = A rows 64-127 (distances to first use: 4, 3, 3, 3 phases).
 template <int PH>
 PLLM_DEV int pp_blk0(int w) {
-  return PH == 0 ? 8 * (w >> 1) + 2 * (w & 1)
-         : PH == 1 ? 2 * w + 8 * (w >> 2)
+  return PH == 0 ? 2 * w + 8 * (w >> 2)
+         : PH == 1 ? 8 * (w >> 1) + 2 * (w & 1)
          : PH == 2 ? 4 + 8 * (w >> 1) + 2 * (w & 1)
                    : 8 + 2 * w + 8 * (w >> 2);
+}
+// shift a descriptor's base by `bytes` (its range shrinks by as much, clamped at 0)
+PLLM_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
+  const uint64_t a = ((uint64_t)(uint32_t)r[1] << 32 | (uint32_t)r[0]) + bytes;
+  i32x4v o;  // (readfirstlane: the asm operand must provably live in SGPRs)
+  o[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  o[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
+  o[2] = __builtin_amdgcn_readfirstlane((uint32_t)r[2] > bytes ? (int)((uint32_t)r[2] - bytes) : 0);
+  o[3] = r[3];
+  return o;
 }
 template <int PH>
 PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
   // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
-  constexpr bool isA = PH == 1 || PH == 3;
+  constexpr bool isA = PH == 0 || PH == 3;
   const int blk0 = pp_blk0<PH>(c.w);
   const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG) + blk0 * 512) * 2u;
   if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
+  // groups 2 / 3: the pieces of groups 1 / 0 shifted by 4 (B: 32 rows) / 8 (A: 64 rows) pieces
+  const i32x4v r = PH < 2 ? (isA ? srd.a : srd.b)
+                          : srd_shift(isA ? srd.a : srd.b,
+                                      (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
 #pragma unroll
-  for (int q = 0; q < 2; ++q) blds16(isA ? srd.a : srd.b, c.vo[PH][q], lds0 + 1024u * (unsigned)q);
+  for (int q = 0; q < 2; ++q) blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
 }
 
-// One phase of a K-tile: the LOAD segment (fragment reads for this phase's quadrant, the next
-// K-tile's piece group PH, the counted wait), a barrier, the MFMA segment (16 MFMAs), a barrier.
-// VM: the vmcnt of the wait (4 in steady state; 4 + the epilogue's stores in the first two
-// phases of a tile).
-template <int PH, bool FIRST, int VM>
-PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
-                       const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl, int sk) {
+// ---------------------------------------------------------------------------------------------
+// Quadrant epilogues.  Quadrant q = (rows half jh, column pair p) = (0,0) (0,1) (1,1) (1,0) of a wave's
+// 128x64 tile: rows wr*128 + 16j + r16 (j = 4 jh .. 4 jh + 3), columns wc*64 + 32p + 8g + [0, 8)
+// (lane: r16 = lane & 15, g = lane >> 4; acc[2p][j] then acc[2p+1][j]).
+//
+// The quadrant's bias (EPI <= 2: its 32 columns, 64 B) or aux rows (EPI 3 / 4 / 6: 64 rows x 32
+// columns, 4 KiB) are DMA'd into the wave's own LDS area one phase ahead (kAuxN instructions);
+// only this wave reads it, so its own counted vmcnt orders the reads.
+// quadrant of phase q (snake order: one column-pair fragment set is re-read, not held)
+constexpr int pp_qjh(int q) { return q >> 1; }
+constexpr int pp_qp(int q) { return (q == 1 || q == 2) ? 1 : 0; }
+
+template <int EPI, int Q>
+PLLM_DEV void pp_aux_issue(const PPCtx& c, const PPEpi& e) {
+  const pllm::GemmArgs& g = *c.g;
+  constexpr int jh = pp_qjh(Q), p = pp_qp(Q);
+  const int col0 = e.tn * PT + c.wc * 64 + 32 * p;
+  const unsigned dst = (unsigned)(uintptr_t)c.aux;
+  if constexpr (EPI <= 2) {
+    const bool has = e.valid && g.bias != nullptr && col0 < g.N;
+    const i32x4v srd = srd_of(g.bias != nullptr ? g.bias + (has ? col0 : 0) : g.A, has ? (uint32_t)(g.N - col0) * 2u : 0u);
+    blds16(srd, c.lane < 4 ? (uint32_t)c.lane * 16u : kPOff, dst);  // lanes 0-3: 8 columns each
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int row0 = e.tm * PT + c.wr * 128 + 16 * (4 * jh + jj);
+      const bool has = e.valid && row0 < g.M && col0 < g.N;
+      const uint32_t bytes = has ? (uint32_t)((int64_t)(g.M - row0 - 1) * g.ldaux * 2 + (int64_t)(g.N - col0) * 2) : 0u;
+      const uint16_t* base = has ? g.aux + (int64_t)row0 * g.ldaux + col0 : g.C;
+      blds16(srd_of(base, bytes), c.vaux, dst + 1024u * (unsigned)jj);  // [jj][row 0..15][64 B]
+    }
+  }
+}
+
+// The epilogue of quadrant Q of tile e (its aux / bias already in the wave's LDS area and read
+// into ax).  EPI 6's delta needs both column pairs of a row: dsum carries pair 0's partial to
+// the pair-1 quadrant that follows it.  EPI 3 / 4 write the quadrant's column sums to colpart
+// row 4 tm + 2 wr + jh (gemm_colsum_groups = 4 per tile row with this kernel).
+template <int EPI, int Q>
+PLLM_DEV void pp_epi_quad(f32x4 (&acc)[4][8], const PPCtx& c, const PPEpi& e, const u32x4 (&ax)[4],
+                          float (&dsum)[4]) {
+  const pllm::GemmArgs& g = *c.g;
+  constexpr int jh = pp_qjh(Q), p = pp_qp(Q);
+  constexpr bool first_of_half = (Q & 1) == 0;  // EPI 6: the row half's first column pair
+  const int M = g.M, N = g.N;
+  const int m0 = e.tm * PT, n0 = e.tn * PT;
+  const int rows_ok = e.valid ? min(PT, M - m0) : 0;  // no predecessor: every store is dropped
+  const int lane = c.lane, r16 = lane & 15, g4 = lane >> 4;
+  const int col = n0 + c.wc * 64 + 32 * p + 8 * g4;
+  const bool ok = col < N;
+  // per row tile j a descriptor based at its first row (scalar), so the per-lane offsets are
+  // the same for every j: one VGPR each instead of eight hoisted row offsets (those spilled)
+  const uint32_t off = ok ? (uint32_t)(((int64_t)r16 * g.ldc + col) * 2) : kPOff;
+  const uint32_t aoff = ok ? (uint32_t)(((int64_t)r16 * g.ldaux + col) * 2) : kPOff;
+  float csum[8];
+#pragma unroll
+  for (int e2 = 0; e2 < 8; ++e2) csum[e2] = 0.f;
+#pragma unroll
+  for (int jj = 0; jj < 4; ++jj) {
+    const int j = 4 * jh + jj;
+    const int r0 = c.wr * 128 + 16 * j;  // first row of the row tile within the tile
+    const int rows_j = max(0, rows_ok - r0);
+    const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)(e.valid ? m0 + r0 : 0) * g.ldc, rows_j, g.ldc, N);
+    const __amdgpu_buffer_rsrc_t ars =
+        rows_rsrc(g.aux != nullptr ? g.aux + (int64_t)(e.valid ? m0 + r0 : 0) * g.ldaux : g.C, EPI == 1 ? rows_j : 0,
+                  g.ldaux, N);
+    float v[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = acc[2 * p][j][q];
+      v[4 + q] = acc[2 * p + 1][j][q];
+    }
+    float bias[8];
+    if constexpr (EPI <= 2) unpack8(ax[0], bias);  // (kept packed between row tiles)
+    if constexpr (EPI == 0) {
+      // (written as a max against an opaque -inf: the plain add made hipcc hoist and spill)
+      float lo = -INFINITY;
+      asm volatile("" : "+v"(lo));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q] + bias[q], lo);
+      pp_st16(crs, off, pack8(v));
+    } else if constexpr (EPI == 1) {
+      float lo = -INFINITY;  // (as EPI 0)
+      asm volatile("" : "+v"(lo));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q] + bias[q], lo);
+      const u32x4 pre = pack8(v);
+      float f[8];
+      unpack8(pre, f);  // the activation reads the bf16-rounded pre-activation
+#pragma unroll
+      for (int q = 0; q < 8; ++q) f[q] = gelu_f(f[q]);
+      pp_st16(ars, aoff, pre);
+      pp_st16(crs, off, pack8(f));
+    } else if constexpr (EPI == 2) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = fmaxf(v[q] + bias[q], 0.f);
+      pp_st16(crs, off, pack8(v));
+    } else if constexpr (EPI == 3 || EPI == 4) {
+      float a[8];
+      unpack8(ax[jj], a);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float d = bfr(v[q]);  // the unfused path's bf16 data gradient
+        v[q] = EPI == 3 ? d * gelu_df(a[q]) : (a[q] > 0.f ? d : 0.f);
+      }
+      const u32x4 o = pack8(v);
+      pp_st16(crs, off, o);
+      unpack8(o, v);  // the bias gradient sums the bf16-rounded values, like act_bwd_colsum
+#pragma unroll
+      for (int q = 0; q < 8; ++q) csum[q] += v[q];
+    } else {  // EPI 6: dO stored; delta = sum over the wave's 64 columns (one head) of dO * O
+      const u32x4 o = pack8(v);
+      pp_st16(crs, off, o);
+      float d[8], oo[8];
+      unpack8(o, d);
+      unpack8(ax[jj], oo);
+      float sum = first_of_half ? 0.f : dsum[jj];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sum = __builtin_fmaf(d[q], oo[q], sum);
+      dsum[jj] = sum;
+    }
+    __builtin_amdgcn_sched_barrier(0);  // one row tile at a time: bounded temporaries
+  }
+  if constexpr (EPI == 3 || EPI == 4) {
+    // lanes r16 = 0..15 of a lane group hold the same 8 columns (fixed butterfly order)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float t = csum[q];
+      t += __shfl_xor(t, 1, 64);
+      t += __shfl_xor(t, 2, 64);
+      t += __shfl_xor(t, 4, 64);
+      t += __shfl_xor(t, 8, 64);
+      csum[q] = t;
+    }
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.colpart + (int64_t)(4 * e.tm + 2 * c.wr + jh) * N), (short)0, e.valid ? N * 4 : 0, 0x00020000);
+    const uint32_t po = (ok && r16 == 0) ? (uint32_t)col * 4u : kPOff;
+    pp_st16(prs, po, __builtin_bit_cast(u32x4, f32x4{csum[0], csum[1], csum[2], csum[3]}));
+    pp_st16(prs, po == kPOff ? kPOff : po + 16u, __builtin_bit_cast(u32x4, f32x4{csum[4], csum[5], csum[6], csum[7]}));
+  }
+  if constexpr (EPI == 6 && !first_of_half) {
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(g.delta != nullptr ? g.delta : (float*)g.C), (short)0, e.valid ? (int)(4ll * M * N / 64) : 0,
+        0x00020000);
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      // the row's 4 lane groups (g = 0..3: lanes r16, r16 + 16, + 32, + 48) in a fixed order
+      float sum = dsum[jj];
+      sum += __shfl_xor(sum, 16, 64);
+      sum += __shfl_xor(sum, 32, 64);
+      // a 16-row tile never crosses a sequence (T % 16 == 0, checked by the dispatcher): the
+      // (batch, position) split of its first row is scalar, the lanes add their r16
+      const int mb = m0 + c.wr * 128 + 16 * (4 * jh + jj);
+      const int bq = mb / g.T, tq0 = mb - bq * g.T, hd = (n0 + c.wc * 64) >> 6;
+      const uint32_t doff = (g4 == 0 && mb + r16 < M && (n0 + c.wc * 64) < N)
+                                ? (uint32_t)((((int64_t)bq * (N >> 6) + hd) * g.T + tq0 + r16) * 4) : kPOff;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sum), drs, doff, 0, 0);
+    }
+  }
+}
+
+// read quadrant aux / bias out of the wave's LDS area (and make sure the reads have returned
+// before the next quadrant's DMA overwrites the area)
+template <int EPI>
+PLLM_DEV void pp_aux_read(const PPCtx& c, u32x4 (&ax)[4]) {
+  const int r16 = c.lane & 15, g4 = c.lane >> 4;
+  if constexpr (EPI <= 2) {
+    ax[0] = *reinterpret_cast<const u32x4*>(c.aux + 8 * g4);
+  } else {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) ax[jj] = *reinterpret_cast<const u32x4*>(c.aux + 512 * jj + 32 * r16 + 8 * g4);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// ---------------------------------------------------------------------------------------------
+// Counted waits.  Per phase a wave's vector-memory instructions issue in this order: the aux DMA
+// of the next quadrant (kAuxN; in the FIRST K-tile's phases 0-2 and the LAST K-tile's phase 3),
+// the quadrant's stores (FIRST only), the K-tile DMA (2).  Waits count the instructions issued
+// AFTER the ones they need (vmcnt(N) = all but the N youngest are done), so the stores never
+// have to complete.  Where a phase belongs to the previous K-tile its kind is only partly known
+// (a FIRST K-tile follows a LAST one; nothing else is guaranteed): the count is a lower bound.
+template <int EPI>
+constexpr int pp_phase_ops(bool F, bool L, int q) {
+  return 2 + (!kQuadEpi<EPI> ? 0 : (((F && q < 3) || (L && q == 3)) ? kAuxN<EPI> : 0) + (F ? kStQ<EPI>(q) : 0));
+}
+// the DMA wait of phase PH (piece group PH - 2 landed): everything issued in phases PH - 1, PH
+template <int EPI, bool F, bool L, int PH>
+constexpr int pp_dma_wait() {
+  int n = pp_phase_ops<EPI>(F, L, PH);
+  n += PH >= 1 ? pp_phase_ops<EPI>(F, L, PH - 1) : pp_phase_ops<EPI>(false, F, 3);
+  if constexpr (!kQuadEpi<EPI>) {
+    if (F && PH < 2) n += kPPEpi5Stores;  // EPI 5: the end-of-tile epilogue's stores
+  }
+  return n > 63 ? 63 : n;
+}
+// the aux wait of phase PH of a FIRST K-tile (aux issued first in phase PH - 1)
+template <int EPI, int PH>
+constexpr int pp_aux_wait() {
+  return 2 + (PH == 0 ? 0 : kStQ<EPI>(PH - 1));
+}
+
+// One phase of a K-tile: the LOAD segment (in a FIRST K-tile the previous tile's quadrant-PH
+// epilogue, then the fragment reads for this phase's quadrant, the next K-tile's piece group
+// PH, the counted wait), a barrier, the MFMA segment (16 MFMAs into quadrant PH), a barrier.
+// The epilogue goes first: the fragments it would otherwise overlap are not live yet.
+template <int PH, bool FIRST, bool LAST, int EPI>
+PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+                       const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl, int sk,
+                       const PPEpi& pe, const PPEpi& ce, float (&dsum)[4]) {
   const int wr = c.wr, wc = c.wc;
   const int st0 = sk < 0 ? -1 : 24 * sk + 6 * PH;  // stamp indices of this phase (kPPStamps)
   pp_stamp(c, st0);
-  // ---- LOAD segment: 8 / 4 / 8 / 4 fragment reads (PH 3 reads the NEXT K-tile's column pair 0)
-  if constexpr (PH == 0 || PH == 2) {
-    const char* sb = reinterpret_cast<const char*>(slotp);
-    const int jh = PH == 0 ? 0 : 1;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        fa[k][jj] = ldsf(reinterpret_cast<const uint16_t*>(
-            sb + c.rdA[k] + (unsigned)((wr * 128 + 16 * (4 * jh + jj)) * PBK * 2)));
-  } else {
-    const char* sb = reinterpret_cast<const char*>(PH == 1 ? slotp : nslotp);
-    const int p = PH == 1 ? 1 : 0;
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-        fb[p][k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
-            sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
+  if constexpr (kQuadEpi<EPI>) {
+    u32x4 ax[4];
+    if constexpr (FIRST) {
+      pp_vmwait<pp_aux_wait<EPI, PH>()>();
+      pp_aux_read<EPI>(c, ax);
+    }
+    if constexpr (FIRST && PH < 3) pp_aux_issue<EPI, PH + 1>(c, pe);
+    if constexpr (LAST && PH == 3) pp_aux_issue<EPI, 0>(c, ce);
+    if constexpr (FIRST) pp_epi_quad<EPI, PH>(acc, c, pe, ax, dsum);
+    __builtin_amdgcn_sched_barrier(0);
   }
   pp_stamp(c, st0 < 0 ? -1 : st0 + 1);
+  // ---- fragment reads: 12 / 4 / 8 / 4 (snake order: A rows half + column pair, then pair 1,
+  // rows half 1, pair 0 again; one column-pair set of registers)
+  {
+    const char* sb = reinterpret_cast<const char*>(slotp);
+    if constexpr (PH == 0 || PH == 2) {
+      const int jh = PH == 0 ? 0 : 1;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          fa[k][jj] = ldsf(reinterpret_cast<const uint16_t*>(
+              sb + c.rdA[k] + (unsigned)((wr * 128 + 16 * (4 * jh + jj)) * PBK * 2)));
+    }
+    if constexpr (PH != 2) {
+      const int p = PH == 1 ? 1 : 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int ii = 0; ii < 2; ++ii)
+          fb[k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
+              sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
+    }
+  }
   pp_issue<PH>(c, srd, nsl);
   pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
-  pp_vmwait<VM>();
+  pp_vmwait<pp_dma_wait<EPI, FIRST, LAST, PH>()>();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
   pp_barrier();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 4);
-  // ---- MFMA segment: quadrant (rows half jh, column pair p): (0,0) (0,1) (1,0) (1,1)
+  // ---- MFMA segment: quadrant (rows half jh, column pair p): (0,0) (0,1) (1,1) (1,0)
   {
-    constexpr int jh = PH >= 2 ? 1 : 0;
-    constexpr int p = PH & 1;
+    constexpr int jh = pp_qjh(PH);
+    constexpr int p = pp_qp(PH);
     if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
@@ -367,8 +623,8 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
 #pragma unroll
         for (int ii = 0; ii < 2; ++ii) {
           f32x4& a = acc[2 * p + ii][4 * jh + jj];
-          if (FIRST && k == 0) a = mfma16(fb[p][k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
-          else a = mfma16(fb[p][k][ii], fa[k][jj], a);
+          if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
+          else a = mfma16(fb[k][ii], fa[k][jj], a);
         }
     if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(0);
   }
@@ -376,28 +632,30 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   pp_barrier();
 }
 
-template <bool FIRST, int EPI>
-PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
-                       const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid) {
+template <bool FIRST, bool LAST, int EPI>
+PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+                       const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid, const PPEpi& pe,
+                       const PPEpi& ce, float (&dsum)[4]) {
   const uint16_t* slotp = smem + (s & 1) * PSLOT;
   const int nsl = (s + 1) & 1;
   const uint16_t* nslotp = smem + nsl * PSLOT;
   const PPSrd srd = pp_srds(c, ntm, ntn, nkt, nvalid);  // the DMA carries the next K-tile
-  constexpr int VE = FIRST ? 4 + kPPEpiStores<EPI> : 4;
-  constexpr int VL = (PLLM_PP_EXP & 16) && FIRST ? VE : 4;
-  // kPPStamps: the third tile's K-tile 0 (right after an epilogue) and its K-tile S / 2
+  // kPPStamps: the third tile's K-tile 0 (its first phases carry the second tile's epilogue) and
+  // its K-tile S / 2
   const int S = c.g->K / PBK;
   const int sk = !kPPStamps ? -1 : s == 2 * S ? 0 : s == 2 * S + S / 2 ? 1 : -1;
-  pp_phase<0, FIRST, VE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
-  pp_phase<1, FIRST, VE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
-  pp_phase<2, FIRST, VL>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
-  pp_phase<3, FIRST, VL>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk);
+  pp_phase<0, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<1, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<2, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<3, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
 }
 
 template <int EPI>
 __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
-  // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads)
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
+  // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads):
+  // two 64 KiB K-tile slots, then 8 x 4 KiB per-wave bias / aux areas (quadrant epilogues)
+  constexpr int kAuxElems = kQuadEpi<EPI> ? 8 * 2048 : 0;
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + kAuxElems + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
   const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + PT - 1) / PT, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
@@ -410,8 +668,10 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   c.wc = c.w & 3;
   c.lane = lane;
   c.lds = (unsigned)(uintptr_t)smem;
+  c.aux = smem + 2 * PSLOT + 2048 * c.w;
   c.stamp = kPPStamps && blockIdx.x == 0;
-  c.stamp_at = reinterpret_cast<uint64_t*>(smem + 2 * PSLOT) + kPPStampN * c.w;
+  c.stamp_at = reinterpret_cast<uint64_t*>(smem + 2 * PSLOT + kAuxElems) + kPPStampN * c.w;
+  c.vaux = (uint32_t)(((int64_t)(lane >> 2) * g.ldaux + 8 * (lane & 3)) * 2);
   {
     // per-lane source offsets of this wave's pieces: lane l of piece blk fills image row
     // 8 * blk + l / 8 at 16-B position l % 8, which holds logical chunk (l % 8) ^ swz(row),
@@ -429,10 +689,8 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     };
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
-      c.vo[0][q] = voB(pp_blk0<0>(c.w) + q);
-      c.vo[1][q] = voA(pp_blk0<1>(c.w) + q);
-      c.vo[2][q] = voB(pp_blk0<2>(c.w) + q);
-      c.vo[3][q] = voA(pp_blk0<3>(c.w) + q);
+      c.vo[0][q] = voA(pp_blk0<0>(c.w) + q);
+      c.vo[1][q] = voB(pp_blk0<1>(c.w) + q);
     }
   }
   {
@@ -446,10 +704,6 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     }
   }
   const int S = g.K / PBK;
-  if constexpr ((PLLM_PP_EXP & 32) != 0) {
-    if (lid & 1)
-      for (int i = 0; i < S * 24; ++i) __builtin_amdgcn_s_sleep(63);  // ~1.5k cycles per K-tile
-  }
   int tm, tn;
   pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
   // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
@@ -469,41 +723,50 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
 
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
-  bf16x8 fb[2][2][2];
-  {
-    // K-tile 0's column pair 0 (every later K-tile's is read in its predecessor's phase 3)
-    const char* sb = reinterpret_cast<const char*>(smem);
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii)
-        fb[0][k][ii] = ldsf(reinterpret_cast<const uint16_t*>(
-            sb + c.rdB[k] + (unsigned)((PIMG + (c.wc * 64 + 16 * ii) * PBK) * 2)));
-  }
+  bf16x8 fb[2][2];
+  float dsum[4] = {0.f, 0.f, 0.f, 0.f};
   int s = 0;
+  PPEpi pe{tm, tn, false};  // the previous tile (none yet)
   for (int t = lid; t < ntiles; t += G) {
     pp_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
+    const PPEpi ce{tm, tn, true};
     const bool more = t + G < ntiles;
     int tm2 = tm, tn2 = tn;
     if (more) pp_tile(t + G, tiles_m, tiles_n, g.group_m, tm2, tn2);
     // K-tile kt's DMA carries K-tile kt + 1, or the next tile's K-tile 0 after the last one.
-    // K-tile 0 is peeled (its MFMAs start the accumulators from zero): no path reaches an
-    // accumulating body without passing it, so the accumulators are dead after the epilogue
-    {
-      const bool last = S == 1;
-      pp_ktile<true, EPI>(c, acc, fa, fb, smem, s, last ? tm2 : tm, last ? tn2 : tn, last ? 0 : 1, !last || more);
-      ++s;
+    // K-tile 0 is peeled: its MFMAs start the accumulators from zero, each quadrant right after
+    // that quadrant's epilogue of the previous tile
+    // (S >= 2: gemm_tn sends K < 128 to the round-3 kernel)
+    pp_ktile<true, false, EPI>(c, acc, fa, fb, smem, s, tm, tn, 1, true, pe, ce, dsum);
+    ++s;
+    for (int kt = 1; kt + 1 < S; ++kt, ++s)
+      pp_ktile<false, false, EPI>(c, acc, fa, fb, smem, s, tm, tn, kt + 1, true, pe, ce, dsum);
+    pp_ktile<false, true, EPI>(c, acc, fa, fb, smem, s, tm2, tn2, 0, more, pe, ce, dsum);
+    ++s;
+    if constexpr (!kQuadEpi<EPI>) {
+      // EPI 5: the end-of-tile epilogue, in this wave's next LOAD slot
+      pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
     }
-    for (int kt = 1; kt < S; ++kt, ++s) {
-      const bool last = kt + 1 == S;
-      pp_ktile<false, EPI>(c, acc, fa, fb, smem, s, last ? tm2 : tm, last ? tn2 : tn, last ? 0 : kt + 1,
-                           !last || more);
-    }
-    // the epilogue runs in this wave's next LOAD slot: beside the partner group's MFMAs
-    const bool st_epi = kPPStamps && t == lid + G;  // the second tile's epilogue
-    pp_stamp(c, st_epi ? 48 : -1);
-    pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
-    pp_stamp(c, st_epi ? 49 : -1);
+    pe = ce;
+  }
+  if constexpr (kQuadEpi<EPI>) {
+    // the last tile's epilogue (its quadrant-0 aux was DMA'd in its last K-tile's phase 3)
+    u32x4 ax[4];
+    pp_vmwait<0>();
+    pp_aux_read<EPI>(c, ax);
+    pp_aux_issue<EPI, 1>(c, pe);
+    pp_epi_quad<EPI, 0>(acc, c, pe, ax, dsum);
+    pp_vmwait<0>();
+    pp_aux_read<EPI>(c, ax);
+    pp_aux_issue<EPI, 2>(c, pe);
+    pp_epi_quad<EPI, 1>(acc, c, pe, ax, dsum);
+    pp_vmwait<0>();
+    pp_aux_read<EPI>(c, ax);
+    pp_aux_issue<EPI, 3>(c, pe);
+    pp_epi_quad<EPI, 2>(acc, c, pe, ax, dsum);
+    pp_vmwait<0>();
+    pp_aux_read<EPI>(c, ax);
+    pp_epi_quad<EPI, 3>(acc, c, pe, ax, dsum);
   }
   if (c.wr == 0) pp_barrier();  // balance the stagger
   if constexpr (kPPStamps) {
@@ -522,6 +785,8 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
 }  // namespace
 
 namespace pllm {
+
+int gemm_pp_colsum_groups(int M) { return 4 * ((M + PT - 1) / PT); }
 
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
   const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + PT - 1) / PT);

@@ -14,6 +14,5 @@ for shape in "65536 3072 768" "65536 768 3072" "32768 2048 2048"; do
     done
   done
 done
-PLLM_SO=$R/pretraining_llm_amd/_C_ppexp64.so timeout -k 10 120 python bench/gemm_pp_stamps.py --M 65536 --N 3072 --K 768 > gpurun_out/r4pp6_stamps_k768.jsonl 2>&1 || { tail -5 gpurun_out/r4pp6_stamps_k768.jsonl; exit 1; }
 timeout -k 10 400 python -u bench/gemm_pp_bench.py --fused > gpurun_out/r4pp6_bench.jsonl 2>&1
 rc=$?; cat gpurun_out/r4pp6_bench.jsonl | cut -c1-400; exit $rc
