@@ -52,9 +52,12 @@ def main():
             wdt = (torch.randn(F_, C, device="cuda") / C ** 0.5).bfloat16()  # W_down^T shadow [F, C]
             gu = torch.randn(M, 2 * F_, device="cuda").bfloat16()
             fused = timeit(lambda: P.gemm_tn(dy, wdt, None, 5, gu))
+            P.gemm_set_config(args.mf, args.group, 4)
+            fused_pp = timeit(lambda: P.gemm_tn(dy, wdt, None, 5, gu))
+            P.gemm_set_config(args.mf, args.group, args.phased)
             unf = timeit(lambda: P.swiglu_bwd(dy @ wdt.t(), gu))
             dg = timeit(lambda: dy @ wdt.t())
-            print(json.dumps({"M": M, "F": F_, "C": C, "mf": args.mf, "fused_swiglu_bwd_us": round(fused, 1),
+            print(json.dumps({"M": M, "F": F_, "C": C, "mf": args.mf, "fused_swiglu_bwd_us": round(fused, 1), "pp_fused_swiglu_bwd_us": round(fused_pp, 1),
                               "blas_plus_swiglu_bwd_us": round(unf, 1), "blas_dgrad_us": round(dg, 1)}), flush=True)
             del dy, wdt, gu
         return

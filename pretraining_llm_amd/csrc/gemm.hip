@@ -394,8 +394,10 @@ static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
 // removed (profiles/r3_gemm_tn.md): 1 = two k32 phases per K-tile with counted vmcnt across raw
 // barriers (3-12 % slower), 3 = one wave per SIMD with 128x128 per wave and the DMA pinned between
 // MFMA groups (hipBLASLt's geometry; 4-18 % slower, its fused epilogues up to 40 % slower)
-// 4: the ping-pong kernel of gemm_pp.hip (two wave groups one barrier apart, counted waits)
-static int g_gemm_phased = 0;
+// 4 (default): the ping-pong kernel of gemm_pp.hip (two wave groups one barrier apart, counted
+// waits): 4-6 % faster than this file's kernel on every fused epilogue measured (GELU' / SwiGLU' /
+// attention delta; gpurun_out/r4pp7_bench.jsonl, r4ab1_swiglu.jsonl), whole GPT-2 step +0.5 %
+static int g_gemm_phased = 4;
 // CUs the persistent grids leave free, for RCCL kernels overlapping the backward (world > 1)
 static int g_gemm_reserve = 0;
 void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus) {
@@ -410,7 +412,7 @@ void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus) {
 // the ping-pong kernel serves a call when selected, with >= 2 K-tiles and (epilogue 6) 16 | T
 bool gemm_uses_pp(int K, int epi, int T) { return g_gemm_phased == 4 && K >= 128 && (epi != 6 || T % 16 == 0); }
 int gemm_colsum_groups(int M, int K) {
-  return gemm_uses_pp(K, 3, 0) ? gemm_pp_colsum_groups(M) : 2 * ((M + GT - 1) / GT);
+  return gemm_uses_pp(K, 3, 0) ? gemm_pp_colsum_groups(M, K) : 2 * ((M + GT - 1) / GT);
 }
 
 static int num_cus() {

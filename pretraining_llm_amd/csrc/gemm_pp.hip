@@ -43,7 +43,8 @@
 
 // Ablation builds (scripts/build_variant.py gemm_pp.hip x.so -DPLLM_PP_EXP=n; numerics WRONG):
 // bit 0: the epilogue computes but stores nothing; bit 1: the main loop issues no DMA (stale LDS);
-// bit 2: non-temporal stores; bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third
+// bit 2: non-temporal stores; bit 5: odd workgroups sleep ~half a tile first (epilogue bursts
+// desynchronised across CUs, at the price of the sleep); bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third
 // tile, 6 points per phase) written over the start of C (diagnostic: bench/gemm_pp_stamps.py);
 // bit 7: waves 4-7 at static priority 1 instead of per-segment flips.
 #ifndef PLLM_PP_EXP
@@ -86,14 +87,18 @@ PLLM_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn)
   tn = (t % per_group) / gsize;
 }
 
-// EPI 5's end-of-tile epilogue: the vector-memory instructions it issues after its last wait
-// (its stores); a lower bound is what the counted waits of the next tile's first phases need
-constexpr int kPPEpi5Stores = 32;
-// quadrant epilogues (every EPI but 5): DMA ops of the bias / aux rows of one quadrant, and the
-// stores of one quadrant epilogue (C, the EPI 1 pre-activation, the EPI 3 / 4 column-sum
-// partials, the EPI 6 delta on the second column pair)
+// Two epilogue placements (template flag QE, chosen per call by gemm_pp_quad_epilogue):
+//  * end of tile (QE = false): the vector-memory instructions it issues after its last wait
+//    (its stores; a lower bound) are what the counted waits of the next tile's first phases
+//    leave outstanding;
+//  * quadrant epilogues (QE = true; K >= 2048, every EPI but 5, whose 8 KiB of aux rows per wave
+//    and quadrant do not fit the LDS): kAuxN DMA ops of the bias / aux rows of one quadrant, and
+//    kStQ stores of one quadrant epilogue (C, the EPI 1 pre-activation, the EPI 3 / 4 column-sum
+//    partials, the EPI 6 delta on the second column pair).  Measured: faster at K = 3072 / 5504
+//    (fewer, longer tiles), slower at K = 768 (the epilogue work lands in the critical LOAD
+//    segments of four phases per tile).
 template <int EPI>
-constexpr bool kQuadEpi = EPI != 5;
+constexpr int kEndStores = (EPI == 1 || EPI == 5) ? 32 : 16;
 template <int EPI>
 constexpr int kAuxN = EPI <= 2 ? 1 : 4;
 template <int EPI>
@@ -162,11 +167,25 @@ PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, i
       }
     }
   };
-  aux_load(0, axc);
+  // EPI 3 / 4 / 6 (two loads per row tile): all 16 issued up front instead -- one round trip
+  // per tile, not eight (the pipelined form cost ~1k cycles per row tile under load)
+  constexpr bool PRE = EPI == 3 || EPI == 4 || EPI == 6;
+  u32x4 axall[PRE ? 8 : 1][2];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) aux_load(j, axall[j]);
+  } else {
+    aux_load(0, axc);
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int rt = wr * 128 + 16 * j + r16;  // row within the tile
-    if (j + 1 < 8) aux_load(j + 1, axn);
+    if constexpr (!PRE) {
+      if (j + 1 < 8) aux_load(j + 1, axn);
+    } else {
+      axc[0] = axall[j][0];
+      axc[1] = axall[j][1];
+    }
     float dsum = 0.f;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -245,7 +264,7 @@ PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, i
                                 ? (uint32_t)((((int64_t)bq * (N >> 6) + hd) * g.T + tq) * 4) : kPOff;
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dsum), drs, doff, 0, 0);
     }
-    if constexpr (NAX > 0) {
+    if constexpr (NAX > 0 && !PRE) {
 #pragma unroll
       for (int x = 0; x < NAX; ++x) axc[x] = axn[x];
       __builtin_amdgcn_sched_barrier(0);
@@ -539,17 +558,17 @@ PLLM_DEV void pp_aux_read(const PPCtx& c, u32x4 (&ax)[4]) {
 // AFTER the ones they need (vmcnt(N) = all but the N youngest are done), so the stores never
 // have to complete.  Where a phase belongs to the previous K-tile its kind is only partly known
 // (a FIRST K-tile follows a LAST one; nothing else is guaranteed): the count is a lower bound.
-template <int EPI>
+template <int EPI, bool QE>
 constexpr int pp_phase_ops(bool F, bool L, int q) {
-  return 2 + (!kQuadEpi<EPI> ? 0 : (((F && q < 3) || (L && q == 3)) ? kAuxN<EPI> : 0) + (F ? kStQ<EPI>(q) : 0));
+  return 2 + (!QE ? 0 : (((F && q < 3) || (L && q == 3)) ? kAuxN<EPI> : 0) + (F ? kStQ<EPI>(q) : 0));
 }
 // the DMA wait of phase PH (piece group PH - 2 landed): everything issued in phases PH - 1, PH
-template <int EPI, bool F, bool L, int PH>
+template <int EPI, bool QE, bool F, bool L, int PH>
 constexpr int pp_dma_wait() {
-  int n = pp_phase_ops<EPI>(F, L, PH);
-  n += PH >= 1 ? pp_phase_ops<EPI>(F, L, PH - 1) : pp_phase_ops<EPI>(false, F, 3);
-  if constexpr (!kQuadEpi<EPI>) {
-    if (F && PH < 2) n += kPPEpi5Stores;  // EPI 5: the end-of-tile epilogue's stores
+  int n = pp_phase_ops<EPI, QE>(F, L, PH);
+  n += PH >= 1 ? pp_phase_ops<EPI, QE>(F, L, PH - 1) : pp_phase_ops<EPI, QE>(false, F, 3);
+  if constexpr (!QE) {
+    if (F && PH < 2) n += kEndStores<EPI>;  // the end-of-tile epilogue's stores
   }
   return n > 63 ? 63 : n;
 }
@@ -563,14 +582,14 @@ constexpr int pp_aux_wait() {
 // epilogue, then the fragment reads for this phase's quadrant, the next K-tile's piece group
 // PH, the counted wait), a barrier, the MFMA segment (16 MFMAs into quadrant PH), a barrier.
 // The epilogue goes first: the fragments it would otherwise overlap are not live yet.
-template <int PH, bool FIRST, bool LAST, int EPI>
+template <int PH, bool FIRST, bool LAST, int EPI, bool QE>
 PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
                        const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl, int sk,
                        const PPEpi& pe, const PPEpi& ce, float (&dsum)[4]) {
   const int wr = c.wr, wc = c.wc;
   const int st0 = sk < 0 ? -1 : 24 * sk + 6 * PH;  // stamp indices of this phase (kPPStamps)
   pp_stamp(c, st0);
-  if constexpr (kQuadEpi<EPI>) {
+  if constexpr (QE) {
     u32x4 ax[4];
     if constexpr (FIRST) {
       pp_vmwait<pp_aux_wait<EPI, PH>()>();
@@ -607,7 +626,7 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   }
   pp_issue<PH>(c, srd, nsl);
   pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
-  pp_vmwait<pp_dma_wait<EPI, FIRST, LAST, PH>()>();
+  pp_vmwait<pp_dma_wait<EPI, QE, FIRST, LAST, PH>()>();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
   pp_barrier();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 4);
@@ -632,7 +651,7 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   pp_barrier();
 }
 
-template <bool FIRST, bool LAST, int EPI>
+template <bool FIRST, bool LAST, int EPI, bool QE>
 PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
                        const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid, const PPEpi& pe,
                        const PPEpi& ce, float (&dsum)[4]) {
@@ -644,17 +663,17 @@ PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   // its K-tile S / 2
   const int S = c.g->K / PBK;
   const int sk = !kPPStamps ? -1 : s == 2 * S ? 0 : s == 2 * S + S / 2 ? 1 : -1;
-  pp_phase<0, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<1, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<2, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<3, FIRST, LAST, EPI>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<0, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<1, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<2, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<3, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
 }
 
-template <int EPI>
+template <int EPI, bool QE>
 __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads):
   // two 64 KiB K-tile slots, then 8 x 4 KiB per-wave bias / aux areas (quadrant epilogues)
-  constexpr int kAuxElems = kQuadEpi<EPI> ? 8 * 2048 : 0;
+  constexpr int kAuxElems = QE ? 8 * 2048 : 0;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + kAuxElems + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
   const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + PT - 1) / PT, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
@@ -704,6 +723,10 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     }
   }
   const int S = g.K / PBK;
+  if constexpr ((PLLM_PP_EXP & 32) != 0) {
+    if (lid & 1)
+      for (int i = 0; i < S / 3; ++i) __builtin_amdgcn_s_sleep(63);  // ~4k cycles each
+  }
   int tm, tn;
   pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
   // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
@@ -737,19 +760,19 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     // K-tile 0 is peeled: its MFMAs start the accumulators from zero, each quadrant right after
     // that quadrant's epilogue of the previous tile
     // (S >= 2: gemm_tn sends K < 128 to the round-3 kernel)
-    pp_ktile<true, false, EPI>(c, acc, fa, fb, smem, s, tm, tn, 1, true, pe, ce, dsum);
+    pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, 1, true, pe, ce, dsum);
     ++s;
     for (int kt = 1; kt + 1 < S; ++kt, ++s)
-      pp_ktile<false, false, EPI>(c, acc, fa, fb, smem, s, tm, tn, kt + 1, true, pe, ce, dsum);
-    pp_ktile<false, true, EPI>(c, acc, fa, fb, smem, s, tm2, tn2, 0, more, pe, ce, dsum);
+      pp_ktile<false, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kt + 1, true, pe, ce, dsum);
+    pp_ktile<false, true, EPI, QE>(c, acc, fa, fb, smem, s, tm2, tn2, 0, more, pe, ce, dsum);
     ++s;
-    if constexpr (!kQuadEpi<EPI>) {
-      // EPI 5: the end-of-tile epilogue, in this wave's next LOAD slot
+    if constexpr (!QE) {
+      // the end-of-tile epilogue, in this wave's next LOAD slot
       pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
     }
     pe = ce;
   }
-  if constexpr (kQuadEpi<EPI>) {
+  if constexpr (QE) {
     // the last tile's epilogue (its quadrant-0 aux was DMA'd in its last K-tile's phase 3)
     u32x4 ax[4];
     pp_vmwait<0>();
@@ -786,21 +809,34 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
 
 namespace pllm {
 
-int gemm_pp_colsum_groups(int M) { return 4 * ((M + PT - 1) / PT); }
+// EPI 3 / 4 column-sum partial rows: 4 per tile row with quadrant epilogues, 2 otherwise
+int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 4 : 2) * ((M + PT - 1) / PT); }
+
+// quadrant epilogues at K >= 2048, except EPI 5 (aux too large for the LDS) and EPI 1 (the GELU's
+// VALU work in the LOAD segments: 1410 vs 1344 us for the end-of-tile form + hipBLASLt at the llama
+// shape 32768 x 11008 x 2048, gpurun_out/r4pp7_bench.jsonl)
+bool gemm_pp_quad_epilogue(int K, int epi) { return K >= 2048 && epi != 5 && epi != 1; }
 
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
   const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + PT - 1) / PT);
   if (ntiles == 0) return;
   const int grid = ntiles < ctas ? ntiles : ctas;
+  const bool qe = gemm_pp_quad_epilogue(a.K, epi);
+#define PLLM_PP_CASE(E)                                                                          \
+  do {                                                                                           \
+    if (qe) hipLaunchKernelGGL((gemm_pp_kernel<E, E != 5>), dim3(grid), dim3(PNT), 0, st, a);     \
+    else hipLaunchKernelGGL((gemm_pp_kernel<E, false>), dim3(grid), dim3(PNT), 0, st, a);         \
+  } while (0)
   switch (epi) {
-    case 0: hipLaunchKernelGGL((gemm_pp_kernel<0>), dim3(grid), dim3(PNT), 0, st, a); break;
-    case 1: hipLaunchKernelGGL((gemm_pp_kernel<1>), dim3(grid), dim3(PNT), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((gemm_pp_kernel<2>), dim3(grid), dim3(PNT), 0, st, a); break;
-    case 3: hipLaunchKernelGGL((gemm_pp_kernel<3>), dim3(grid), dim3(PNT), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((gemm_pp_kernel<4>), dim3(grid), dim3(PNT), 0, st, a); break;
-    case 5: hipLaunchKernelGGL((gemm_pp_kernel<5>), dim3(grid), dim3(PNT), 0, st, a); break;
-    default: hipLaunchKernelGGL((gemm_pp_kernel<6>), dim3(grid), dim3(PNT), 0, st, a); break;
+    case 0: PLLM_PP_CASE(0); break;
+    case 1: PLLM_PP_CASE(1); break;
+    case 2: PLLM_PP_CASE(2); break;
+    case 3: PLLM_PP_CASE(3); break;
+    case 4: PLLM_PP_CASE(4); break;
+    case 5: PLLM_PP_CASE(5); break;
+    default: PLLM_PP_CASE(6); break;
   }
+#undef PLLM_PP_CASE
 }
 
 }  // namespace pllm

@@ -123,7 +123,8 @@ void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 // free by the persistent grids (collectives in flight), -1 keeps the current setting
 void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1);
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
-int gemm_pp_colsum_groups(int M);
+int gemm_pp_colsum_groups(int M, int K);
+bool gemm_pp_quad_epilogue(int K, int epi);
 int gemm_colsum_groups(int M, int K);  // column-sum partial rows (epi 3 / 4) of the kernel serving K
 bool gemm_uses_pp(int K, int epi, int T);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)

@@ -37,7 +37,9 @@ SHAPES = [(512, 768, 768), (300, 520, 128), (1024, 3072, 768), (777, 264, 192), 
           (16640, 1032, 320)]
 
 
-# phased 4 = the ping-pong kernel (csrc/gemm_pp.hip; its MFMA shape is fixed, mf is ignored)
+# phased 4 = the ping-pong kernel (csrc/gemm_pp.hip; its MFMA shape is fixed, mf is ignored),
+# the default (csrc/gemm.hip g_gemm_phased); 0 / 2 = the round-3 kernel kept for A/B
+DEFAULT_KERNEL = 4
 KERNELS = [(16, 0), (32, 0), (16, 2), (32, 2), (16, 4)]
 
 
@@ -67,7 +69,7 @@ def test_gemm_tn_forward_epilogues(M, N, K, mf, phased):
         assert _rel(y, torch.relu(pre_ref)) < 5e-3
         assert torch.equal(torch.ops.pllm.gemm_tn(a, b, bias, 1)[0], act)  # deterministic
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL)
 
 
 @pytest.mark.parametrize("mf,phased", KERNELS)
@@ -94,7 +96,7 @@ def test_gemm_tn_backward_epilogues(M, N, K, mf, f32_bias_grad, phased):
             out2, _ = torch.ops.pllm.gemm_tn(dy, wt, None, epi, aux)
             assert torch.equal(out, out2)
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL)
 
 
 def test_gemm_tn_contract_checks():
@@ -182,7 +184,7 @@ def test_gemm_tn_swiglu_backward_epilogue(M, N, K, mf, phased):
         assert (out.float() - unfused.float()).abs().max().item() <= 2 ** -6 * unfused.float().abs().max().item()
         assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 5, gu)[0], out)  # deterministic
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL)
 
 
 def test_fused_swiglu_mlp_matches_unfused():
@@ -236,7 +238,7 @@ def test_gemm_tn_attn_delta_epilogue(B, T, H, phased):
         assert _rel(delta.double(), ref) < 1e-6, _rel(delta.double(), ref)
         assert torch.equal(torch.ops.pllm.gemm_tn(dy, wt, None, 6, o, None, T)[1], delta)  # deterministic
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL)
 
 
 @pytest.mark.parametrize("bias", [True, False])
@@ -294,7 +296,7 @@ def test_gemm_tn_reserved_cus(phased, reserve):
         assert torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1])
         assert _rel(out[1], a.float() @ b.float().t() + bias.float()) < 5e-3
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL, 0)
 
 
 @pytest.mark.parametrize("M,N,K", [(65536, 768, 768), (65536, 3072, 768), (8192, 2304, 3072)])
@@ -310,7 +312,7 @@ def test_gemm_pp_large_shapes(M, N, K):
         torch.ops.pllm.gemm_set_config(16, 4, 0)
         old = torch.ops.pllm.gemm_tn(a, b, None, 0)[0]
     finally:
-        torch.ops.pllm.gemm_set_config(16, 4, 0)
+        torch.ops.pllm.gemm_set_config(16, 4, DEFAULT_KERNEL)
     rows = torch.randint(0, M, (512,), device=DEV)
     ref = a[rows].float() @ b.float().t()
     assert _rel(out[rows], ref) < 5e-3
