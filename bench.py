@@ -64,6 +64,9 @@ def parse(argv=None):
                     help="replay the whole step as one captured hipGraph; auto: the Trainer's own policy "
                          "(train/graph.py graph_step_policy): on for one GPU on the HIP path (+0.5 %%, "
                          "profiles/r3s3_graph_ab.txt), off with N > 1 ranks unless --graph-collectives, off for ZeRO")
+    ap.add_argument("--reserve-cus", type=int, default=0,
+                    help="CUs the persistent fused-epilogue GEMM grid leaves free (for RCCL kernels overlapping "
+                         "the backward at N > 1); 0 = every CU")
     ap.add_argument("--graph-collectives", action="store_true",
                     help="with N > 1 and --cuda-graph auto: capture the RCCL all-reduces inside the step's hipGraph "
                          "(opt-in, as the Trainer's graph_collectives=True; default: eager hook-overlapped step)")
@@ -135,6 +138,7 @@ def main(argv=None):
     ops.set_backend(args.backend)
     if args.backend == "auto" and not cpu:
         ops._lib.require()  # the HIP path must be the one that runs: fail loudly if the extension is missing
+        ops.gemm_config(reserve_cus=args.reserve_cus)
 
     torch.manual_seed(1234)
     mcfg = get_preset(args.model)
@@ -248,6 +252,7 @@ def main(argv=None):
                        "parallelism": f"dp{world}" + ("-zero1" if args.zero else ""), "micro_batch_per_gpu": B, "backend": args.backend,
                        "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph),
                        "step_mode": "graph" if args.cuda_graph else "eager",
+                       "gemm_reserve_cus": args.reserve_cus,
                        "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev))),
                        "checkpointed_blocks": int(model.checkpointed_blocks(torch.empty(B, T, device=dev)))},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),

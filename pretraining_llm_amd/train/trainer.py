@@ -101,6 +101,9 @@ class Trainer:
                                         growth_interval=int(self.cfg.get("loss_scale_growth_interval", 2000)),
                                         enabled=loss_scaling_default(dtype_name) if ls is None else bool(ls))
         self.tuned_gemms = False
+        if self.device.type == "cuda":
+            # CUs the persistent fused-epilogue GEMM grid leaves to RCCL kernels (world > 1); 0 = all
+            ops.gemm_config(reserve_cus=int(self.cfg.get("gemm_reserve_cus", 0)))
         if self.device.type == "cuda" and self.cfg.get("tuned_gemms", True):
             # the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/), as bench.py uses them
             from ..utils.gemm_tuning import enable_tuned_gemms
