@@ -229,8 +229,12 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   check_bf16(b, "b");
   TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_tn: a [M, K], b [N, K]");
   TORCH_CHECK(a.stride(1) == 1 && b.is_contiguous(), "gemm_tn: K-contiguous operands");
-  TORCH_CHECK(epi >= 0 && epi <= 6, "gemm_tn: epi 0..6");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(epi >= 0 && epi <= 7, "gemm_tn: epi 0..7");
+  const int64_t M = a.size(0), K = a.size(1), N = epi == 7 ? b.size(0) / 2 : b.size(0);
+  // epi 7: b = [gate | up] rows [2F, K] -> out = silu(gate) * up [M, F], aux = [gate | up] [M, 2F]
+  // (the llama up-projection with its SwiGLU; ping-pong kernel only)
+  TORCH_CHECK(epi != 7 || (b.size(0) % 16 == 0 && pllm::gemm_uses_pp((int)K, 7, 0)),
+              "gemm_tn: epi 7 needs 2F % 16 == 0, K >= 128 and the ping-pong kernel");
   TORCH_CHECK(K % 64 == 0 && K > 0, "gemm_tn: K must be a positive multiple of 64, got ", K);
   TORCH_CHECK(N % 8 == 0 && a.stride(0) % 8 == 0, "gemm_tn: N and lda must be multiples of 8");
   TORCH_CHECK(M < (1 << 30) && N < (1 << 30), "gemm_tn: dims");
@@ -246,8 +250,9 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     TORCH_CHECK(epi <= 2, "gemm_tn: bias only in the forward epilogues");
   }
   Tensor out = at::empty({M, epi == 5 ? 2 * N : N}, a.options());
-  Tensor aux_out = epi == 6 ? at::empty({T > 0 ? M / T : 0, N / 64, T}, a.options().dtype(at::kFloat))
-                            : at::empty({epi == 1 ? M : 0, N}, a.options());
+  Tensor aux_out = epi == 6   ? at::empty({T > 0 ? M / T : 0, N / 64, T}, a.options().dtype(at::kFloat))
+                   : epi == 7 ? at::empty({M, 2 * N}, a.options())
+                              : at::empty({epi == 1 ? M : 0, N}, a.options());
   pllm::GemmArgs g{};
   g.A = (const uint16_t*)a.data_ptr();
   g.B = (const uint16_t*)b.data_ptr();
@@ -263,6 +268,10 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
   if (epi == 1) {
     g.aux = (uint16_t*)aux_out.data_ptr();
     g.ldaux = N;
+  } else if (epi == 7) {
+    TORCH_CHECK(!bias, "gemm_tn: epi 7 has no bias");
+    g.aux = (uint16_t*)aux_out.data_ptr();
+    g.ldaux = 2 * N;
   } else if (epi == 6) {
     TORCH_CHECK(aux.has_value(), "gemm_tn: epi 6 needs aux = the attention output [M, N]");
     check_bf16(*aux, "aux");
@@ -969,6 +978,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
+  m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1) -> ()",
         [](int64_t mf, int64_t gm, int64_t ph, int64_t rc) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc); });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });

@@ -98,7 +98,13 @@ PLLM_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn)
 //    (fewer, longer tiles), slower at K = 768 (the epilogue work lands in the critical LOAD
 //    segments of four phases per tile).
 template <int EPI>
-constexpr int kEndStores = (EPI == 1 || EPI == 5) ? 32 : 16;
+constexpr int kEndStores = (EPI == 1 || EPI == 5) ? 32 : EPI == 7 ? 24 : 16;
+// EPI 7 (SwiGLU forward of the llama up-projection, W1 = [gate | up] rows): a tile is 128 output
+// columns whose gate AND up weight rows form the 256-row B panel -- wave wc's column pair 0 holds
+// gate rows wc*32 + [0,32), its pair 1 the up rows of the same columns -- so every lane holds
+// gate and up of the same 8 columns: a = silu(g) * u in registers, [g | u] kept for the backward
+template <int EPI>
+constexpr int kNT = EPI == 7 ? 128 : PT;
 template <int EPI>
 constexpr int kAuxN = EPI <= 2 ? 1 : 4;
 template <int EPI>
@@ -297,6 +303,45 @@ PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, i
 }
 
 
+// EPI 7 epilogue (end of tile): per row tile the lane's gate (pair 0) and up (pair 1) values of
+// columns n0 + wc*32 + 8g + [0, 8) -> [g | u] rounded to bf16 into aux [M, 2F] and
+// a = silu(g) * u from those bf16 values (swiglu_fwd_kernel's numerics) into C [M, F]: 24 stores
+PLLM_DEV void pp_epilogue_swiglu(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc,
+                                 int lane) {
+  const int M = g.M, F = g.N;
+  const int m0 = tm * PT, n0 = tn * 128;
+  const int r16 = lane & 15, g4 = lane >> 4;
+  const int col = n0 + wc * 32 + 8 * g4;
+  const bool ok = col < F;
+  const uint32_t off = ok ? (uint32_t)(((int64_t)r16 * g.ldc + col) * 2) : kPOff;
+  const uint32_t aoff = ok ? (uint32_t)(((int64_t)r16 * g.ldaux + col) * 2) : kPOff;
+  const int rows_ok = min(PT, M - m0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int r0 = wr * 128 + 16 * j;
+    const int rows_j = max(0, rows_ok - r0);
+    const __amdgpu_buffer_rsrc_t crs = rows_rsrc(g.C + (int64_t)(m0 + r0) * g.ldc, rows_j, g.ldc, F);
+    const __amdgpu_buffer_rsrc_t ars = rows_rsrc(g.aux + (int64_t)(m0 + r0) * g.ldaux, rows_j, g.ldaux, 2 * F);
+    float gt[8], up[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      gt[q] = acc[0][j][q];
+      gt[4 + q] = acc[1][j][q];
+      up[q] = acc[2][j][q];
+      up[4 + q] = acc[3][j][q];
+    }
+    const u32x4 gp = pack8(gt), upk = pack8(up);
+    unpack8(gp, gt);
+    unpack8(upk, up);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) gt[q] = gt[q] * pp_sigmoid(gt[q]) * up[q];
+    pp_st16(ars, aoff, gp);
+    pp_st16(ars, ok ? aoff + (uint32_t)F * 2u : kPOff, upk);
+    pp_st16(crs, off, pack8(gt));
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 struct PPCtx {
   const pllm::GemmArgs* g;
@@ -330,15 +375,22 @@ PLLM_DEV void pp_stamp(const PPCtx& c, int idx) {
 // issue, so the counted waits stay exact; nothing reads that slot again).  Built once per K-tile:
 // the pieces differ only in their per-lane offsets (PPCtx::vo), which hold the row.
 struct PPSrd {
-  i32x4v a, b;
+  i32x4v a, b, b2;  // b2: EPI 7's up-row panel (piece group 2)
 };
+template <int EPI>
 PLLM_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
   const pllm::GemmArgs& g = *c.g;
-  const int ra = min(PT, g.M - tm * PT), rb = min(PT, g.N - tn * PT);
+  constexpr int NT = kNT<EPI>;
+  const int ra = min(PT, g.M - tm * PT), rb = min(NT, g.N - tn * NT);
   const int64_t kleft2 = (int64_t)(g.K - kt * PBK) * 2;
   const uint32_t ba = valid ? (uint32_t)((int64_t)(ra - 1) * g.lda * 2 + kleft2) : 0u;
   const uint32_t bb = valid ? (uint32_t)((int64_t)(rb - 1) * g.ldb * 2 + kleft2) : 0u;
-  return {srd_of(g.A + (int64_t)tm * PT * g.lda + kt * PBK, ba), srd_of(g.B + (int64_t)tn * PT * g.ldb + kt * PBK, bb)};
+  const uint16_t* bp = g.B + (int64_t)tn * NT * g.ldb + kt * PBK;
+  PPSrd r;
+  r.a = srd_of(g.A + (int64_t)tm * PT * g.lda + kt * PBK, ba);
+  r.b = srd_of(bp, bb);
+  if constexpr (EPI == 7) r.b2 = srd_of(bp + (int64_t)g.N * g.ldb, bb);  // up rows N (= F) further
+  return r;
 }
 
 // DMA piece group PH (2 pieces per wave) of the target K-tile into LDS slot sl, in the order of
@@ -361,7 +413,7 @@ PLLM_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
   o[3] = r[3];
   return o;
 }
-template <int PH>
+template <int PH, int EPI = 0>
 PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
   // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
   constexpr bool isA = PH == 0 || PH == 3;
@@ -369,9 +421,11 @@ PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
   const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG) + blk0 * 512) * 2u;
   if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
   // groups 2 / 3: the pieces of groups 1 / 0 shifted by 4 (B: 32 rows) / 8 (A: 64 rows) pieces
+  // (EPI 7: group 2 = the up rows of group 1's columns, from their own panel)
   const i32x4v r = PH < 2 ? (isA ? srd.a : srd.b)
-                          : srd_shift(isA ? srd.a : srd.b,
-                                      (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
+                   : (EPI == 7 && !isA) ? srd.b2
+                                        : srd_shift(isA ? srd.a : srd.b,
+                                                    (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
 #pragma unroll
   for (int q = 0; q < 2; ++q) blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
 }
@@ -624,7 +678,7 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
               sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
     }
   }
-  pp_issue<PH>(c, srd, nsl);
+  pp_issue<PH, EPI>(c, srd, nsl);
   pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
   pp_vmwait<pp_dma_wait<EPI, QE, FIRST, LAST, PH>()>();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
@@ -658,7 +712,7 @@ PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   const uint16_t* slotp = smem + (s & 1) * PSLOT;
   const int nsl = (s + 1) & 1;
   const uint16_t* nslotp = smem + nsl * PSLOT;
-  const PPSrd srd = pp_srds(c, ntm, ntn, nkt, nvalid);  // the DMA carries the next K-tile
+  const PPSrd srd = pp_srds<EPI>(c, ntm, ntn, nkt, nvalid);  // the DMA carries the next K-tile
   // kPPStamps: the third tile's K-tile 0 (its first phases carry the second tile's epilogue) and
   // its K-tile S / 2
   const int S = c.g->K / PBK;
@@ -675,7 +729,7 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   // two 64 KiB K-tile slots, then 8 x 4 KiB per-wave bias / aux areas (quadrant epilogues)
   constexpr int kAuxElems = QE ? 8 * 2048 : 0;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + kAuxElems + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
-  const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + PT - 1) / PT, ntiles = tiles_m * tiles_n;
+  const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + kNT<EPI> - 1) / kNT<EPI>, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
   if (lid >= ntiles) return;
@@ -703,7 +757,9 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     };
     auto voB = [&](int blk) {
       const int ch = (lane & 7) ^ ((4 * (blk & 1) + (lane >> 4)) & 7);
-      const int row = 32 * (blk >> 2) + 16 * (blk & 1) + 4 * ((blk >> 1) & 1) + prow;
+      // EPI 7: image 32-row block 2 wc + h holds gate (h = 0) / up (h = 1) rows wc*32 + [0, 32)
+      const int b32 = EPI == 7 ? (blk >> 2) >> 1 : blk >> 2;
+      const int row = 32 * b32 + 16 * (blk & 1) + 4 * ((blk >> 1) & 1) + prow;
       return (uint32_t)(((int64_t)row * g.ldb + ch * 8) * 2);
     };
 #pragma unroll
@@ -731,11 +787,11 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
   // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
   {
-    const PPSrd srd = pp_srds(c, tm, tn, 0, true);
-    pp_issue<0>(c, srd, 0);
-    pp_issue<1>(c, srd, 0);
-    pp_issue<2>(c, srd, 0);
-    pp_issue<3>(c, srd, 0);
+    const PPSrd srd = pp_srds<EPI>(c, tm, tn, 0, true);
+    pp_issue<0, EPI>(c, srd, 0);
+    pp_issue<1, EPI>(c, srd, 0);
+    pp_issue<2, EPI>(c, srd, 0);
+    pp_issue<3, EPI>(c, srd, 0);
   }
   pp_vmwait<0>();
   pp_barrier();
@@ -768,7 +824,8 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     ++s;
     if constexpr (!QE) {
       // the end-of-tile epilogue, in this wave's next LOAD slot
-      pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
+      if constexpr (EPI == 7) pp_epilogue_swiglu(acc, g, tm, tn, c.wr, c.wc, lane);
+      else pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
     }
     pe = ce;
   }
@@ -818,13 +875,14 @@ int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 
 bool gemm_pp_quad_epilogue(int K, int epi) { return K >= 2048 && epi != 5 && epi != 1; }
 
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
-  const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + PT - 1) / PT);
+  const int nt = epi == 7 ? 128 : PT;
+  const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + nt - 1) / nt);
   if (ntiles == 0) return;
   const int grid = ntiles < ctas ? ntiles : ctas;
   const bool qe = gemm_pp_quad_epilogue(a.K, epi);
 #define PLLM_PP_CASE(E)                                                                          \
   do {                                                                                           \
-    if (qe) hipLaunchKernelGGL((gemm_pp_kernel<E, E != 5>), dim3(grid), dim3(PNT), 0, st, a);     \
+    if (qe) hipLaunchKernelGGL((gemm_pp_kernel<E, E != 5 && E != 1>), dim3(grid), dim3(PNT), 0, st, a); \
     else hipLaunchKernelGGL((gemm_pp_kernel<E, false>), dim3(grid), dim3(PNT), 0, st, a);         \
   } while (0)
   switch (epi) {
@@ -834,7 +892,8 @@ void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
     case 3: PLLM_PP_CASE(3); break;
     case 4: PLLM_PP_CASE(4); break;
     case 5: PLLM_PP_CASE(5); break;
-    default: PLLM_PP_CASE(6); break;
+    case 6: PLLM_PP_CASE(6); break;
+    default: hipLaunchKernelGGL((gemm_pp_kernel<7, false>), dim3(grid), dim3(PNT), 0, st, a); break;
   }
 #undef PLLM_PP_CASE
 }

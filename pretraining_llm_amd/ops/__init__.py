@@ -272,6 +272,8 @@ def gemm_config(kernel: Optional[str] = None, reserve_cus: Optional[int] = None)
 _FM = _os.environ.get("PLLM_FUSED_MLP", "bwd")
 FUSED_MLP = _FM in ("1", "all", "bwd")
 FUSED_MLP_FWD = _FM in ("1", "all")
+# PLLM_FUSED_SWIGLU_FWD=1|0: the llama up-projection with its SwiGLU in the GEMM epilogue (epilogue 7)
+FUSED_SWIGLU_FWD = _os.environ.get("PLLM_FUSED_SWIGLU_FWD", "1") == "1"
 
 
 def fused_mlp_ok(x, w1, b1, w2, act: str) -> bool:
@@ -400,8 +402,13 @@ class _FusedSwiGLUMLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, w2):
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
-        gu = F.linear(x2, w1)
-        a = _ops().swiglu_fwd(gu)
+        if FUSED_SWIGLU_FWD and _ops().gemm_uses_pp(C, 7):
+            # the SwiGLU in the up-projection's epilogue (gemm_tn epilogue 7, ping-pong kernel):
+            # no swiglu_fwd pass re-reading the [tokens, 2F] pre-activations
+            a, gu = _ops().gemm_tn(x2, w1, None, 7)
+        else:
+            gu = F.linear(x2, w1)
+            a = _ops().swiglu_fwd(gu)
         ctx.save_for_backward(x2, gu, a)
         ctx.params = (w1, w2)
         ctx.xshape = x.shape

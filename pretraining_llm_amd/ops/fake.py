@@ -59,6 +59,8 @@ def register() -> None:
         M, N = a.shape[0], b.shape[0]
         if epi == 6:  # dO and delta [M / T, N / 64, T] fp32
             return a.new_empty((M, N)), a.new_empty((M // T, N // 64, T), dtype=torch.float32)
+        if epi == 7:  # SwiGLU forward: silu(gate) * up [M, F] and [gate | up] [M, 2F], b = [2F, K]
+            return a.new_empty((M, N // 2)), a.new_empty((M, N))
         return a.new_empty((M, 2 * N if epi == 5 else N)), a.new_empty((M if epi == 1 else 0, N))
 
     @_reg("act_fwd")

@@ -1,0 +1,12 @@
+#!/bin/bash
+# GEMM tests (incl. epilogue 7), desync experiment, llama SwiGLU-forward epilogue A/B
+R="${GRAFT_REPO_ROOT:-/root/repo}"
+cd "$R"; mkdir -p gpurun_out
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+timeout -k 10 400 python -u -m pytest tests/test_gemm_gpu.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r4ab2_tests.log 2>&1
+rc=$?; grep -E "FAILED|passed|failed|Error" gpurun_out/r4ab2_tests.log | tail -8; [ $rc -ne 0 ] && exit $rc
+bash scripts/gpu/r4_pp8.sh || exit 1
+for v in 0 1 0 1; do
+  PLLM_FUSED_SWIGLU_FWD=$v timeout -k 10 400 python bench.py --model llama-1.3b --batch 16 --seq 2048 --steps 5 --warmup 2 > gpurun_out/r4ab2_llama_$v.log 2>&1 || { tail -3 gpurun_out/r4ab2_llama_$v.log; exit 1; }
+  echo "llama swiglu_fwd_epi=$v $(tail -1 gpurun_out/r4ab2_llama_$v.log | python -c 'import json,sys; r=json.loads(sys.stdin.read()); print(r["value"], r["ms_per_step"])')"
+done
