@@ -3,7 +3,10 @@
 data, the variants INTERLEAVED round by round in one process (cdna_hip_programming.md §5.4 rule 24).
 One JSON line per shape: median and min microseconds per variant, TF/s of the medians.
 
-usage: python bench/gemm_pp_bench.py [--rounds 7] [--fused] [--shapes gpt2|llama|all]"""
+Variants: pp (ping-pong kernel with the opt-in desynchronising tile split where it applies),
+pp_ns (the default: without the split), r3, blas.
+
+usage: python bench/gemm_pp_bench.py [--rounds 7] [--fused] [--shapes gpt2|llama|all] [--no-r3]"""
 import argparse
 import json
 import os
@@ -35,15 +38,16 @@ def main():
     ap.add_argument("--fused", action="store_true", help="also the fused MLP epilogues (GELU fwd / dGELU+colsum)")
     ap.add_argument("--shapes", default="all", choices=["gpt2", "llama", "all"])
     ap.add_argument("--group", type=int, default=4)
+    ap.add_argument("--no-r3", action="store_true", help="skip the round-3 kernel variants")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
     P = torch.ops.pllm
     shapes = (GPT2 if args.shapes != "llama" else []) + (LLAMA if args.shapes != "gpt2" else [])
 
-    def with_cfg(ph, fn):
+    def with_cfg(ph, fn, split=1):
         def run():
-            P.gemm_set_config(16, args.group, ph)
+            P.gemm_set_config(16, args.group, ph, -1, split)
             fn()
         return run
 
@@ -53,6 +57,7 @@ def main():
         w = (torch.empty(N, K, device="cuda").uniform_(-1, 1, generator=g) / K ** 0.5).bfloat16()
         b = torch.empty(N, device="cuda").uniform_(-1, 1, generator=g).bfloat16()
         var = {"pp": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0)),
+               "pp_ns": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0), 0),
                "r3": with_cfg(0, lambda: P.gemm_tn(a, w, b, 0)),
                "blas": lambda: F.linear(a, w, b)}
         extra = {}
@@ -62,12 +67,15 @@ def main():
             wdt = (torch.empty(N, K, device="cuda").uniform_(-1, 1, generator=g) / N ** 0.5).bfloat16()
             acc = torch.zeros(N, device="cuda")
             extra = {"pp_gelu": with_cfg(4, lambda: P.gemm_tn(a, w, b, 1)),
+                     "pp_ns_gelu": with_cfg(4, lambda: P.gemm_tn(a, w, b, 1), 0),
                      "r3_gelu": with_cfg(0, lambda: P.gemm_tn(a, w, b, 1)),
                      "blas_gelu": lambda: P.act_fwd(F.linear(a, w, b), 1),
                      "pp_dgelu": with_cfg(4, lambda: P.gemm_tn(dy, wdt, None, 3, pre, acc)),
                      "r3_dgelu": with_cfg(0, lambda: P.gemm_tn(dy, wdt, None, 3, pre, acc)),
                      "blas_dgelu": lambda: P.act_bwd_bias(dy @ wdt.t(), pre, 1, acc)}
         var.update(extra)
+        if args.no_r3:
+            var = {k: v for k, v in var.items() if not k.startswith("r3")}
         for fn in var.values():  # warm-up (TunableOp off: library heuristics)
             for _ in range(3):
                 fn()
@@ -75,14 +83,14 @@ def main():
         for _ in range(args.rounds):
             for k, fn in var.items():
                 ts[k].append(once(fn, args.reps))
-        P.gemm_set_config(16, 4, 4)  # the default kernel
+        P.gemm_set_config(16, 4, 4, -1, 0)  # the default kernel
         fl = 2 * M * N * K
         rec = {"M": M, "N": N, "K": K}
         for k, v in ts.items():
             med = statistics.median(v)
             rec[k + "_us"] = round(med, 1)
             rec[k + "_min_us"] = round(min(v), 1)
-            if k in ("pp", "r3", "blas"):
+            if k in ("pp", "pp_ns", "r3", "blas"):
                 rec[k + "_tflops"] = round(fl / med / 1e6, 1)
         rec["pp_vs_blas"] = round(rec["blas_us"] / rec["pp_us"], 3)
         print(json.dumps(rec), flush=True)

@@ -308,7 +308,13 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     of32 = check_grad(*bias_acc, "bias_acc");
     TORCH_CHECK(bias_acc->numel() == N && bias_acc->is_contiguous(), "gemm_tn: bias_acc [N]");
   }
+  Tensor splitws;
   if (M > 0) {
+    const int64_t wsf = pllm::gemm_split_ws_floats((int)M, (int)N, (int)K, (int)epi, (int)T);
+    if (wsf > 0) {
+      splitws = at::empty({wsf}, a.options().dtype(at::kFloat));
+      g.splitws = splitws.data_ptr<float>();
+    }
     pllm::gemm_tn(g, (int)epi, cur_stream());
     if (bias_acc)
       pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M, (int)K), (int)N, bias_acc->data_ptr(), of32, true,
@@ -979,8 +985,10 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
-  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1) -> ()",
-        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc) { pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc); });
+  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int split=-1) -> ()",
+        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc, int64_t sp) {
+          pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc, (int)sp);
+        });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });

@@ -370,6 +370,40 @@ PLLM_DEV void pp_stamp(const PPCtx& c, int idx) {
   }
 }
 
+// The desynchronising split's parked partial tile: this wave's 128 accumulator floats per lane in
+// their register order, 32 x 1 KiB coalesced stores into the workgroup's 256 KiB workspace slot (as
+// many as an end-of-tile epilogue: the following counted waits still hold), added back before the
+// same tile's epilogue at the end of the workgroup's work.
+// (not with the column-sum epilogues 3 / 4: their branch around the 16 aux rows spills)
+template <int EPI, bool QE>
+constexpr bool kPPSplit = !QE && EPI != 3 && EPI != 4;
+PLLM_DEV __amdgpu_buffer_rsrc_t pp_park_rsrc(const PPCtx& c, int lid) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(c.g->splitws + (int64_t)lid * PT * PT), (short)0, PT * PT * 4,
+                                           0x00020000);
+}
+PLLM_DEV void pp_park(f32x4 (&acc)[4][8], const PPCtx& c, int lid) {
+  const __amdgpu_buffer_rsrc_t r = pp_park_rsrc(c, lid);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), r,
+                                             (uint32_t)((((c.w * 4 + i) * 8 + j) * 64 + c.lane) * 16), 0, 0);
+}
+PLLM_DEV void pp_unpark(f32x4 (&acc)[4][8], const PPCtx& c, int lid) {
+  const __amdgpu_buffer_rsrc_t r = pp_park_rsrc(c, lid);
+  // the accumulators START from the parked partial (the finishing segment's first K-tile is a
+  // plain accumulating one).  Device-scope loads: the partial was written by this same wave long
+  // before, only this CU's L1 could hold a stale copy of the lines
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      acc[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                r, (uint32_t)((((c.w * 4 + i) * 8 + j) * 64 + c.lane) * 16), 0, 16));
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // Descriptors of the DMA target K-tile's A and B panels (256 rows from the K-tile's first column,
 // range-checked: rows past M / N read zeros); valid = false: empty ranges (the same instructions
 // issue, so the counted waits stay exact; nothing reads that slot again).  Built once per K-tile:
@@ -783,11 +817,34 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     if (lid & 1)
       for (int i = 0; i < S / 3; ++i) __builtin_amdgcn_s_sleep(63);  // ~4k cycles each
   }
+  // Segments: (tile, K-tile range, mode).  Normally one full-K segment per tile.  With the
+  // desynchronising split (end-of-tile epilogues; odd workgroups with >= 2 tiles; a workspace), the
+  // workgroup first runs the SECOND half of the K range of its last tile and parks that partial
+  // fp32 tile in its own workspace slot, then its other tiles, then the first half of the last tile,
+  // adding the parked partial before the epilogue: same work per workgroup, but its tile
+  // boundaries -- and the epilogue store bursts -- fall half a tile after the even workgroups'
+  // (measured: every CU storing its 128 KiB at once parked both wave groups ~4.5k cycles a tile)
+  const int R = (ntiles - lid + G - 1) / G;
+  const bool split = kPPSplit<EPI, QE> && g.splitws != nullptr && (lid & 1) && R >= 2 && S >= 4;
+  const int nseg = split ? R + 1 : R;
+  auto segment = [&](int i, int& t, int& kb, int& ke, int& mode) {  // mode 0 full, 1 park, 2 finish
+    if (!split) {
+      t = lid + i * G, kb = 0, ke = S, mode = 0;
+    } else if (i == 0) {
+      t = lid + (R - 1) * G, kb = S / 2, ke = S, mode = 1;
+    } else if (i == R) {
+      t = lid + (R - 1) * G, kb = 0, ke = S / 2, mode = 2;
+    } else {
+      t = lid + (i - 1) * G, kb = 0, ke = S, mode = 0;
+    }
+  };
   int tm, tn;
-  pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
-  // prologue: K-tile 0 of the first tile, all four piece groups, fully landed
+  // prologue: the first segment's first K-tile, all four piece groups, fully landed
   {
-    const PPSrd srd = pp_srds<EPI>(c, tm, tn, 0, true);
+    int t0, kb0, ke0, mode0;
+    segment(0, t0, kb0, ke0, mode0);
+    pp_tile(t0, tiles_m, tiles_n, g.group_m, tm, tn);
+    const PPSrd srd = pp_srds<EPI>(c, tm, tn, kb0, true);
     pp_issue<0, EPI>(c, srd, 0);
     pp_issue<1, EPI>(c, srd, 0);
     pp_issue<2, EPI>(c, srd, 0);
@@ -806,26 +863,47 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   float dsum[4] = {0.f, 0.f, 0.f, 0.f};
   int s = 0;
   PPEpi pe{tm, tn, false};  // the previous tile (none yet)
-  for (int t = lid; t < ntiles; t += G) {
+  for (int i = 0; i < nseg; ++i) {
+    int t, kb, ke, mode;
+    segment(i, t, kb, ke, mode);
     pp_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
     const PPEpi ce{tm, tn, true};
-    const bool more = t + G < ntiles;
-    int tm2 = tm, tn2 = tn;
-    if (more) pp_tile(t + G, tiles_m, tiles_n, g.group_m, tm2, tn2);
-    // K-tile kt's DMA carries K-tile kt + 1, or the next tile's K-tile 0 after the last one.
-    // K-tile 0 is peeled: its MFMAs start the accumulators from zero, each quadrant right after
-    // that quadrant's epilogue of the previous tile
-    // (S >= 2: gemm_tn sends K < 128 to the round-3 kernel)
-    pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, 1, true, pe, ce, dsum);
+    const bool more = i + 1 < nseg;
+    int tm2 = tm, tn2 = tn, kb2 = 0;
+    if (more) {
+      int t2, ke2, mode2;
+      segment(i + 1, t2, kb2, ke2, mode2);
+      pp_tile(t2, tiles_m, tiles_n, g.group_m, tm2, tn2);
+    }
+    // K-tile kt's DMA carries K-tile kt + 1, or the next segment's first K-tile after the last one.
+    // The first K-tile is peeled: its MFMAs start the accumulators from zero (with quadrant
+    // epilogues: each quadrant right after that quadrant's epilogue of the previous tile).
+    // (>= 2 K-tiles per segment: gemm_tn sends K < 128 to the round-3 kernel; split needs S >= 4)
+    if constexpr (kPPSplit<EPI, QE>) {
+      if (mode == 2) {
+        pp_unpark(acc, c, lid);
+        pp_ktile<false, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
+      } else {
+        pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
+      }
+    } else {
+      pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
+    }
     ++s;
-    for (int kt = 1; kt + 1 < S; ++kt, ++s)
+    for (int kt = kb + 1; kt + 1 < ke; ++kt, ++s)
       pp_ktile<false, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kt + 1, true, pe, ce, dsum);
-    pp_ktile<false, true, EPI, QE>(c, acc, fa, fb, smem, s, tm2, tn2, 0, more, pe, ce, dsum);
+    pp_ktile<false, true, EPI, QE>(c, acc, fa, fb, smem, s, tm2, tn2, kb2, more, pe, ce, dsum);
     ++s;
     if constexpr (!QE) {
       // the end-of-tile epilogue, in this wave's next LOAD slot
-      if constexpr (EPI == 7) pp_epilogue_swiglu(acc, g, tm, tn, c.wr, c.wc, lane);
-      else pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
+      __builtin_amdgcn_sched_barrier(0);
+      if (mode == 1) {
+        pp_park(acc, c, lid);
+      } else {
+        if constexpr (EPI == 7) pp_epilogue_swiglu(acc, g, tm, tn, c.wr, c.wc, lane);
+        else pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
+      }
+      __builtin_amdgcn_sched_barrier(0);
     }
     pe = ce;
   }
@@ -865,6 +943,15 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
 }  // namespace
 
 namespace pllm {
+
+int64_t gemm_pp_split_ws_floats(int M, int N, int K, int epi, int ctas) {
+  const int nt = epi == 7 ? 128 : PT;
+  const int ntiles = ((M + PT - 1) / PT) * ((N + nt - 1) / nt);
+  const int grid = ntiles < ctas ? ntiles : ctas;
+  // end-of-tile epilogues only, >= 4 K-tiles, and odd workgroups with >= 2 tiles must exist
+  if (gemm_pp_quad_epilogue(K, epi) || epi == 3 || epi == 4 || K / PBK < 4 || ntiles < 2 * grid || grid < 2) return 0;
+  return (int64_t)grid * PT * PT;
+}
 
 // EPI 3 / 4 column-sum partial rows: 4 per tile row with quadrant epilogues, 2 otherwise
 int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 4 : 2) * ((M + PT - 1) / PT); }

@@ -117,14 +117,18 @@ struct GemmArgs {
   int group_m;  // set by gemm_tn
   float* delta;  // epilogue 6: [M / T, N / 64, T] row sums of C * aux per 64-column head
   int T;         // epilogue 6: rows per sequence
+  float* splitws;  // gemm_pp: per-workgroup 256x256 fp32 parking slots of the desynchronising split
+                   // (gemm_pp_split_ws_floats; nullptr = no split)
 };
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 // phased: 0 single-phase, 2 asym DMA, 4 ping-pong kernel (gemm_pp.hip); reserve_cus >= 0: CUs left
 // free by the persistent grids (collectives in flight), -1 keeps the current setting
-void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1);
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, int split = -1);
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
 int gemm_pp_colsum_groups(int M, int K);
 bool gemm_pp_quad_epilogue(int K, int epi);
+int64_t gemm_pp_split_ws_floats(int M, int N, int K, int epi, int ctas);  // 0: the call does not split
+int64_t gemm_split_ws_floats(int M, int N, int K, int epi, int T);  // gemm.hip: for the current config
 int gemm_colsum_groups(int M, int K);  // column-sum partial rows (epi 3 / 4) of the kernel serving K
 bool gemm_uses_pp(int K, int epi, int T);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
