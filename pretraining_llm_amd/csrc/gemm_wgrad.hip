@@ -538,15 +538,30 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 
 namespace pllm {
 
-// Variant selection (wgrad_set_mfma: 16 / 32 = that MFMA shape with every wave loading, 116 / 132 =
-// the asymmetric-DMA kernel, 0 = per shape).  Same-box A/B (profiles/r3_wgrad_asym_ab.md): the
-// asymmetric DMA is +1-8 % over the symmetric kernel; 16x16x32 wins everywhere except the LM-head
-// shapes (P = vocabulary), where 32x32x16 does (+0.5-4 %)
+// Variant selection (wgrad_set_mfma): 0 = default -- the ping-pong kernel of wgrad_pp.hip where it
+// applies (fp32 gradient target), else this file's kernel per shape; 100 = this file's kernel per
+// shape; 16 / 32 = that MFMA shape with every wave loading, 116 / 132 = the asymmetric-DMA kernel.
+// Same-box A/B of this file's variants (profiles/r3_wgrad_asym_ab.md): the asymmetric DMA is +1-8 %
+// over the symmetric kernel; 16x16x32 wins everywhere except the LM-head shapes (P = vocabulary),
+// where 32x32x16 does (+0.5-4 %)
 static int g_wgrad_mfma = 0;
 static int g_wgrad_asym = 1;
+static bool g_wgrad_pp = true;
 void wgrad_set_mfma(int mf) {
-  g_wgrad_mfma = mf == 0 ? 0 : ((mf % 100) == 16 ? 16 : 32);
+  g_wgrad_pp = mf == 0;
+  const int v = mf % 100;
+  g_wgrad_mfma = v == 0 ? 0 : (v == 16 ? 16 : 32);
   g_wgrad_asym = mf == 0 || mf >= 100;
+}
+
+static int wgrad_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
 }
 
 // A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices
@@ -612,6 +627,22 @@ bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);
+  if (g_wgrad_pp && out_f32 && wgrad_pp_supported(M, P, Q, S, slice)) {
+    const bool fb = bpart != nullptr && bout != nullptr;
+    wgrad_pp(dy, lda, x, ldb, M, P, Q, S, slice, part, (float*)out, accumulate, fb ? bpart : nullptr,
+             wgrad_num_cus(), st);
+    if (fb) {
+      const dim3 bg((unsigned)((P / 8 + 255) / 256));
+      if (bout_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);
+      else hipLaunchKernelGGL(wgrad_reduce_kernel<false>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);
+    }
+    if (S > 1) {
+      const int64_t PQ = (int64_t)P * Q;
+      const dim3 rg((unsigned)((PQ / 8 + 255) / 256));
+      hipLaunchKernelGGL(wgrad_reduce_kernel<true>, rg, dim3(256), 0, st, part, S, PQ, out, (int)accumulate);
+    }
+    return fb;
+  }
   const int mfma = g_wgrad_mfma != 0 ? g_wgrad_mfma : (P >= 16384 ? 32 : 16);
   // the bias gradient rides along only on the 16x16x32 kernel (see wgrad_kernel)
   const bool fuse_b = bpart != nullptr && bout != nullptr && mfma == 16 && !kWgradLoaders;

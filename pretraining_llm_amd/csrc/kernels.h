@@ -138,6 +138,10 @@ void wgrad_force_slices(int s);
 // bpart / bout (optional): also the bias gradient db[P] (+)= column sums of dY, through an fp32 [S][P]
 // workspace (S = wgrad_bias_slices); returns whether it was computed (16x16x32 kernel only)
 int wgrad_bias_slices(int M, int P, int Q);
+// wgrad_pp.hip: the ping-pong weight-gradient kernel (fp32 targets; wgrad() dispatches to it)
+bool wgrad_pp_supported(int M, int P, int Q, int S, int slice);
+void wgrad_pp(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, int S, int slice,
+              float* part, float* out, bool accumulate, float* bpart, int ctas, hipStream_t st);
 bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool out_f32, bool accumulate, hipStream_t st, float* bpart = nullptr, void* bout = nullptr,
            bool bout_f32 = false);

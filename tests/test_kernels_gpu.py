@@ -977,3 +977,34 @@ def _rope_case(D, Hkv):
     rq, rk, rv = ops._split_qkv(qkvf.grad, H, Hkv, D)
     for a, b, n in ((gq, rq, "q"), (gk, rk, "k"), (gv, rv, "v")):
         assert _rel(a, b) < 3e-2, (n, _rel(a, b))
+
+
+@pytest.mark.parametrize("M,P,Q", [(4096, 4096, 8192), (8192, 2304, 768), (4096, 50304, 768), (2048, 200, 136)])
+def test_wgrad_pp_kernel(M, P, Q):
+    """The ping-pong weight-gradient kernel (csrc/wgrad_pp.hip; wgrad's default for fp32 targets):
+    persistent workgroups with several (slice, tile) items each, edge tiles, the split-K slab and the
+    single-slice accumulate paths -- against fp64 math and against the one-barrier kernel it replaces."""
+    torch.manual_seed(23)
+    dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
+    x = torch.randn(M, Q, device=DEV).bfloat16()
+    w0 = torch.randn(P, Q, device=DEV)
+    ref = w0.double() + dy.double().t() @ x.double()
+    acc = w0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc)
+    assert _rel(acc.double(), ref) < 1e-5, _rel(acc.double(), ref)
+    acc2 = w0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc2)
+    assert torch.equal(acc, acc2)  # deterministic
+    try:
+        torch.ops.pllm.wgrad_set_mfma(100)  # the one-barrier kernel
+        acc3 = w0.clone()
+        torch.ops.pllm.wgrad(dy, x, acc3)
+    finally:
+        torch.ops.pllm.wgrad_set_mfma(0)
+    assert _rel(acc.double(), acc3.double()) < 1e-6
+    # bias gradient on the side (all-ones MFMAs on the first column tile's items)
+    b0 = torch.randn(P, device=DEV)
+    acc4, bacc = w0.clone(), b0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc4, bacc)
+    assert torch.equal(acc4, acc)
+    assert _rel(bacc.double(), b0.double() + dy.double().sum(0)) < 1e-6
