@@ -199,6 +199,9 @@ constexpr bool kFwdDma = PLLM_FWD_DMA != 0;
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
 #endif
+#ifndef PLLM_BWD_QSPREAD
+#define PLLM_BWD_QSPREAD 0  // 1: the next Q / dO tile's DMA pieces spread over the dQ task's MFMAs (A/B build)
+#endif
 #ifndef PLLM_BWD_STAGGER
 #define PLLM_BWD_STAGGER 0  // diagnostic: s_sleep units (64 cycles) for waves 4-7 per backward iteration
 #endif
@@ -214,10 +217,14 @@ constexpr bool kFwdSched = PLLM_FWD_SCHED != 0;
 #ifndef PLLM_FWD_MINW
 #define PLLM_FWD_MINW 2  // __launch_bounds__ minimum waves per SIMD of the forward (A/B builds)
 #endif
+#ifndef PLLM_FWD128_NW
+#define PLLM_FWD128_NW 4  // waves per workgroup at D = 128 (8: 256 query rows share each K/V tile)
+#endif
 
 template <int D>
 struct FwdCfg {
-  static constexpr int NW = 4;
+  static constexpr int NW = D == 128 ? PLLM_FWD128_NW : 4;
+  static constexpr int MINB = NW == 8 ? 1 : PLLM_FWD_MINW;  // launch bounds: 2 waves per SIMD either way
   static constexpr int QB = D <= 64 ? PLLM_FWD64_QB : 1;
   static constexpr int BM = NW * 32 * QB, BN = 64;
   static constexpr int CPR = D / 8;   // 16 B chunks per row
@@ -229,7 +236,7 @@ struct FwdCfg {
 };
 
 template <int D, bool ROPE, bool PIPE = false, bool V3 = false>
-__global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArgs a) {
+__global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_kernel(AttnFwdArgs a) {
   static_assert(!PIPE || (FwdCfg<D>::QB == 2 && !ROPE), "pipelined tile loop: QB = 2, no fused RoPE");
   static_assert(!V3 || (!PIPE && !ROPE), "sum-checked softmax: plain tile loop, no fused RoPE");
   using C = FwdCfg<D>;
@@ -298,9 +305,9 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
   const int ntiles = (kv_end + BN - 1) / BN;
 
   // chunk i of this thread: row c / CPR, column chunk (c % CPR2) + (i odd ? CPR2 : 0) with
-  // c = tid + 256 * (i / 2) and CPR2 = CPR / 2, so a thread holds both RoPE partners of a row
-  constexpr int CPR2 = CPR / 2;
-  constexpr int NPAIR = (BN * CPR2 + 255) / 256;
+  // c = tid + NTH * (i / 2) and CPR2 = CPR / 2, so a thread holds both RoPE partners of a row
+  constexpr int CPR2 = CPR / 2, NTH = 64 * NW;
+  constexpr int NPAIR = (BN * CPR2 + NTH - 1) / NTH;
   u32x4 kr[2 * NPAIR], vr[2 * NPAIR];
   // K / V rows by buffer loads through a per-tile descriptor (scalar base = the tile's first
   // row): rows past S read as zeros (range check), per-lane offsets loop-invariant
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
     const auto vrs = rows_rsrc(vp + (int64_t)kv0 * a.v_st, a.S - kv0, a.v_st, D);
 #pragma unroll
     for (int i = 0; i < 2 * NPAIR; ++i) {
-      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
+      const int c = tid + NTH * (i / 2), row = c / CPR2, col = c % CPR2 + (i & 1) * CPR2;
       if (c < BN * CPR2) {
         kr[i] = buf_ld16(krs, (uint32_t)(row * (int)a.k_st + col * 8) * 2u);
         vr[i] = buf_ld16(vrs, (uint32_t)(row * (int)a.v_st + col * 8) * 2u);
@@ -325,7 +332,7 @@ __global__ __launch_bounds__(256, PLLM_FWD_MINW) void attn_fwd_kernel(AttnFwdArg
     uint16_t* Vb = smem + 2 * TILE + vbuf * TILE;
 #pragma unroll
     for (int i = 0; i < 2 * NPAIR; i += 2) {
-      const int c = tid + 256 * (i / 2), row = c / CPR2, col = c % CPR2;
+      const int c = tid + NTH * (i / 2), row = c / CPR2, col = c % CPR2;
       if (c >= BN * CPR2) continue;
       if (ROPE) {
         const int key = t * BN + row;
@@ -1063,6 +1070,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // Pieces of 1 KiB = QRP rows; lane l fills row blk * QRP + l / CPR at chunk position l % CPR,
   // which holds logical chunk (l % CPR) ^ I::f(row) (the image's swizzle, applied to the source)
   constexpr bool QDMA = ROPE == 0;
+  constexpr bool kQSpread = QDMA && PLLM_BWD_QSPREAD != 0;
   constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW;
   static_assert(2 * QNP % C::NW == 0, "Q/dO pieces per wave");
   u32x4 qr[QDMA ? 1 : 2 * QPAIR], dor[QDMA ? 1 : 2 * QPAIR];
@@ -1074,20 +1082,25 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
   }
   const unsigned lds_q = (unsigned)(uintptr_t)Ql, lds_o = (unsigned)(uintptr_t)Ol;
-  auto qdma = [&](int it) {
+  auto qdma_srd = [&](int it, i32x4v& qs, i32x4v& os) {
     const int h = hk * G + it / per_head;
     const int q0 = (qb_start + it % per_head) * BQ;
     const int rows = a.T - q0;
-    const i32x4v qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
-                             (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
-    const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
-                             (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
+    qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
+                (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
+    os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
+                (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
+  };
+  auto qdma_piece = [&](const i32x4v& qs, const i32x4v& os, int k) {
     const int wu = __builtin_amdgcn_readfirstlane(w);  // wave-uniform piece numbers: scalar descriptors
+    const int pc = wu * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
+  };
+  auto qdma = [&](int it) {
+    i32x4v qs, os;
+    qdma_srd(it, qs, os);
 #pragma unroll
-    for (int k = 0; k < QPPW; ++k) {
-      const int pc = wu * QPPW + k, img = pc / QNP, blk = pc % QNP;
-      blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
-    }
+    for (int k = 0; k < QPPW; ++k) qdma_piece(qs, os, k);
   };
   float rc = 0.f;
   auto gload = [&](int it) {
@@ -1392,9 +1405,15 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
           const bool live = qn + (tid & (BQ - 1)) < a.T;
           rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
         }
-        qdma(it + 1);
+        if constexpr (!kQSpread) qdma(it + 1);
       }
     }
+    // kQSpread: the pieces go out one per BK / 16 / QPPW MFMAs of the dQ task below (a burst of
+    // them here cost ~190 cycles each, profiles/r3_attn_bwd_stamps.md)
+    i32x4v nqs, nos;
+    int nsent = 0;
+    const bool spread = kQSpread && it + 1 < total;
+    if (spread) qdma_srd(it + 1, nqs, nos);
     PLLM_BSTAMP(4);
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
@@ -1422,6 +1441,13 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
         const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
+        if constexpr (kQSpread) {
+          constexpr int EVERY = BK / 16 / QPPW;
+          if (spread && ti == 0 && ks % EVERY == EVERY - 1) {
+            qdma_piece(nqs, nos, ks / EVERY);
+            ++nsent;
+          }
+        }
       }
       float lo[8], hi[8];
 #pragma unroll
@@ -1433,6 +1459,13 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       dqv[ti][1] = pack8(hi);
       dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
                 ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
+    }
+    if constexpr (kQSpread) {
+      // a wave whose dQ task did not run (ragged last query block) sends its pieces here
+      if (spread && nsent == 0) {
+#pragma unroll
+        for (int k = 0; k < QPPW; ++k) qdma_piece(nqs, nos, k);
+      }
     }
     PLLM_BSTAMP(5);
 #if PLLM_BWD_STAMPS
@@ -1938,13 +1971,13 @@ static bool attn_fwd_pipe() {
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
-  const dim3 grid(nqb * a.B * a.H);
-  if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, dim3(256), 0, st, a);
-  else if constexpr (PLLM_FWD_V3 != 0) hipLaunchKernelGGL((attn_fwd_kernel<D, false, false, true>), grid, dim3(256), 0, st, a);
+  const dim3 grid(nqb * a.B * a.H), blk(64 * FwdCfg<D>::NW);
+  if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, blk, 0, st, a);
+  else if constexpr (PLLM_FWD_V3 != 0) hipLaunchKernelGGL((attn_fwd_kernel<D, false, false, true>), grid, blk, 0, st, a);
   else if constexpr (FwdCfg<D>::QB == 2) {
-    if (attn_fwd_pipe()) hipLaunchKernelGGL((attn_fwd_kernel<D, false, true>), grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);
-  } else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, dim3(256), 0, st, a);
+    if (attn_fwd_pipe()) hipLaunchKernelGGL((attn_fwd_kernel<D, false, true>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, blk, 0, st, a);
+  } else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, blk, 0, st, a);
 }
 
 template <int D, int ROPE>
