@@ -734,16 +734,22 @@ class _AttnProjFn(torch.autograd.Function):
 
 # PLLM_ATTN_PROJ_FUSED=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
 FUSED_ATTN_PROJ = os.environ.get("PLLM_ATTN_PROJ_FUSED", "1") == "1"
+# head dims served by it; PLLM_ATTN_PROJ_D128=1 adds D = 128 (llama: two 64-column delta halves per
+# head, added by the role-split backward).  Off by default: llama-1.3B 274.4 vs 273.0 ms per step
+# (profiles/r4_attn_experiments.md) -- the ping-pong projection dgrad is slower than hipBLASLt's by
+# about what the delta pre-pass costs
+ATTN_PROJ_HEAD_DIMS = (64, 128) if os.environ.get("PLLM_ATTN_PROJ_D128", "0") == "1" else (64,)
 
 
 def attn_proj_ok(qkv, n_head: int, n_kv_head: int, w, b) -> bool:
-    """The fused attention + output projection path (_AttnProjFn): HIP training path, head dim 64."""
+    """The fused attention + output projection path (_AttnProjFn): HIP training path, head dim 64 or
+    128 (128: epilogue 6's per-64-column delta halves, added by the role-split backward)."""
     if not FUSED_ATTN_PROJ or not torch.is_grad_enabled() or not (_hip_op("attn", qkv) and _hip_op("linear", qkv)):
         return False
     B, T, W = qkv.shape
     D = W // (n_head + 2 * n_kv_head)
     C_out = w.shape[0]
-    return (D == 64 and B * T > 0 and tuple(w.shape) == (C_out, n_head * D) and C_out % 64 == 0
+    return (D in ATTN_PROJ_HEAD_DIMS and B * T > 0 and tuple(w.shape) == (C_out, n_head * D) and C_out % 64 == 0
             and w.is_contiguous() and _aligned16(w) and (b is None or b.is_contiguous()))
 
 

@@ -245,14 +245,18 @@ def test_gemm_tn_attn_delta_epilogue(B, T, H, phased):
 
 @pytest.mark.parametrize("bias", [True, False])
 @pytest.mark.parametrize("ext", [False, True])
-def test_attn_proj_fused_matches_unfused(bias, ext):
+@pytest.mark.parametrize("D,Hkv", [(64, 4), (128, 4), (128, 2)])
+def test_attn_proj_fused_matches_unfused(bias, ext, D, Hkv, monkeypatch):
     """ops.attention_proj (projection dgrad + delta in one GEMM, attention backward without its
-    delta pass) vs attention_packed + linear."""
+    delta pass; D = 128: two 64-column delta halves added by the role-split kernel, GQA too) vs
+    attention_packed + linear."""
     from pretraining_llm_amd import ops
+    if D not in ops.ATTN_PROJ_HEAD_DIMS:
+        monkeypatch.setattr(ops, "ATTN_PROJ_HEAD_DIMS", (64, 128))  # the opt-in D = 128 path
     torch.manual_seed(23)
-    B, T, H, D = 2, 256, 4, 64
+    B, T, H = 2, 256, 4
     C = H * D
-    qkv0 = (0.5 * torch.randn(B, T, 3 * C, device=DEV)).bfloat16()
+    qkv0 = (0.5 * torch.randn(B, T, (H + 2 * Hkv) * D, device=DEV)).bfloat16()
     w0 = (torch.randn(C, C, device=DEV) / C ** 0.5).bfloat16()
     b0 = (0.1 * torch.randn(C, device=DEV)).bfloat16() if bias else None
     dy = torch.randn(B, T, C, device=DEV).bfloat16()
@@ -262,10 +266,10 @@ def test_attn_proj_fused_matches_unfused(bias, ext):
         qkv, w, b = ps
         with torch.enable_grad():
             if fused:
-                assert ops.attn_proj_ok(qkv, H, H, w, b)
-                y = ops.attention_proj(qkv, H, H, w, b, bias_grad_external=ext)
+                assert ops.attn_proj_ok(qkv, H, Hkv, w, b)
+                y = ops.attention_proj(qkv, H, Hkv, w, b, bias_grad_external=ext)
             else:
-                y = ops.linear(ops.attention_packed(qkv, H, H), w, b, bias_grad_external=ext)
+                y = ops.linear(ops.attention_packed(qkv, H, Hkv), w, b, bias_grad_external=ext)
             y.backward(dy)
         return y.detach(), [p.grad if p is not None else None for p in ps]
 
