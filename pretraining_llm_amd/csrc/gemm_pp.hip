@@ -51,6 +51,13 @@
 #define PLLM_PP_EXP 0
 #endif
 constexpr bool kPPStamps = (PLLM_PP_EXP & 64) != 0;
+#ifndef PLLM_PP_DMA_MFMA
+#define PLLM_PP_DMA_MFMA 0
+#endif
+// the K-tile DMA pieces issued between the phase's own MFMAs (after MFMAs 4 and 12) instead of in
+// its LOAD segment: an LDS-DMA piece costs ~60 cycles among bare MFMAs but 100-185 in a LOAD segment
+// that also carries fragment reads (MI355X_MICROARCH.md, per-instruction constants)
+constexpr bool kPPDmaMfma = PLLM_PP_DMA_MFMA != 0;
 constexpr bool kPPStaticPrio = (PLLM_PP_EXP & 128) != 0;  // bit 7: waves 4-7 at priority 1, no flips
 constexpr int kPPStampN = 52;  // per wave
 
@@ -447,21 +454,33 @@ PLLM_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
   o[3] = r[3];
   return o;
 }
+// the descriptor and LDS address of piece group PH (pieces q = 0, 1 at + 1 KiB)
 template <int PH, int EPI = 0>
-PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
+PLLM_DEV void pp_group(const PPCtx& c, const PPSrd& srd, int sl, i32x4v& r, unsigned& lds0) {
   // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
   constexpr bool isA = PH == 0 || PH == 3;
   const int blk0 = pp_blk0<PH>(c.w);
-  const unsigned lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG) + blk0 * 512) * 2u;
-  if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
+  lds0 = c.lds + (unsigned)(sl * PSLOT + (isA ? 0 : PIMG) + blk0 * 512) * 2u;
   // groups 2 / 3: the pieces of groups 1 / 0 shifted by 4 (B: 32 rows) / 8 (A: 64 rows) pieces
   // (EPI 7: group 2 = the up rows of group 1's columns, from their own panel)
-  const i32x4v r = PH < 2 ? (isA ? srd.a : srd.b)
-                   : (EPI == 7 && !isA) ? srd.b2
-                                        : srd_shift(isA ? srd.a : srd.b,
-                                                    (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
+  r = PH < 2 ? (isA ? srd.a : srd.b)
+             : (EPI == 7 && !isA) ? srd.b2
+                                  : srd_shift(isA ? srd.a : srd.b,
+                                              (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
+}
+template <int PH>
+PLLM_DEV void pp_piece(const PPCtx& c, const i32x4v& r, unsigned lds0, int q) {
+  constexpr bool isA = PH == 0 || PH == 3;
+  if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
+  blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
+}
+template <int PH, int EPI = 0>
+PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
+  i32x4v r;
+  unsigned lds0;
+  pp_group<PH, EPI>(c, srd, sl, r, lds0);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
+  for (int q = 0; q < 2; ++q) pp_piece<PH>(c, r, lds0, q);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -653,7 +672,8 @@ constexpr int pp_phase_ops(bool F, bool L, int q) {
 // the DMA wait of phase PH (piece group PH - 2 landed): everything issued in phases PH - 1, PH
 template <int EPI, bool QE, bool F, bool L, int PH>
 constexpr int pp_dma_wait() {
-  int n = pp_phase_ops<EPI, QE>(F, L, PH);
+  // (kPPDmaMfma: this phase's 2 DMA ops are issued after the wait, among its MFMAs)
+  int n = pp_phase_ops<EPI, QE>(F, L, PH) - (kPPDmaMfma ? 2 : 0);
   n += PH >= 1 ? pp_phase_ops<EPI, QE>(F, L, PH - 1) : pp_phase_ops<EPI, QE>(false, F, 3);
   if constexpr (!QE) {
     if (F && PH < 2) n += kEndStores<EPI>;  // the end-of-tile epilogue's stores
@@ -712,7 +732,13 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
               sb + c.rdB[k] + (unsigned)((PIMG + (wc * 64 + 16 * (2 * p + ii)) * PBK) * 2)));
     }
   }
-  pp_issue<PH, EPI>(c, srd, nsl);
+  i32x4v gr;
+  unsigned glds;
+  pp_group<PH, EPI>(c, srd, nsl, gr, glds);
+  if constexpr (!kPPDmaMfma) {
+    pp_piece<PH>(c, gr, glds, 0);
+    pp_piece<PH>(c, gr, glds, 1);
+  }
   pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
   pp_vmwait<pp_dma_wait<EPI, QE, FIRST, LAST, PH>()>();
   pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
@@ -732,6 +758,14 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
           f32x4& a = acc[2 * p + ii][4 * jh + jj];
           if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
           else a = mfma16(fb[k][ii], fa[k][jj], a);
+          if constexpr (kPPDmaMfma) {
+            const int idx = 8 * k + 2 * jj + ii;
+            if (idx == 3 || idx == 11) {
+              __builtin_amdgcn_sched_barrier(0);
+              pp_piece<PH>(c, gr, glds, idx == 3 ? 0 : 1);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
         }
     if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(0);
   }
