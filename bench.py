@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs the persistent fused-epilogue GEMM grid leaves free (for RCCL kernels overlapping "
                          "the backward at N > 1); 0 = every CU")
+    ap.add_argument("--gemm-persistent", default="auto", choices=["auto", "0", "1"],
+                    help="persistent ping-pong GEMM / weight-gradient grids; auto: at one GPU only "
+                         "(train/graph.py gemm_persistent_policy)")
     ap.add_argument("--graph-collectives", action="store_true",
                     help="with N > 1 and --cuda-graph auto: capture the RCCL all-reduces inside the step's hipGraph "
                          "(opt-in, as the Trainer's graph_collectives=True; default: eager hook-overlapped step)")
@@ -136,9 +139,12 @@ def main(argv=None):
         from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
         tuned = enable_tuned_gemms(dev.index or 0, tune_missing=args.tune_missing and args.warmup > 0)
     ops.set_backend(args.backend)
+    gemm_persistent = None  # (the hand-written GEMMs' grids; HIP path only)
     if args.backend == "auto" and not cpu:
         ops._lib.require()  # the HIP path must be the one that runs: fail loudly if the extension is missing
-        ops.gemm_config(reserve_cus=args.reserve_cus)
+        from pretraining_llm_amd.train.graph import gemm_persistent_policy
+        gemm_persistent = gemm_persistent_policy(world, args.gemm_persistent)
+        ops.gemm_config(reserve_cus=args.reserve_cus, persistent=gemm_persistent)
 
     torch.manual_seed(1234)
     mcfg = get_preset(args.model)
@@ -253,6 +259,7 @@ def main(argv=None):
                        "tokens_per_step": B * T * world, "tuned_gemms": tuned, "cuda_graph": bool(args.cuda_graph),
                        "step_mode": "graph" if args.cuda_graph else "eager",
                        "gemm_reserve_cus": args.reserve_cus,
+                       "gemm_persistent": gemm_persistent,
                        "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev))),
                        "checkpointed_blocks": int(model.checkpointed_blocks(torch.empty(B, T, device=dev)))},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),

@@ -989,9 +989,9 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
-  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int split=-1) -> ()",
-        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc, int64_t sp) {
-          pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc, (int)sp);
+  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int split=-1, int persistent=-1) -> ()",
+        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc, int64_t sp, int64_t pe) {
+          pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc, (int)sp, (int)pe);
         });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });

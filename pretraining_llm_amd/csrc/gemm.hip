@@ -404,12 +404,16 @@ static int g_gemm_reserve = 0;
 // measured 6-10 % SLOWER at K = 768 (293 -> 311 us, GELU 376 -> 411), +2.5 % only on the plain
 // 32768x11008x2048 (profiles/r4_gemm_pp.md): the store bursts are not what a half-tile shift fixes
 static int g_gemm_split = 0;
-void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus, int split) {
+// 0: the persistent kernels (gemm_pp / wgrad_pp / this file's) launch one workgroup per tile instead
+// of one per CU, so the hardware deals tiles to whichever CUs are free (e.g. beside RCCL kernels)
+static int g_gemm_persistent = 1;
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus, int split, int persistent) {
   if (mfma == 16 || mfma == 32) g_gemm_mfma = mfma;
   if (group_m > 0) g_gemm_group_m = group_m;
   if (phased >= 0) g_gemm_phased = phased;
   if (reserve_cus >= 0) g_gemm_reserve = reserve_cus;
   if (split >= 0) g_gemm_split = split;
+  if (persistent >= 0) g_gemm_persistent = persistent;
 }
 
 // column-sum partial rows of the EPI 3 / 4 bias gradient: 2 per tile row here, 4 (one per
@@ -431,9 +435,12 @@ static int num_cus() {
 }
 
 static int gemm_ctas() {
-  // persistent grid: one workgroup per CU, minus the CUs reserved for concurrent collectives
+  // persistent grid: one workgroup per CU, minus the CUs reserved for concurrent collectives;
+  // non-persistent: no cap (one workgroup per tile / work item)
+  if (!g_gemm_persistent) return 1 << 30;
   return num_cus() - g_gemm_reserve > 8 ? num_cus() - g_gemm_reserve : 8;
 }
+int gemm_grid_cap() { return gemm_ctas(); }
 
 // workspace (floats) of the ping-pong kernel's desynchronising tile split for this call; 0 when
 // the call does not split

@@ -554,16 +554,6 @@ void wgrad_set_mfma(int mf) {
   g_wgrad_asym = mf == 0 || mf >= 100;
 }
 
-static int wgrad_num_cus() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-  }
-  return n;
-}
-
 // A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices
 static int g_wgrad_force_s = 0;
 void wgrad_force_slices(int s) { g_wgrad_force_s = s > 0 ? s : 0; }
@@ -630,7 +620,7 @@ bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   if (g_wgrad_pp && out_f32 && wgrad_pp_supported(M, P, Q, S, slice)) {
     const bool fb = bpart != nullptr && bout != nullptr;
     wgrad_pp(dy, lda, x, ldb, M, P, Q, S, slice, part, (float*)out, accumulate, fb ? bpart : nullptr,
-             wgrad_num_cus(), st);
+             gemm_grid_cap(), st);
     if (fb) {
       const dim3 bg((unsigned)((P / 8 + 255) / 256));
       if (bout_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);

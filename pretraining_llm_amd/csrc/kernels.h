@@ -124,7 +124,9 @@ struct GemmArgs {
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 // phased: 0 single-phase, 2 asym DMA, 4 ping-pong kernel (gemm_pp.hip); reserve_cus >= 0: CUs left
 // free by the persistent grids (collectives in flight), -1 keeps the current setting
-void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, int split = -1);
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, int split = -1, int persistent = -1);
+// workgroup cap of the persistent GEMM grids (CUs minus reserve_cus; 2^30 when non-persistent)
+int gemm_grid_cap();
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
 int gemm_pp_colsum_groups(int M, int K);
 bool gemm_pp_quad_epilogue(int K, int epi);

@@ -55,9 +55,11 @@ def load(raise_on_error: bool = False) -> bool:
                 kern = os.environ.get("PLLM_GEMM_KERNEL")
                 res = os.environ.get("PLLM_GEMM_RESERVE_CUS")
                 spl = os.environ.get("PLLM_GEMM_SPLIT")
-                if kern or res or spl:
+                per = os.environ.get("PLLM_GEMM_PERSISTENT")  # 0|1: persistent GEMM grids
+                if kern or res or spl or per:
                     torch.ops.pllm.gemm_set_config(0, 0, GEMM_KERNELS.get(kern, -1) if kern else -1,
-                                                   int(res) if res else -1, int(spl) if spl else -1)
+                                                   int(res) if res else -1, int(spl) if spl else -1,
+                                                   int(per) if per else -1)
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box

@@ -57,6 +57,21 @@ def graph_step_policy(*, cuda: bool, world: int, dist_backend: Optional[str], ze
     return True, None
 
 
+def gemm_persistent_policy(world: int, setting="auto") -> bool:
+    """Whether the ping-pong GEMM / weight-gradient kernels use persistent grids (one workgroup per CU
+    walking a tile list) -- shared by ``Trainer`` (config ``gemm_persistent``) and ``bench.py``
+    (``--gemm-persistent``).  ``auto``: persistent at world 1 (0.6 % faster than one workgroup per
+    tile, profiles/r4_gemm_persistent_ab.txt); at world > 1 one workgroup per tile, because the
+    RCCL kernels of the overlapped all-reduces occupy CUs, and a persistent workgroup that cannot
+    start there would hold its whole tile list back (a workgroup of these kernels fills a CU's
+    registers, so nothing shares the CU with it)."""
+    if setting in (None, "auto"):
+        return world <= 1
+    if isinstance(setting, str):
+        return setting.lower() in ("1", "true", "yes", "on")
+    return bool(setting)
+
+
 class GraphedTrainStep:
     def __init__(self, model, optimizer, engine, batch: int, seq: int, device, warmup: int = 2, accum: int = 1):
         self.model, self.opt, self.engine = model, optimizer, engine

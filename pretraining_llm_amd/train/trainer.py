@@ -102,8 +102,11 @@ class Trainer:
                                         enabled=loss_scaling_default(dtype_name) if ls is None else bool(ls))
         self.tuned_gemms = False
         if self.device.type == "cuda":
-            # CUs the persistent fused-epilogue GEMM grid leaves to RCCL kernels (world > 1); 0 = all
-            ops.gemm_config(reserve_cus=int(self.cfg.get("gemm_reserve_cus", 0)))
+            # CUs the persistent fused-epilogue GEMM grid leaves to RCCL kernels (world > 1); 0 = all;
+            # persistent grids at world 1 only (train/graph.py gemm_persistent_policy)
+            from .graph import gemm_persistent_policy
+            ops.gemm_config(reserve_cus=int(self.cfg.get("gemm_reserve_cus", 0)),
+                            persistent=gemm_persistent_policy(self.di.world_size, self.cfg.get("gemm_persistent", "auto")))
         if self.device.type == "cuda" and self.cfg.get("tuned_gemms", True):
             # the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/), as bench.py uses them
             from ..utils.gemm_tuning import enable_tuned_gemms

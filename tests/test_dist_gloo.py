@@ -231,3 +231,11 @@ def test_trainer_and_bench_share_the_step_policy():
     assert g.graph_step_policy(cuda=True, world=1, dist_backend=None) == (True, None)
     assert not g.graph_step_policy(cuda=True, world=1, dist_backend=None, zero=True)[0]
     assert not g.graph_step_policy(cuda=False, world=1, dist_backend=None)[0]
+    # persistent GEMM grids: world 1 only by default, the same decision in both
+    assert "gemm_persistent_policy(" in inspect.getsource(tr.Trainer.__init__)
+    assert "gemm_persistent_policy(" in inspect.getsource(bench.main)
+    assert g.gemm_persistent_policy(1) and g.gemm_persistent_policy(1, "auto")
+    for world in (2, 4, 8):
+        assert not g.gemm_persistent_policy(world)
+        assert g.gemm_persistent_policy(world, "1") and g.gemm_persistent_policy(world, True)
+    assert not g.gemm_persistent_policy(1, "0")

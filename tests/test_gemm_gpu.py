@@ -385,3 +385,31 @@ def test_gemm_tn_swiglu_forward_epilogue(M, F, K):
     unf = torch.ops.pllm.swiglu_fwd(gu)
     assert (a.float() - unf.float()).abs().max().item() <= 2 ** -7 * unf.float().abs().max().item()
     assert torch.equal(torch.ops.pllm.gemm_tn(x, w1, None, 7)[0], a)  # deterministic
+
+
+def test_gemm_non_persistent_grids():
+    """gemm_config(persistent=False): one workgroup per tile / work item (the hardware deals them to
+    free CUs, e.g. beside RCCL kernels) -- the same results bit for bit as the persistent grids, for the
+    fused-epilogue GEMM and the weight-gradient kernel, with several tiles / items per CU."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(43)
+    M, N, K = 16384, 3072, 768
+    a = torch.randn(M, K, device=DEV).bfloat16()
+    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    bias = torch.randn(N, device=DEV).bfloat16()
+    dy = (0.3 * torch.randn(M, 2304, device=DEV)).bfloat16()
+    w0 = torch.randn(2304, K, device=DEV)
+    outs = []
+    try:
+        for pers in (True, False):
+            ops.gemm_config(persistent=pers)
+            g = torch.ops.pllm.gemm_tn(a, b, bias, 1)
+            acc = w0.clone()
+            torch.ops.pllm.wgrad(dy, a, acc)
+            outs.append((g, acc))
+    finally:
+        ops.gemm_config(persistent=True)
+    (g1, w1), (g2, w2) = outs
+    assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
+    assert torch.equal(w1, w2)
+    assert _rel(w1.double(), w0.double() + dy.double().t() @ a.double()) < 1e-5
