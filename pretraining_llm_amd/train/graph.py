@@ -19,6 +19,7 @@ step over the fp32 accumulated gradient scaled by 1/accum.  The static inputs ar
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -66,6 +67,9 @@ def gemm_persistent_policy(world: int, setting="auto") -> bool:
     start there would hold its whole tile list back (a workgroup of these kernels fills a CU's
     registers, so nothing shares the CU with it)."""
     if setting in (None, "auto"):
+        env = os.environ.get("PLLM_GEMM_PERSISTENT")  # A/B override of the automatic choice
+        if env:
+            return env == "1"
         return world <= 1
     if isinstance(setting, str):
         return setting.lower() in ("1", "true", "yes", "on")
