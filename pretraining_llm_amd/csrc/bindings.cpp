@@ -535,6 +535,29 @@ void scale_(Tensor& x, const Tensor& s) {
   if (x.numel()) pllm::scale_bf16(x.data_ptr(), s.data_ptr<float>(), x.numel(), cur_stream());
 }
 
+// ring attention: fold a partial block result (o [B, T, H, D] bf16, lse [B, H, T] fp32) into the
+// fp32 accumulators o_acc [B, T, H, D] / lse_acc [B, H, T] in place (views with any row strides)
+void lse_merge_(Tensor& o_acc, Tensor& lse_acc, const Tensor& o, const Tensor& lse) {
+  TORCH_CHECK(o_acc.scalar_type() == at::kFloat && lse_acc.scalar_type() == at::kFloat && lse.scalar_type() == at::kFloat,
+              "lse_merge_: o_acc / lse_acc / lse fp32");
+  check_bf16(o, "o");
+  TORCH_CHECK(o_acc.dim() == 4 && o.sizes() == o_acc.sizes(), "lse_merge_: o_acc / o [B, T, H, D]");
+  const int64_t B = o.size(0), T = o.size(1), H = o.size(2), D = o.size(3);
+  TORCH_CHECK(lse_acc.dim() == 3 && lse_acc.size(0) == B && lse_acc.size(1) == H && lse_acc.size(2) == T &&
+                  lse.sizes() == lse_acc.sizes(), "lse_merge_: lse_acc / lse [B, H, T]");
+  TORCH_CHECK(D % 8 == 0 && D <= 128 && o_acc.stride(3) == 1 && o.stride(3) == 1, "lse_merge_: D % 8, unit head stride");
+  for (int d = 0; d < 3; ++d)
+    TORCH_CHECK(o_acc.stride(d) % 4 == 0 && o.stride(d) % 8 == 0, "lse_merge_: 16-B aligned rows");
+  check_aligned16(o_acc, "o_acc");
+  check_aligned16(o, "o");
+  const int64_t st[12] = {o_acc.stride(0), o_acc.stride(1), o_acc.stride(2), lse_acc.stride(0), lse_acc.stride(1),
+                          lse_acc.stride(2), o.stride(0), o.stride(1), o.stride(2), lse.stride(0), lse.stride(1),
+                          lse.stride(2)};
+  if (o.numel())
+    pllm::lse_merge(o_acc.data_ptr<float>(), lse_acc.data_ptr<float>(), o.data_ptr(), lse.data_ptr<float>(), st,
+                    (int)B, (int)T, (int)H, (int)D, cur_stream());
+}
+
 // ---------------------------------------------------------------- cross entropy
 // returns per-row losses (fp32, 0 for ignored rows); if dlogits is given it is
 // overwritten with d(mean loss)/dlogits (it may alias logits).
@@ -1005,6 +1028,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("rope(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T, int pos_offset, bool inverse) -> Tensor");
   m.def("rope_qk(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
+  m.def("lse_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o, Tensor lse) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
@@ -1034,6 +1058,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("rope", rope);
   m.impl("rope_qk", rope_qk);
   m.impl("scale_", scale_);
+  m.impl("lse_merge_", lse_merge_);
   m.impl("cross_entropy", cross_entropy);
   m.impl("adamw_", adamw_);
   m.impl("sumsq", sumsq);

@@ -199,6 +199,52 @@ __global__ __launch_bounds__(256) void scale_kernel(uint16_t* __restrict__ x, co
   }
 }
 
+
+// Ring attention's LSE merge (parallel/context.py _merge; the reference has no context parallelism,
+// its attention is /root/reference/src/models/attention.py:47-57): a partial block result (o bf16,
+// lse fp32) folded into the fp32 accumulators in place --
+//   new = logaddexp(lse_acc, lse); o_acc = o_acc e^(lse_acc - new) + o e^(lse - new); lse_acc = new
+// (a weight whose exponent is -inf - -inf is 0, as torch's nan_to_num).  One lane per 8 head
+// elements; a row's D / 8 <= 16 lanes sit in one wave, which reads lse_acc before its lane 0
+// writes it.  Replaces five fp32 torch passes per block pair.
+struct LseMergeArgs {
+  float* o_acc;
+  float* lse_acc;
+  const uint16_t* o;
+  const float* lse;
+  int64_t oa_b, oa_t, oa_h, la_b, la_h, la_t, o_b, o_t, o_h, l_b, l_h, l_t;
+  int B, T, H, D;
+};
+__global__ __launch_bounds__(256) void lse_merge_kernel(LseMergeArgs a) {
+  const int cpr = a.D / 8;
+  const int64_t gid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = gid / cpr;
+  const int c = (int)(gid - row * cpr);
+  if (row >= (int64_t)a.B * a.T * a.H) return;
+  const int h = (int)(row % a.H);
+  const int64_t bt = row / a.H;
+  const int t = (int)(bt % a.T), b = (int)(bt / a.T);
+  float* lap = a.lse_acc + b * a.la_b + h * a.la_h + t * a.la_t;
+  const float la = *lap, lb = a.lse[b * a.l_b + h * a.l_h + t * a.l_t];
+  const float mx = fmaxf(la, lb);
+  const float nw = mx == -INFINITY ? -INFINITY : mx + log1pf(__expf(-fabsf(la - lb)));
+  const float wa = la == -INFINITY ? 0.f : __expf(la - nw);
+  const float wb = lb == -INFINITY ? 0.f : __expf(lb - nw);
+  float* oa = a.o_acc + b * a.oa_b + t * a.oa_t + h * a.oa_h + 8 * c;
+  float x[8];
+  unpack8(*reinterpret_cast<const u32x4*>(a.o + b * a.o_b + t * a.o_t + h * a.o_h + 8 * c), x);
+  f32x4* o4 = reinterpret_cast<f32x4*>(oa);
+  f32x4 v0 = o4[0], v1 = o4[1];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v0[e] = v0[e] * wa + x[e] * wb;
+    v1[e] = v1[e] * wa + x[4 + e] * wb;
+  }
+  o4[0] = v0;
+  o4[1] = v1;
+  if (c == 0) *lap = nw;
+}
+
 }  // namespace
 
 namespace pllm {
@@ -255,6 +301,14 @@ void rope(const void* in, void* out, const float* cosb, const float* sinb, size_
 void scale_bf16(void* x, const float* s, size_t n, hipStream_t st) {
   const size_t nv = n / 8;
   hipLaunchKernelGGL(scale_kernel, dim3(ew_grid(nv)), dim3(256), 0, st, (uint16_t*)x, s, nv);
+}
+
+void lse_merge(float* o_acc, float* lse_acc, const void* o, const float* lse, const int64_t* st, int B, int T, int H,
+               int D, hipStream_t stream) {
+  LseMergeArgs a{o_acc, lse_acc, (const uint16_t*)o, lse, st[0], st[1], st[2], st[3], st[4], st[5], st[6],
+                 st[7], st[8], st[9], st[10], st[11], B, T, H, D};
+  const int64_t n = (int64_t)B * T * H * (D / 8);
+  hipLaunchKernelGGL(lse_merge_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, a);
 }
 
 }  // namespace pllm

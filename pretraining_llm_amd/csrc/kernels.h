@@ -83,6 +83,9 @@ void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, h
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
           int n_rot, int D, int pos_offset, bool inverse, hipStream_t st, int out_heads = 0);
 void scale_bf16(void* x, const float* s, size_t n, hipStream_t st);
+// ring-attention LSE merge; st: element strides of o_acc (b, t, h), lse_acc (b, h, t), o (b, t, h), lse (b, h, t)
+void lse_merge(float* o_acc, float* lse_acc, const void* o, const float* lse, const int64_t* st, int B, int T, int H,
+               int D, hipStream_t stream);
 
 // cross_entropy.hip
 void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,

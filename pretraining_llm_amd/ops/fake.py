@@ -95,6 +95,10 @@ def register() -> None:
     def _(x, s):
         return None
 
+    @_reg("lse_merge_")
+    def _(o_acc, lse_acc, o, lse):
+        return None
+
     @_reg("cross_entropy")
     def _(logits, targets, dlogits, ignore_index, inv_n=None):
         return logits.new_empty((logits.shape[0],), dtype=f32)

@@ -131,7 +131,13 @@ def _split(x: torch.Tensor, n: int) -> List[torch.Tensor]:
 
 
 def _merge(o_acc, lse_acc, o, lse):
-    """In-place LSE merge of a partial block result (o [B,T,H,D], lse [B,H,T]) into fp32 accumulators."""
+    """In-place LSE merge of a partial block result (o [B,T,H,D], lse [B,H,T]) into fp32 accumulators
+    (the HIP path: one fused kernel, csrc/elementwise.hip lse_merge_kernel)."""
+    from .. import ops
+    if (ops._hip(o) and o.dtype == torch.bfloat16 and o.shape[-1] % 8 == 0 and o.shape[-1] <= 128
+            and o.stride(-1) == 1 and o_acc.stride(-1) == 1):
+        ops._ops().lse_merge_(o_acc, lse_acc, o, lse.float())
+        return
     lse = lse.float()
     new = torch.logaddexp(lse_acc, lse)
     a = torch.exp(lse_acc - new).nan_to_num_(0.0).transpose(1, 2).unsqueeze(-1)

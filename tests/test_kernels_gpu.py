@@ -1008,3 +1008,29 @@ def test_wgrad_pp_kernel(M, P, Q):
     torch.ops.pllm.wgrad(dy, x, acc4, bacc)
     assert torch.equal(acc4, acc)
     assert _rel(bacc.double(), b0.double() + dy.double().sum(0)) < 1e-6
+
+
+@pytest.mark.parametrize("D", [32, 64, 128])
+def test_lse_merge_kernel(D):
+    """Ring attention's fused LSE merge (lse_merge_) vs the torch formula of parallel/context.py, on
+    strided accumulator views (a T-chunk of a bigger buffer) with fully masked (-inf) rows on either side."""
+    torch.manual_seed(29)
+    B, T, H = 2, 96, 4
+    full = torch.randn(B, 2 * T, H, D, device=DEV)
+    o_acc = full[:, T:]                      # strided view, as the per-chunk accumulators
+    lfull = torch.randn(B, H, 2 * T, device=DEV)
+    lse_acc = lfull[:, :, T:]
+    o = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    lse = torch.randn(B, H, T, device=DEV)
+    lse_acc[:, :, :5] = float("-inf")        # accumulator rows not yet seen
+    lse[:, :, 3:8] = float("-inf")           # block rows fully masked (rows 3, 4: both)
+    ref_o, ref_l = o_acc.clone(), lse_acc.clone()
+    before = full[:, :T].clone()
+    new = torch.logaddexp(ref_l, lse)
+    a = torch.exp(ref_l - new).nan_to_num_(0.0).transpose(1, 2).unsqueeze(-1)
+    b = torch.exp(lse - new).nan_to_num_(0.0).transpose(1, 2).unsqueeze(-1)
+    ref_o = ref_o * a + o.float() * b
+    torch.ops.pllm.lse_merge_(o_acc, lse_acc, o, lse)
+    assert torch.allclose(lse_acc, new, rtol=1e-5, atol=1e-5, equal_nan=True)
+    assert torch.allclose(o_acc, ref_o, rtol=1e-5, atol=1e-5)
+    assert torch.equal(full[:, :T], before)  # the rest of the buffer is untouched
