@@ -1,4 +1,7 @@
-// Weight-gradient GEMM for linear layers on gfx950 MFMA:
+// Weight-gradient GEMM for linear layers on gfx950 MFMA (the one-barrier kernel; since round 4 the
+// default for fp32 gradient targets is the ping-pong kernel of wgrad_pp.hip, dispatched from wgrad()
+// below with the same split-K plan, slab layout and reduce; this kernel serves bf16 targets and
+// wgrad_set_mfma(100 / 16 / 32 / 1xx) A/B runs):
 //     dW[P, Q] (+)= sum_m dY[m, P] * X[m, Q]          (bf16 in, fp32 accumulate)
 // i.e. the reduction runs over the token dimension (M = batch*seq, 65536 for the
 // headline config) while the output is small (768x768 .. 50304x768).  Both operands
