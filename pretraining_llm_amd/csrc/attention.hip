@@ -199,6 +199,9 @@ constexpr bool kFwdDma = PLLM_FWD_DMA != 0;
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
 #endif
+#ifndef PLLM_BWD_QASYM
+#define PLLM_BWD_QASYM 0  // 1: waves 0-3 issue every Q / dO DMA piece, 4-7 start their dQ tasks at once (A/B build)
+#endif
 #ifndef PLLM_BWD_QSPREAD
 #define PLLM_BWD_QSPREAD 0  // 1: the next Q / dO tile's DMA pieces spread over the dQ task's MFMAs (A/B build)
 #endif
@@ -1071,13 +1074,17 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // which holds logical chunk (l % CPR) ^ I::f(row) (the image's swizzle, applied to the source)
   constexpr bool QDMA = ROPE == 0;
   constexpr bool kQSpread = QDMA && PLLM_BWD_QSPREAD != 0;
-  constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW;
+  // kQAsym: the older half of the waves issues every piece (twice as many each) while the SIMD
+  // partners of the other half (priority 1) start their dQ tasks on the matrix pipe
+  constexpr bool kQAsym = QDMA && !kQSpread && PLLM_BWD_QASYM != 0;
+  constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW * (kQAsym ? 2 : 1);
   static_assert(2 * QNP % C::NW == 0, "Q/dO pieces per wave");
   u32x4 qr[QDMA ? 1 : 2 * QPAIR], dor[QDMA ? 1 : 2 * QPAIR];
   uint32_t qvo[QPPW];
+  const bool qloader = !kQAsym || w < C::NW / 2;
 #pragma unroll
   for (int k = 0; k < QPPW; ++k) {
-    const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    const int pc = (kQAsym ? (w % (C::NW / 2)) : w) * QPPW + k, img = pc / QNP, blk = pc % QNP;
     const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
     qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
   }
@@ -1097,6 +1104,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
   };
   auto qdma = [&](int it) {
+    if (!qloader) return;
     i32x4v qs, os;
     qdma_srd(it, qs, os);
 #pragma unroll
