@@ -14,6 +14,12 @@ namespace {
 
 constexpr int CE_THREADS = 512;
 constexpr int CE_WAVES = CE_THREADS / 64;
+#ifndef PLLM_CE_ONLINE
+// 1: each lane's (max, exp-sum) pair merged in ONE block reduction (2 barriers per row instead of 5):
+// 2,524 vs 2,551 us at 65536 x 50304 (bench/ce_bench.py, scripts/gpu/r4_ce1.sh, same box, 3 rounds)
+#define PLLM_CE_ONLINE 1
+#endif
+constexpr bool kCeOnline = PLLM_CE_ONLINE != 0;
 
 template <int CH, bool WRITE_GRAD>
 __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restrict__ logits, int64_t ld,
@@ -24,7 +30,7 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
   // VGPRs for V = 50304 and several blocks fit per CU; exp2 is recomputed in the output
   // pass instead of being stored (VALU is idle in this HBM-bound kernel).
   constexpr float LOG2E = 1.4426950408889634f;
-  __shared__ float scratch[CE_WAVES];
+  __shared__ float scratch[2 * CE_WAVES];
   const int row = blockIdx.x;
   const uint16_t* x = logits + (size_t)row * ld;
   const int nch = V >> 3;
@@ -50,12 +56,66 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
     tv = bf2f(x[tj]);
     m = fmaxf(m, tv);
   }
+  const int64_t t = targets[row];
+  const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
+  float mc, s;
+  if constexpr (kCeOnline) {
+    // the lane's own max, its exp-sum against it, then ONE block reduction of (max, sum) pairs
+    // (2 barriers instead of 4; the target logit is read before any lane can overwrite it)
+    const float xt = (threadIdx.x == 0 && valid) ? bf2f(x[t]) : 0.f;
+    const float ml = m == -INFINITY ? 0.f : m * LOG2E;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
+    float sl = 0.f;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) {
+      float f[8];
+      unpack8(v[k], f);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sl += fast_exp2(__builtin_fmaf(f[j], LOG2E, -ml));
+    }
+    if (tj < V) sl += fast_exp2(__builtin_fmaf(tv, LOG2E, -ml));
+    // wave: pairwise (m, s) merge, then across waves through LDS
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(m, o, 64), s2 = __shfl_xor(sl, o, 64);
+      const float mn = fmaxf(m, m2);
+      const float mnl = mn == -INFINITY ? 0.f : mn * LOG2E;
+      sl = (m == -INFINITY ? 0.f : sl * fast_exp2(m * LOG2E - mnl)) +
+           (m2 == -INFINITY ? 0.f : s2 * fast_exp2(m2 * LOG2E - mnl));
+      m = mn;
+    }
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    if (l == 0) {
+      scratch[w] = m;
+      scratch[CE_WAVES + w] = sl;
+    }
+    __syncthreads();
+    float mb = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < CE_WAVES; ++i) mb = fmaxf(mb, scratch[i]);
+    mc = mb * LOG2E;
+    float sb = 0.f;
+#pragma unroll
+    for (int i = 0; i < CE_WAVES; ++i) {
+      const float mi = scratch[i];
+      if (mi != -INFINITY) sb += scratch[CE_WAVES + i] * fast_exp2(mi * LOG2E - mc);
+    }
+    m = mb;
+    s = sb;
+#pragma unroll
+    for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
+    if (threadIdx.x == 0) PLLM_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
+    if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - xt) : 0.f;
+    if (!WRITE_GRAD) return;
+    __syncthreads();  // lane 0's target-logit read (consumed by the loss above) precedes every store
+  } else {
   m = block_max<CE_WAVES>(m, scratch);
-  const float mc = m * LOG2E;
+  mc = m * LOG2E;
   // opaque to the optimiser: keeps only the packed row live across the passes
 #pragma unroll
   for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
-  float s = 0.f;
+  s = 0.f;
 #pragma unroll
   for (int k = 0; k < CH; ++k) {
     float f[8];
@@ -67,12 +127,11 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
   s = block_sum<CE_WAVES>(s, scratch);
 #pragma unroll
   for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
-  const int64_t t = targets[row];
-  const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
   if (threadIdx.x == 0) PLLM_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
   if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - bf2f(x[t])) : 0.f;
   if (!WRITE_GRAD) return;
   __syncthreads();  // every lane has read its logits before in-place overwrite (x may alias dlogits)
+  }
   const float in = *inv_n;
   const float scale = valid ? in / s : 0.f;
   uint16_t* dx = dlogits + (size_t)row * ld;
