@@ -103,11 +103,13 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         cmd = [hipcc, *COMMON_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []), "-c", src, "-o", obj]
         jobs_list.append((obj, [src, *headers], cmd))
-    bobj = os.path.join(BUILD, "bindings.o")
+    # torch-facing translation units: bindings.cpp (op registration) and blaslt.cpp (hipBLASLt epilogues)
     py_inc = sysconfig.get_paths()["include"]
-    bcmd = [hipcc, *COMMON_FLAGS, "-c", "-x", "hip", bind_src, "-o", bobj, f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-            "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1", *[f"-I{p}" for p in inc], f"-I{py_inc}"]
-    jobs_list.append((bobj, [bind_src, *headers], bcmd))
+    for src in [bind_src] + sorted(p for p in glob.glob(os.path.join(CSRC, "*.cpp")) if p != bind_src):
+        bobj = os.path.join(BUILD, os.path.splitext(os.path.basename(src))[0] + ".o")
+        bcmd = [hipcc, *COMMON_FLAGS, "-c", "-x", "hip", src, "-o", bobj, f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+                "-DUSE_ROCM=1", "-D__HIP_PLATFORM_AMD__=1", *[f"-I{p}" for p in inc], f"-I{py_inc}"]
+        jobs_list.append((bobj, [src, *headers], bcmd))
     todo = [(o, c) for (o, d, c) in jobs_list if force or _needs(o, d)]
     if todo:
         with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
@@ -119,7 +121,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = False, debug: bool
     objs = [o for (o, _, _) in jobs_list]
     if force or todo or _needs(OUT, objs):
         lcmd = [hipcc, "-shared", f"--offload-arch={ARCH}", *objs, "-o", OUT + ".tmp", f"-L{lib}", "-lc10", "-lc10_hip",
-                "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{lib}"]
+                "-ltorch", "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt", f"-Wl,-rpath,{lib}"]
         _run(lcmd)
         os.replace(OUT + ".tmp", OUT)
     return OUT

@@ -282,6 +282,11 @@ FUSED_MLP = _FM in ("1", "all", "bwd")
 FUSED_MLP_FWD = _FM in ("1", "all")
 # PLLM_FUSED_SWIGLU_FWD=1|0: the llama up-projection with its SwiGLU in the GEMM epilogue (epilogue 7)
 FUSED_SWIGLU_FWD = _os.environ.get("PLLM_FUSED_SWIGLU_FWD", "1") == "1"
+# PLLM_LT_RELU=1|0: the ReLU MLP's up-projection (reference architecture) with bias + ReLU in hipBLASLt's
+# epilogue (csrc/blaslt.cpp) instead of the library GEMM + act_fwd pass (bench/gelu_epi_bench.py:
+# 394 vs 494 us at the ref-3b shape).  GELU has no such path: the library build that ships with torch has
+# no GELU epilogue with the pre-activation output the backward needs (HIPBLASLT_EPILOGUE_GELU_AUX*)
+LT_RELU_FWD = _os.environ.get("PLLM_LT_RELU", "1") == "1"
 
 
 def fused_mlp_ok(x, w1, b1, w2, act: str) -> bool:
@@ -313,7 +318,13 @@ class _FusedMLPFn(torch.autograd.Function):
     def forward(ctx, x, w1, b1, w2, b2, gelu, out_bias_ext):
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
-        if not FUSED_MLP_FWD:
+        if not FUSED_MLP_FWD and not gelu and LT_RELU_FWD:
+            # ReLU in hipBLASLt's own bias epilogue: one pass writes the activation (the
+            # backward needs only its sign); relu commutes with the bf16 rounding, so the result
+            # equals the separate pass
+            a = _ops().gemm_lt(x2.contiguous(), w1, b1, 2, not torch.are_deterministic_algorithms_enabled())[0]
+            ctx.save_for_backward(x2, a)
+        elif not FUSED_MLP_FWD:
             pre = F.linear(x2, w1, b1)
             a = _ops().act_fwd(pre, 1 if gelu else 0)
             if gelu:

@@ -54,6 +54,15 @@ def register() -> None:
             return dy.new_empty((0,))
         return dy.new_empty((dy.shape[1], x.shape[1]))
 
+    @_reg("gemm_lt")
+    def _(x, w, bias, epi, tune=True):
+        M, N = x.shape[0], w.shape[0]
+        return x.new_empty((M, N)), x.new_empty((M, N) if epi == 1 else (0,))
+
+    @_reg("gemm_lt_out")
+    def _(x, w, bias, out, tune=True):
+        return None
+
     @_reg("gemm_tn")
     def _(a, b, bias, epi, aux=None, bias_acc=None, T=0):
         M, N = a.shape[0], b.shape[0]

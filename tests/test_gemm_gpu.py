@@ -413,3 +413,71 @@ def test_gemm_non_persistent_grids():
     assert torch.equal(g1[0], g2[0]) and torch.equal(g1[1], g2[1])
     assert torch.equal(w1, w2)
     assert _rel(w1.double(), w0.double() + dy.double().t() @ a.double()) < 1e-5
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (300, 520, 128), (4096, 3072, 768), (777, 264, 192)])
+@pytest.mark.parametrize("bias", [False, True])
+def test_gemm_lt_epilogues(M, N, K, bias):
+    """torch.ops.pllm.gemm_lt (hipBLASLt called directly, csrc/blaslt.cpp): plain / bias and bias + ReLU
+    epilogues vs fp32 math; the ``out`` variant writes into a caller's buffer; ReLU equals ReLU of the
+    plain product bit for bit (ReLU commutes with the bf16 rounding)."""
+    torch.manual_seed(5)
+    x = torch.randn(M, K, device=DEV).bfloat16()
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
+    b = (0.1 * torch.randn(N, device=DEV)).bfloat16() if bias else None
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0)
+    y, pre = torch.ops.pllm.gemm_lt(x, w, b, 0)
+    assert y.shape == (M, N) and pre.numel() == 0
+    assert _rel(y, ref) < 1e-2
+    r, _ = torch.ops.pllm.gemm_lt(x, w, b, 2)
+    assert _rel(r, ref.relu()) < 1e-2
+    assert torch.equal(r, y.relu())
+    out = torch.full((M + 3, N), 7.0, device=DEV).bfloat16()
+    torch.ops.pllm.gemm_lt_out(x, w, b, out[1:M + 1])
+    assert torch.equal(out[1:M + 1], y)
+    assert (out[0] == 7).all() and (out[M + 1:] == 7).all()
+    plans = torch.ops.pllm.gemm_lt_plans()
+    assert len(plans) % 7 == 0 and plans
+
+
+def test_gemm_lt_contract_checks():
+    x = torch.randn(64, 128, device=DEV).bfloat16()
+    w = torch.randn(96, 128, device=DEV).bfloat16()
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_lt(x, w[:, :64].contiguous(), None, 0)  # K mismatch
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_lt(x.float(), w, None, 0)  # dtype
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_lt(x, w, torch.zeros(95, device=DEV).bfloat16(), 0)  # bias length
+    with pytest.raises(RuntimeError):
+        torch.ops.pllm.gemm_lt_out(x, w, None, torch.empty(64, 95, device=DEV).bfloat16())
+
+
+@pytest.mark.parametrize("lt", [False, True])
+def test_relu_mlp_lt_forward(lt, monkeypatch):
+    """The reference architecture's ReLU MLP with bias + ReLU in hipBLASLt's epilogue vs the library GEMM +
+    act_fwd pass: same forward and gradients."""
+    from pretraining_llm_amd import ops
+    monkeypatch.setattr(ops, "FUSED_MLP_FWD", False)
+    torch.manual_seed(3)
+    C, Fh = 256, 1024
+    x0 = torch.randn(2, 256, C, device=DEV).bfloat16()
+    w1 = (torch.randn(Fh, C, device=DEV) / C ** 0.5).bfloat16()
+    b1 = (0.1 * torch.randn(Fh, device=DEV)).bfloat16()
+    w2 = (torch.randn(C, Fh, device=DEV) / Fh ** 0.5).bfloat16()
+    b2 = (0.1 * torch.randn(C, device=DEV)).bfloat16()
+    dy = torch.randn(2, 256, C, device=DEV).bfloat16()
+
+    def run(use_lt):
+        monkeypatch.setattr(ops, "LT_RELU_FWD", use_lt)
+        ps = [t.clone().requires_grad_() for t in (x0, w1, b1, w2, b2)]
+        with torch.enable_grad():
+            y = ops.fused_mlp(*ps, "relu")
+            y.backward(dy)
+        return y.detach(), [p.grad for p in ps]
+
+    y0, g0 = run(False)
+    y1, g1 = run(lt)
+    assert _rel(y1, y0) < 2e-3
+    for a, b in zip(g1, g0):
+        assert _rel(a, b) < 2e-3
