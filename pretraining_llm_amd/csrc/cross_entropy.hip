@@ -7,13 +7,14 @@
 // exactly once and, in training, overwritten in place by
 //     dlogits = (softmax(x) - onehot(t)) * inv_n          (inv_n = 1 / #valid)
 // so no probability tensor and no second logits-sized buffer ever exist.
+#include <cstdlib>
+
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-constexpr int CE_THREADS = 512;
-constexpr int CE_WAVES = CE_THREADS / 64;
+constexpr int CE_THREADS = 512;  // default block size (PLLM_CE_THREADS=256|1024: A/B)
 #ifndef PLLM_CE_ONLINE
 // 1: each lane's (max, exp-sum) pair merged in ONE block reduction (2 barriers per row instead of 5):
 // 2,524 vs 2,551 us at 65536 x 50304 (bench/ce_bench.py, scripts/gpu/r4_ce1.sh, same box, 3 rounds)
@@ -21,7 +22,8 @@ constexpr int CE_WAVES = CE_THREADS / 64;
 #endif
 constexpr bool kCeOnline = PLLM_CE_ONLINE != 0;
 
-template <int CH, bool WRITE_GRAD>
+// one row per block: stores of the gradient with the non-temporal hint when NTS (A/B)
+template <int CH, bool WRITE_GRAD, int CE_THREADS = 512, bool NTS = false>
 __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restrict__ logits, int64_t ld,
                                                          const int64_t* __restrict__ targets, int V,
                                                          int ignore_index, float* __restrict__ loss,
@@ -30,6 +32,7 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
   // VGPRs for V = 50304 and several blocks fit per CU; exp2 is recomputed in the output
   // pass instead of being stored (VALU is idle in this HBM-bound kernel).
   constexpr float LOG2E = 1.4426950408889634f;
+  constexpr int CE_WAVES = CE_THREADS / 64;
   __shared__ float scratch[2 * CE_WAVES];
   const int row = blockIdx.x;
   const uint16_t* x = logits + (size_t)row * ld;
@@ -144,7 +147,8 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
 #pragma unroll
       for (int j = 0; j < 8; ++j) f[j] = fast_exp2(__builtin_fmaf(f[j], LOG2E, -mc)) * scale;
       if (valid && (int)(t >> 3) == c) f[t & 7] -= in;
-      st16(dx + c * 8, pack8(f));
+      if constexpr (NTS) __builtin_nontemporal_store(pack8(f), reinterpret_cast<u32x4*>(dx + c * 8));
+      else st16(dx + c * 8, pack8(f));
     }
   }
   if (tj < V) {
@@ -158,18 +162,19 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
 
 namespace pllm {
 
-void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
-                   float* loss, void* dlogits, const float* inv_n, hipStream_t st) {
+template <int NT, bool NTS>
+void ce_launch(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index, float* loss,
+               void* dlogits, const float* inv_n, hipStream_t st) {
   const int nch = V / 8;
-  const int CH = (nch + CE_THREADS - 1) / CE_THREADS;
+  const int CH = (nch + NT - 1) / NT;
   const bool g = dlogits != nullptr;
 #define L(C)                                                                                               \
   do {                                                                                                     \
     if (g)                                                                                                 \
-      hipLaunchKernelGGL((ce_kernel<C, true>), dim3(N), dim3(CE_THREADS), 0, st, (const uint16_t*)logits, ld, \
+      hipLaunchKernelGGL((ce_kernel<C, true, NT, NTS>), dim3(N), dim3(NT), 0, st, (const uint16_t*)logits, ld, \
                          targets, V, ignore_index, loss, (uint16_t*)dlogits, inv_n);                       \
     else                                                                                                   \
-      hipLaunchKernelGGL((ce_kernel<C, false>), dim3(N), dim3(CE_THREADS), 0, st, (const uint16_t*)logits, ld, \
+      hipLaunchKernelGGL((ce_kernel<C, false, NT, NTS>), dim3(N), dim3(NT), 0, st, (const uint16_t*)logits, ld, \
                          targets, V, ignore_index, loss, (uint16_t*)nullptr, inv_n);                       \
   } while (0)
   if (CH <= 1) L(1);
@@ -178,8 +183,31 @@ void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N
   else if (CH <= 8) L(8);
   else if (CH <= 13) L(13);
   else if (CH <= 16) L(16);
-  else L(32);
+  else if (CH <= 26) L(26);
+  else if (CH <= 32) L(32);
+  else if (CH <= 64) L(64);
+  else L(128);
 #undef L
+}
+
+void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
+                   float* loss, void* dlogits, const float* inv_n, hipStream_t st) {
+  // A/B switches (bench/ce_bench.py): PLLM_CE_THREADS (block size), PLLM_CE_NT (non-temporal stores)
+  static const int nt = std::getenv("PLLM_CE_THREADS") ? std::atoi(std::getenv("PLLM_CE_THREADS")) : CE_THREADS;
+  // non-temporal gradient stores: 2,493 vs 2,524 us at 65536 x 50304; 256 threads 2,533, 1024 2,641
+  // (scripts/gpu/r4_ce2.sh, 3 interleaved rounds)
+  static const bool nts = !std::getenv("PLLM_CE_NT") || std::atoi(std::getenv("PLLM_CE_NT")) != 0;
+  const int nch = V / 8;
+  if (nt == 256 && (nch + 255) / 256 <= 128) {
+    if (nts) ce_launch<256, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+    else ce_launch<256, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+  } else if (nt == 1024) {
+    if (nts) ce_launch<1024, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+    else ce_launch<1024, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+  } else {
+    if (nts) ce_launch<512, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+    else ce_launch<512, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+  }
 }
 
 int cross_entropy_max_vocab() { return CE_THREADS * 8 * 32 + CE_THREADS; }
