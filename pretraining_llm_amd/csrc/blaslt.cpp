@@ -103,10 +103,12 @@ Plan make_plan(DevState& ds, int64_t M, int64_t N, int64_t K, int epi, bool bias
   return p;
 }
 
-void run(DevState& ds, Plan& p, int idx, const void* w, const void* x, void* y, void* ws, hipStream_t s) {
+// D = w^T x (+ bias) (+ C when c != nullptr: beta = 1, C laid out as D)
+void run(DevState& ds, Plan& p, int idx, const void* w, const void* x, void* y, const void* c, void* ws,
+         hipStream_t s) {
   const float one = 1.f, zero = 0.f;
-  LT_CHECK(hipblasLtMatmul(ds.handle, p.desc, &one, w, p.a, x, p.b, &zero, y, p.d, y, p.d, &p.cands[idx].algo, ws,
-                           p.cands[idx].workspaceSize, s));
+  LT_CHECK(hipblasLtMatmul(ds.handle, p.desc, &one, w, p.a, x, p.b, c ? &one : &zero, c ? c : y, p.d, y, p.d,
+                           &p.cands[idx].algo, ws, p.cands[idx].workspaceSize, s));
 }
 
 void set_ptrs(Plan& p, const void* bias, void* aux) {
@@ -121,7 +123,7 @@ Tensor workspace(size_t bytes, const Tensor& like) {
 }
 
 // times every candidate (3 launches each after one untimed) on the live operands; returns the fastest
-int autotune(DevState& ds, Plan& p, const Tensor& w, const Tensor& x, void* y, hipStream_t s) {
+int autotune(DevState& ds, Plan& p, const Tensor& w, const Tensor& x, void* y, const void* c, hipStream_t s) {
   size_t wmax = 0;
   for (auto& c : p.cands) wmax = std::max(wmax, c.workspaceSize);
   Tensor ws = workspace(wmax, x);
@@ -131,9 +133,9 @@ int autotune(DevState& ds, Plan& p, const Tensor& w, const Tensor& x, void* y, h
   int best = 0;
   float best_ms = 1e30f;
   for (int i = 0; i < (int)p.cands.size(); ++i) {
-    run(ds, p, i, w.data_ptr(), x.data_ptr(), y, ws.data_ptr(), s);
+    run(ds, p, i, w.data_ptr(), x.data_ptr(), y, c, ws.data_ptr(), s);
     (void)hipEventRecord(e0, s);
-    for (int r = 0; r < 3; ++r) run(ds, p, i, w.data_ptr(), x.data_ptr(), y, ws.data_ptr(), s);
+    for (int r = 0; r < 3; ++r) run(ds, p, i, w.data_ptr(), x.data_ptr(), y, c, ws.data_ptr(), s);
     (void)hipEventRecord(e1, s);
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
@@ -160,9 +162,10 @@ void check_operands(const Tensor& x, const Tensor& w, const std::optional<Tensor
   }
 }
 
-// y = act(x w^T + b) into y [M, N] (row stride N); pre (epi 1): the pre-activation
+// y = act(x w^T + b (+ c)) into y [M, N] (row stride N); pre (epi 1): the pre-activation; c: an
+// [M, N] addend (the residual stream: y = residual + x w^T + b in one rounding)
 void lt_matmul(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias, int64_t epi, bool tune,
-               const Tensor& y, void* pre) {
+               const Tensor& y, void* pre, const void* c = nullptr) {
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   if (M == 0 || N == 0) return;
   const int dev = x.get_device();
@@ -170,7 +173,7 @@ void lt_matmul(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bi
   std::lock_guard<std::mutex> lk(g_mu);
   DevState& ds = g_dev[dev];
   if (!ds.handle) LT_CHECK(hipblasLtCreate(&ds.handle));
-  auto key = std::make_tuple(M, N, K, (int)epi, bias.has_value());
+  auto key = std::make_tuple(M, N, K, (int)epi + (c ? 16 : 0), bias.has_value());
   auto it = ds.plans.find(key);
   if (it == ds.plans.end()) it = ds.plans.emplace(key, make_plan(ds, M, N, K, (int)epi, bias.has_value())).first;
   Plan& p = it->second;
@@ -183,23 +186,30 @@ void lt_matmul(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bi
     if (!tune) {
       idx = p.chosen = 0;
     } else if (cs == hipStreamCaptureStatusNone) {
-      idx = p.chosen = autotune(ds, p, w, x, y.data_ptr(), s);
+      idx = p.chosen = autotune(ds, p, w, x, y.data_ptr(), c, s);
     } else {
       idx = 0;
     }
   }
   Tensor ws = workspace(p.cands[idx].workspaceSize, x);
-  run(ds, p, idx, w.data_ptr(), x.data_ptr(), y.data_ptr(), ws.data_ptr(), s);
+  run(ds, p, idx, w.data_ptr(), x.data_ptr(), y.data_ptr(), c, ws.data_ptr(), s);
 }
 
 // y = act(x w^T + b): x [M, K], w [N, K], bias [N] (all bf16, contiguous); epi 1 also returns the
 // pre-activation x w^T + b (the GELU backward's input), else an empty tensor
 std::tuple<Tensor, Tensor> gemm_lt(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bias, int64_t epi,
-                                   bool tune) {
+                                   bool tune, const std::optional<Tensor>& residual) {
   check_operands(x, w, bias, epi);
+  if (residual) {
+    TORCH_CHECK(epi == 0, "gemm_lt: a residual addend only with epi 0");
+    TORCH_CHECK(residual->is_cuda() && residual->scalar_type() == at::kBFloat16 && residual->is_contiguous() &&
+                    residual->dim() == 2 && residual->size(0) == x.size(0) && residual->size(1) == w.size(0),
+                "gemm_lt: residual [M, N] contiguous bf16");
+  }
   Tensor y = at::empty({x.size(0), w.size(0)}, x.options());
   Tensor pre = epi == 1 ? at::empty({x.size(0), w.size(0)}, x.options()) : at::empty({0}, x.options());
-  lt_matmul(x, w, bias, epi, tune, y, epi == 1 ? pre.data_ptr() : nullptr);
+  lt_matmul(x, w, bias, epi, tune, y, epi == 1 ? pre.data_ptr() : nullptr,
+            residual ? residual->data_ptr() : nullptr);
   return {y, pre};
 }
 
@@ -269,7 +279,7 @@ std::vector<int64_t> gemm_lt_plans() {
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(pllm, m) {
-  m.def("gemm_lt(Tensor x, Tensor w, Tensor? bias, int epi, bool tune=True) -> (Tensor, Tensor)");
+  m.def("gemm_lt(Tensor x, Tensor w, Tensor? bias, int epi, bool tune=True, Tensor? residual=None) -> (Tensor, Tensor)");
   m.def("gemm_lt_out(Tensor x, Tensor w, Tensor? bias, Tensor(a!) out, bool tune=True) -> ()");
   m.def("gemm_lt_plans() -> int[]", &gemm_lt_plans);
   m.def("gemm_lt_probe(int M, int N, int K, int epilogue, int bias_type, int aux_type) -> int", &gemm_lt_probe);

@@ -14,7 +14,7 @@
 
 namespace {
 
-constexpr int CE_THREADS = 512;  // default block size (PLLM_CE_THREADS=256|1024: A/B)
+constexpr int CE_THREADS = 512;
 #ifndef PLLM_CE_ONLINE
 // 1: each lane's (max, exp-sum) pair merged in ONE block reduction (2 barriers per row instead of 5):
 // 2,524 vs 2,551 us at 65536 x 50304 (bench/ce_bench.py, scripts/gpu/r4_ce1.sh, same box, 3 rounds)
@@ -183,31 +183,17 @@ void ce_launch(const void* logits, int64_t ld, const int64_t* targets, int N, in
   else if (CH <= 8) L(8);
   else if (CH <= 13) L(13);
   else if (CH <= 16) L(16);
-  else if (CH <= 26) L(26);
-  else if (CH <= 32) L(32);
-  else if (CH <= 64) L(64);
-  else L(128);
+  else L(32);
 #undef L
 }
 
 void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
                    float* loss, void* dlogits, const float* inv_n, hipStream_t st) {
-  // A/B switches (bench/ce_bench.py): PLLM_CE_THREADS (block size), PLLM_CE_NT (non-temporal stores)
-  static const int nt = std::getenv("PLLM_CE_THREADS") ? std::atoi(std::getenv("PLLM_CE_THREADS")) : CE_THREADS;
-  // non-temporal gradient stores: 2,493 vs 2,524 us at 65536 x 50304; 256 threads 2,533, 1024 2,641
-  // (scripts/gpu/r4_ce2.sh, 3 interleaved rounds)
+  // non-temporal gradient stores: 2,493 vs 2,524 us at 65536 x 50304 (PLLM_CE_NT=0: plain stores);
+  // 256- / 1024-thread blocks measured 2,533 / 2,641 us (scripts/gpu/r4_ce2.sh, 3 interleaved rounds)
   static const bool nts = !std::getenv("PLLM_CE_NT") || std::atoi(std::getenv("PLLM_CE_NT")) != 0;
-  const int nch = V / 8;
-  if (nt == 256 && (nch + 255) / 256 <= 128) {
-    if (nts) ce_launch<256, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-    else ce_launch<256, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-  } else if (nt == 1024) {
-    if (nts) ce_launch<1024, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-    else ce_launch<1024, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-  } else {
-    if (nts) ce_launch<512, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-    else ce_launch<512, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
-  }
+  if (nts) ce_launch<CE_THREADS, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
+  else ce_launch<CE_THREADS, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
 }
 
 int cross_entropy_max_vocab() { return CE_THREADS * 8 * 32 + CE_THREADS; }
