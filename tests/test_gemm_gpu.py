@@ -432,6 +432,9 @@ def test_gemm_lt_epilogues(M, N, K, bias):
     r, _ = torch.ops.pllm.gemm_lt(x, w, b, 2)
     assert _rel(r, ref.relu()) < 1e-2
     assert torch.equal(r, y.relu())
+    res = torch.randn(M, N, device=DEV).bfloat16()
+    s_, _ = torch.ops.pllm.gemm_lt(x, w, b, 0, True, res)  # residual addend (beta = 1)
+    assert _rel(s_, ref + res.float()) < 1e-2
     out = torch.full((M + 3, N), 7.0, device=DEV).bfloat16()
     torch.ops.pllm.gemm_lt_out(x, w, b, out[1:M + 1])
     assert torch.equal(out[1:M + 1], y)
