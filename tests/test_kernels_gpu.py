@@ -872,14 +872,16 @@ def test_graphed_steps_without_host_sync_match_eager():
     assert _rel(o1.master, o2.master) < 2e-2
 
 
-@pytest.mark.parametrize("chunk", [128, 8192])
+@pytest.mark.parametrize("chunk,pipe", [(128, 0), (8192, 0), (8192, 4)])
 @pytest.mark.parametrize("with_bias", [False, True])
-def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
+def test_lm_head_ce_chunked(chunk, pipe, with_bias, monkeypatch):
     """Chunked LM head + CE (logits workspace of `chunk` rows, backward GEMMs and head-bias
     column sums done per chunk in the forward, ragged last chunk) vs fp32 torch; into fp32 flat
-    gradient targets and as plain autograd gradients; no-grad evaluation path too."""
+    gradient targets and as plain autograd gradients; no-grad evaluation path too.  pipe > 1: the
+    CE passes on a side stream beside the neighbouring chunks' GEMMs (ops.CE_PIPE)."""
     from pretraining_llm_amd import ops
     monkeypatch.setattr(ops, "CE_CHUNK_ROWS", chunk)
+    monkeypatch.setattr(ops, "CE_PIPE", pipe)
     torch.manual_seed(28)
     N, C, V = 1000, 256, 50304
     h = (torch.randn(N, C, device=DEV) * 0.5).bfloat16().requires_grad_()
