@@ -801,6 +801,9 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
   if (lid >= ntiles) return;
+  if (g.stagger > 0 && (lid & 1)) {
+    for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   PPCtx c;
   c.g = &g;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -995,7 +998,12 @@ int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 
 // shape 32768 x 11008 x 2048, gpurun_out/r4pp7_bench.jsonl)
 bool gemm_pp_quad_epilogue(int K, int epi) { return K >= 2048 && epi != 5 && epi != 1; }
 
-void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
+static int g_pp_stagger = 0;
+void gemm_pp_set_stagger(int n) { g_pp_stagger = n > 0 ? n : 0; }
+
+void gemm_tn_pp(const GemmArgs& a0, int epi, int ctas, hipStream_t st) {
+  GemmArgs a = a0;
+  a.stagger = g_pp_stagger;
   const int nt = epi == 7 ? 128 : PT;
   const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + nt - 1) / nt);
   if (ntiles == 0) return;

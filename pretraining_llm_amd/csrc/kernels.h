@@ -123,7 +123,9 @@ struct GemmArgs {
   int T;         // epilogue 6: rows per sequence
   float* splitws;  // gemm_pp: per-workgroup 256x256 fp32 parking slots of the desynchronising split
                    // (gemm_pp_split_ws_floats; nullptr = no split)
+  int stagger;     // gemm_pp: odd workgroups start this many x 8128 cycles late (gemm_pp_set_stagger)
 };
+void gemm_pp_set_stagger(int n);  // A/B: de-phase the workgroups' end-of-tile store bursts
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 // phased: 0 single-phase, 2 asym DMA, 4 ping-pong kernel (gemm_pp.hip); reserve_cus >= 0: CUs left
 // free by the persistent grids (collectives in flight), -1 keeps the current setting
