@@ -11,11 +11,15 @@
 // Row-major y[M, N] = x[M, K] w[N, K]^T + b is the column-major product y^T = w^T(op T) x (op N):
 // m = N, n = M, k = K; the bias is per column-major row (per output feature).
 //
+// Workspace: each launch takes the bytes its algorithm asks for from torch's caching allocator on the
+// current stream (so concurrent streams and graph captures never share one).
+//
 // Algorithm choice: the heuristic's candidates for each (M, N, K, epilogue) are timed once on the
 // first eager call (hipEvents on the current stream, 3 launches each) and the fastest is cached; a
 // call inside a hipGraph capture or with tune=false takes the heuristic's first candidate (without
 // caching it, unless tune=false: deterministic runs pin the heuristic's choice).
 #include <ATen/ATen.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
@@ -168,6 +172,7 @@ void lt_matmul(const Tensor& x, const Tensor& w, const std::optional<Tensor>& bi
                const Tensor& y, void* pre, const void* c = nullptr) {
   const int64_t M = x.size(0), K = x.size(1), N = w.size(0);
   if (M == 0 || N == 0) return;
+  const c10::DeviceGuard guard(x.device());  // handle, stream and workspace of x's device
   const int dev = x.get_device();
   hipStream_t s = c10::hip::getCurrentHIPStream().stream();
   std::lock_guard<std::mutex> lk(g_mu);
