@@ -195,7 +195,10 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   }
   int S = 1, slice = 1;
   pllm::wgrad_plan((int)M, (int)P, (int)Q, &S, &slice);
-  Tensor part = at::empty({S > 1 ? S : 0, P, Q}, dy.options().dtype(at::kFloat));
+  const bool of32_pre = out_acc && out_acc->scalar_type() == at::kFloat;
+  Tensor part = at::empty({std::max<int64_t>(pllm::wgrad_ws_floats((int)M, (int)P, (int)Q, of32_pre,
+                                                                   bias_acc.has_value()), 1)},
+                          dy.options().dtype(at::kFloat));
   bool bf32 = false;
   Tensor bpart;
   if (bias_acc) {
@@ -208,7 +211,7 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   bool fused_b = false;
   if (M > 0)
     fused_b = pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
-                          S > 1 ? part.data_ptr<float>() : nullptr, out.data_ptr(), of32, out_acc.has_value(),
+                          part.data_ptr<float>(), out.data_ptr(), of32, out_acc.has_value(),
                           cur_stream(), bias_acc ? bpart.data_ptr<float>() : nullptr,
                           bias_acc ? bias_acc->data_ptr() : nullptr, bf32);
   else if (!out_acc)
@@ -1018,6 +1021,7 @@ TORCH_LIBRARY(pllm, m) {
         });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("gemm_pp_set_stagger(int n) -> ()", [](int64_t n) { pllm::gemm_pp_set_stagger((int)n); });
+  m.def("wgrad_set_hy(int on) -> ()", [](int64_t on) { pllm::wgrad_set_hy((int)on); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");

@@ -68,7 +68,10 @@ constexpr bool kWgradLoaders = PLLM_WGRAD_LOADERS != 0;
 #endif
 constexpr bool kWgradBufLds = PLLM_WGRAD_BUFLDS != 0;
 #ifndef PLLM_WGRAD_XCD_ALIGN
-#define PLLM_WGRAD_XCD_ALIGN 0  // 1: wgrad_plan prefers slice counts giving every XCD whole slices (measured slower in the step)
+#define PLLM_WGRAD_XCD_ALIGN 0
+#ifndef PLLM_WGRAD_HY_DEFAULT
+#define PLLM_WGRAD_HY_DEFAULT 1
+#endif  // 1: wgrad_plan prefers slice counts giving every XCD whole slices (measured slower in the step)
 #endif
 #ifndef PLLM_WGRAD_STAGGER
 #define PLLM_WGRAD_STAGGER 0  // n > 0: waves 4-7 (the SIMD partners of 0-3) issue the next stage's DMA before k-step n
@@ -615,8 +618,33 @@ int wgrad_bias_slices(int M, int P, int Q) {
   return S;
 }
 
+// hybrid weight gradients (wgrad_pp_hy), default on: with more tiles than CUs, whole tiles for the whole
+// rounds and slices only for the last one -- LM head 65536 x 50304 x 768 3,984 vs 4,081 us, 32768 x 50304 x
+// 2048 5,190 vs 5,721 us, GPT-2 step +0.3 %, llama +0.2-0.3 % (profiles/r4_wgrad_hybrid.md).  On the
+// persistent grid only (whole rounds of one tile per CU); with a grid per tile the hardware deals the tiles
+// anyway.  (Full stream-K -- equal K-tile runs per workgroup -- lost 13-47 %: r4_wgrad_stream_k_negative.md)
+static int g_wgrad_hy = PLLM_WGRAD_HY_DEFAULT;
+void wgrad_set_hy(int on) { g_wgrad_hy = on; }
+
+static bool wgrad_use_hy(int M, int P, int Q, bool out_f32, bool bias) {
+  int full, rem, S, skt;
+  return g_wgrad_hy && g_wgrad_pp && out_f32 && !bias && gemm_grid_cap() < (1 << 29) &&
+         wgrad_hy_plan(M, P, Q, gemm_grid_cap(), &full, &rem, &S, &skt);
+}
+
+int64_t wgrad_ws_floats(int M, int P, int Q, bool out_f32, bool bias) {
+  if (wgrad_use_hy(M, P, Q, out_f32, bias)) return wgrad_pp_hy_ws_floats(M, P, Q, gemm_grid_cap());
+  int S, slice;
+  wgrad_plan(M, P, Q, &S, &slice);
+  return S > 1 ? (int64_t)S * P * Q : 0;
+}
+
 bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool out_f32, bool accumulate, hipStream_t st, float* bpart, void* bout, bool bout_f32) {
+  if (wgrad_use_hy(M, P, Q, out_f32, bpart != nullptr && bout != nullptr)) {
+    wgrad_pp_hy(dy, lda, x, ldb, M, P, Q, part, (float*)out, accumulate, gemm_grid_cap(), st);
+    return false;
+  }
   int S, slice;
   wgrad_plan(M, P, Q, &S, &slice);
   const int ntiles = ((P + BT - 1) / BT) * ((Q + BT - 1) / BT);

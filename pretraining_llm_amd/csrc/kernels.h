@@ -150,6 +150,15 @@ int wgrad_bias_slices(int M, int P, int Q);
 bool wgrad_pp_supported(int M, int P, int Q, int S, int slice);
 void wgrad_pp(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, int S, int slice,
               float* part, float* out, bool accumulate, float* bpart, int ctas, hipStream_t st);
+// hybrid form (no bias, more tiles than workgroups): whole tiles for the grid's whole rounds, slices for
+// the last one, finished by an ordered fix-up; part: wgrad_pp_hy_ws_floats floats
+bool wgrad_hy_plan(int M, int P, int Q, int ctas, int* full, int* rem, int* S, int* slice_kt);
+int64_t wgrad_pp_hy_ws_floats(int M, int P, int Q, int ctas);
+void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part,
+                 float* out, bool accumulate, int ctas, hipStream_t st);
+void wgrad_set_hy(int on);  // A/B: hybrid weight gradients where they apply
+// workspace floats wgrad() needs for this call (slice slabs or stream-K pieces)
+int64_t wgrad_ws_floats(int M, int P, int Q, bool out_f32, bool bias);
 bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,
            bool out_f32, bool accumulate, hipStream_t st, float* bpart = nullptr, void* bout = nullptr,
            bool bout_f32 = false);

@@ -29,6 +29,8 @@
 //  * bias gradient (dY column sums) by all-ones MFMAs against the dY fragments on the first Q tile's
 //    items, each wave taking the row tiles jj == wc of its row halves (+4 MFMAs per 64).
 // Requires M % 64 == 0, P % 8 == 0, Q % 8 == 0, row strides % 8 == 0 (checked by the binding).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -91,6 +93,17 @@ struct WPArgs {
   float* out;         // S == 1: the fp32 gradient [P, Q]
   int accumulate;     // S == 1: out += tile (else out = tile)
   float* bpart;       // bias gradient partial rows [S][P] (BIAS)
+  // hybrid split (HY): items [0, hy_full) are whole tiles (hy_full = whole rounds of the grid), written
+  // straight into the gradient; the last hy_rem tiles run as hy_s slices of slice_kt K-tiles each (items
+  // hy_full + s hy_rem + j, slice-major), leaving tile-local fp32 pieces [s hy_rem + j][256][256] in `part`
+  int hy_full, hy_rem, hy_s;
+  int kst;            // K-tiles per tile (M / 64)
+};
+
+// one work segment: a tile's K-tiles [kb, ke) and where its accumulators go (dest -1: the gradient,
+// added to it when accumulating; slice mode: slab sidx; stream-K: tile-local piece slot dest)
+struct WPSeg {
+  int tp, tq, kb, ke, dest, sidx;
 };
 
 struct WPCtx {
@@ -251,28 +264,74 @@ PLLM_DEV void wp_item(const WPArgs& g, int i, int tiles_q, int ntiles, int& sidx
   tq = t - tp * tiles_q;
 }
 
-// the item's tile: fp32 stores straight from the accumulators (32 per lane, all issued; rows /
-// columns out of range go to an offset past the descriptor)
-PLLM_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], int sidx, int tp, int tq) {
+// segment i of workgroup lid (G workgroups; tiles_q tiles per row band, ntiles tiles)
+template <bool HY>
+PLLM_DEV WPSeg wp_seg(const WPArgs& g, int lid, int G, int i, int tiles_q, int ntiles) {
+  WPSeg s;
+  if constexpr (HY) {
+    const int it = lid + i * G;
+    int t;
+    if (it < g.hy_full) {
+      t = it;
+      s.kb = 0;
+      s.ke = g.kst;
+      s.dest = -1;
+    } else {
+      const int j = it - g.hy_full, sl = j / g.hy_rem;
+      t = g.hy_full + (j - sl * g.hy_rem);
+      s.kb = sl * g.slice_kt;
+      s.ke = min(g.kst, s.kb + g.slice_kt);
+      s.dest = j;
+    }
+    s.tp = t / tiles_q;
+    s.tq = t - s.tp * tiles_q;
+    s.sidx = 0;
+  } else {
+    wp_item(g, lid + i * G, tiles_q, ntiles, s.sidx, s.tp, s.tq);
+    s.kb = s.sidx * g.slice_kt;
+    s.ke = min(g.M / WBK, s.kb + g.slice_kt);
+    s.dest = g.S > 1 ? s.sidx : -1;
+  }
+  return s;
+}
+
+// segments of workgroup lid
+template <bool HY>
+PLLM_DEV int wp_nseg(const WPArgs& g, int lid, int G, int ntiles) {
+  const int items = HY ? g.hy_full + g.hy_rem * g.hy_s : ntiles * g.S;
+  return lid < items ? (items - lid + G - 1) / G : 0;
+}
+
+// the segment's tile: fp32 stores straight from the accumulators (32 per lane, all issued; rows /
+// columns out of range go to an offset past the descriptor).  Into the gradient (+= when
+// accumulating), the slice's slab, or a stream-K piece slot (tile-local [256][256], no bounds)
+template <bool HY>
+PLLM_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], const WPSeg& sg) {
   const WPArgs& g = *c.g;
   const int r16 = c.lane & 15, g4 = c.lane >> 4;
-  float* base = g.S > 1 ? g.part + (int64_t)sidx * g.P * g.Q : g.out;
-  const int rows_ok = min(WT, g.P - tp * WT);
+  const bool piece = HY && sg.dest >= 0;
+  float* base = piece ? g.part + (int64_t)sg.dest * (WT * WT)
+                      : sg.dest >= 0 ? g.part + (int64_t)sg.dest * g.P * g.Q : g.out;
+  const int ld = piece ? WT : g.Q;
+  const int row0 = piece ? 0 : sg.tp * WT, col0 = piece ? 0 : sg.tq * WT;
+  const int cols_lim = piece ? WT : g.Q;
+  const int rows_ok = piece ? WT : min(WT, g.P - sg.tp * WT);
+  const bool rmw = sg.dest < 0 && g.accumulate;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int r0 = c.wr * 128 + 16 * j;
     const int rows_j = max(0, min(16, rows_ok - r0));
-    const __amdgpu_buffer_rsrc_t rs = wp_rsrc(base + (int64_t)(tp * WT + (rows_j > 0 ? r0 : 0)) * g.Q, rows_j * g.Q * 4);
+    const __amdgpu_buffer_rsrc_t rs = wp_rsrc(base + (int64_t)(row0 + (rows_j > 0 ? r0 : 0)) * ld, rows_j * ld * 4);
     f32x4 v[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) v[t] = acc[t][j];
     uint32_t off[4];
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      const int q = tq * WT + c.wc * 64 + 16 * t + 4 * g4;
-      off[t] = q < g.Q ? (uint32_t)(r16 * g.Q + q) * 4u : kWOff;
+      const int q = col0 + c.wc * 64 + 16 * t + 4 * g4;
+      off[t] = q < cols_lim ? (uint32_t)(r16 * ld + q) * 4u : kWOff;
     }
-    if (g.S == 1 && g.accumulate) {
+    if (rmw) {
 #pragma unroll
       for (int t = 0; t < 4; ++t)
         v[t] += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off[t], 0, 0));
@@ -283,14 +342,14 @@ PLLM_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], int sidx, int tp, 
   }
 }
 
-template <bool BIAS>
+template <bool BIAS, bool HY = false>
 __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * WSLOT];
   const int tiles_p = (g.P + WT - 1) / WT, tiles_q = (g.Q + WT - 1) / WT, ntiles = tiles_p * tiles_q;
-  const int items = ntiles * g.S;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
-  if (lid >= items) return;
+  const int R = wp_nseg<HY>(g, lid, G, ntiles);  // segments of this workgroup
+  if (R == 0) return;
   WPCtx c;
   c.g = &g;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -323,11 +382,9 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
       c.rd[h] = (unsigned)(row * 32 + ((((col >> 3) ^ wp_swz(row))) << 3) + (col & 7)) * 2u;
     }
   }
-  const int R = (items - lid + G - 1) / G;  // items of this workgroup: lid, lid + G, ...
-  int sidx, tp, tq;
-  wp_item(g, lid, tiles_q, ntiles, sidx, tp, tq);
+  WPSeg sg = wp_seg<HY>(g, lid, G, 0, tiles_q, ntiles);
   {
-    const WPSrd srd = wp_srds(g, tp, tq, sidx * g.slice_kt);
+    const WPSrd srd = wp_srds(g, sg.tp, sg.tq, sg.kb);
     wp_issue<0>(c, srd, 0);
     wp_issue<1>(c, srd, 0);
     wp_issue<2>(c, srd, 0);
@@ -342,45 +399,116 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   bf16x8 fb[2][2];
   int s = 0;
   for (int i = 0; i < R; ++i) {
-    const int kb = sidx * g.slice_kt, ke = min(g.M / WBK, kb + g.slice_kt);
-    const bool dob = BIAS && tq == 0;
+    const bool dob = BIAS && sg.tq == 0;
     f32x4 bacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-    int sidx2 = sidx, tp2 = tp, tq2 = tq;
     const bool more = i + 1 < R;
-    if (more) wp_item(g, lid + (i + 1) * G, tiles_q, ntiles, sidx2, tp2, tq2);
-    // K-tile kt's DMA carries kt + 1, or the next item's first K-tile after the last one (an
-    // empty descriptor after the workgroup's last item: the same instructions, nothing read)
-    for (int kt = kb; kt < ke; ++kt, ++s) {
+    // K-tile kt's DMA carries kt + 1, or the next segment's first K-tile after the last one (an
+    // empty descriptor after the workgroup's last segment: the same instructions, nothing read)
+    for (int kt = sg.kb; kt < sg.ke; ++kt, ++s) {
       WPSrd srd;
-      if (kt + 1 < ke) srd = wp_srds(g, tp, tq, kt + 1);
-      else if (more) srd = wp_srds(g, tp2, tq2, sidx2 * g.slice_kt);
-      else srd = WPSrd{srd_of(g.A, 0u), srd_of(g.B, 0u)};
-      if (kt == kb) wp_ktile<true, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
+      if (kt + 1 < sg.ke) {
+        srd = wp_srds(g, sg.tp, sg.tq, kt + 1);
+      } else if (more) {
+        const WPSeg nx = wp_seg<HY>(g, lid, G, i + 1, tiles_q, ntiles);
+        srd = wp_srds(g, nx.tp, nx.tq, nx.kb);
+      } else {
+        srd = WPSrd{srd_of(g.A, 0u), srd_of(g.B, 0u)};
+      }
+      if (kt == sg.kb) wp_ktile<true, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
       else wp_ktile<false, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
     }
-    wp_epilogue(c, acc, sidx, tp, tq);
+    wp_epilogue<HY>(c, acc, sg);
     if constexpr (BIAS) {
       if (dob) {
         // P rows wr 128 + 16 (4 jh + wc) + lane, from lanes 0-15 (buffer stores: in-order vmcnt)
-        const __amdgpu_buffer_rsrc_t brs = wp_rsrc(g.bpart + (int64_t)sidx * g.P, g.P * 4);
+        const __amdgpu_buffer_rsrc_t brs = wp_rsrc(g.bpart + (int64_t)sg.sidx * g.P, g.P * 4);
 #pragma unroll
         for (int jh = 0; jh < 2; ++jh) {
-          const int prow = tp * WT + c.wr * 128 + 16 * (4 * jh + c.wc) + lane;
+          const int prow = sg.tp * WT + c.wr * 128 + 16 * (4 * jh + c.wc) + lane;
           const uint32_t bo = ((lane >> 4) == 0 && prow < g.P) ? (uint32_t)prow * 4u : kWOff;
           __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, bacc[jh][0]), brs, bo, 0, 0);
         }
       }
     }
-    sidx = sidx2;
-    tp = tp2;
-    tq = tq2;
+    if (more) sg = wp_seg<HY>(g, lid, G, i + 1, tiles_q, ntiles);
   }
   if (c.wr == 0) wp_barrier();  // balance the stagger
+}
+
+// hybrid fix-up: the last hy_rem tiles get out (+)= their hy_s pieces in slice order; one block per
+// (tile, 16 rows), 16 columns per thread
+__global__ __launch_bounds__(256) void wgrad_hy_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                              int P, int Q, int tiles_q, int hy_full, int hy_rem,
+                                                              int hy_s, int accumulate) {
+  const int j = blockIdx.x, t = hy_full + j;
+  const int tp = t / tiles_q, tq = t - tp * tiles_q;
+  const int row = blockIdx.y * 16 + (threadIdx.x >> 4), col = (threadIdx.x & 15) * 16;
+  const int grow = tp * WT + row;
+  if (grow >= P) return;
+#pragma unroll
+  for (int c4 = 0; c4 < 4; ++c4) {
+    const int gcol = tq * WT + col + 4 * c4;
+    if (gcol >= Q) break;
+    f32x4* o = reinterpret_cast<f32x4*>(out + (int64_t)grow * Q + gcol);
+    f32x4 f = accumulate ? *o : f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sl = 0; sl < hy_s; ++sl)
+      f += *reinterpret_cast<const f32x4*>(part + (int64_t)(sl * hy_rem + j) * (WT * WT) + row * WT + col + 4 * c4);
+    *o = f;
+  }
 }
 
 }  // namespace
 
 namespace pllm {
+
+// hybrid plan: with more tiles than workgroups, whole tiles for the whole rounds of the grid and the
+// remaining tiles as slices filling the last round (>= 2 K-tiles each); false when it does not apply
+// (no more tiles than workgroups: wgrad_plan's uniform slices)
+bool wgrad_hy_plan(int M, int P, int Q, int ctas, int* full, int* rem, int* S, int* slice_kt) {
+  const int kst = M / WBK;
+  const int ntiles = ((P + WT - 1) / WT) * ((Q + WT - 1) / WT);
+  if (M % WBK != 0 || kst < 2 || ctas <= 0 || ntiles <= ctas) return false;
+  *full = ntiles / ctas * ctas;
+  *rem = ntiles - *full;
+  int s = *rem > 0 ? std::max(1, std::min(ctas / *rem, kst / 2)) : 1;
+  *slice_kt = (kst + s - 1) / s;
+  *S = *rem > 0 ? (kst + *slice_kt - 1) / *slice_kt : 0;
+  return true;
+}
+
+int64_t wgrad_pp_hy_ws_floats(int M, int P, int Q, int ctas) {
+  int full, rem, S, skt;
+  return wgrad_hy_plan(M, P, Q, ctas, &full, &rem, &S, &skt) ? (int64_t)rem * S * WT * WT : 0;
+}
+
+void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part,
+                 float* out, bool accumulate, int ctas, hipStream_t st) {
+  int full, rem, S, skt;
+  if (!wgrad_hy_plan(M, P, Q, ctas, &full, &rem, &S, &skt)) return;
+  WPArgs g;
+  g.A = (const uint16_t*)dy;
+  g.B = (const uint16_t*)x;
+  g.lda = lda;
+  g.ldb = ldb;
+  g.M = M;
+  g.P = P;
+  g.Q = Q;
+  g.S = 1;
+  g.slice_kt = skt;
+  g.part = part;
+  g.out = out;
+  g.accumulate = accumulate ? 1 : 0;
+  g.bpart = nullptr;
+  g.hy_full = full;
+  g.hy_rem = rem;
+  g.hy_s = S;
+  g.kst = M / WBK;
+  const int items = full + rem * S;
+  hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), dim3(items < ctas ? items : ctas), dim3(WNT), 0, st, g);
+  if (rem > 0)
+    hipLaunchKernelGGL(wgrad_hy_reduce_kernel, dim3(rem, WT / 16), dim3(256), 0, st, part, out, P, Q,
+                       (Q + WT - 1) / WT, full, rem, S, g.accumulate);
+}
 
 bool wgrad_pp_supported(int M, int P, int Q, int S, int slice) {
   (void)P;
@@ -405,6 +533,8 @@ void wgrad_pp(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, in
   g.out = out;
   g.accumulate = accumulate ? 1 : 0;
   g.bpart = bpart;
+  g.hy_full = g.hy_rem = g.hy_s = 0;
+  g.kst = M / WBK;
   const int ntiles = ((P + WT - 1) / WT) * ((Q + WT - 1) / WT);
   const int items = ntiles * S;
   const int grid = items < ctas ? items : ctas;

@@ -49,6 +49,10 @@ def load(raise_on_error: bool = False) -> bool:
                 # PLLM_WGRAD_VARIANT: weight-gradient kernel variant for A/B runs (csrc/gemm_wgrad.hip)
                 if os.environ.get("PLLM_WGRAD_VARIANT"):
                     torch.ops.pllm.wgrad_set_mfma(int(os.environ["PLLM_WGRAD_VARIANT"]))
+                # PLLM_WGRAD_HY=0|1: weight gradients with more tiles than CUs as whole tiles + a sliced last
+                # round (csrc/wgrad_pp.hip hybrid) instead of uniform split-K slices
+                if os.environ.get("PLLM_WGRAD_HY") and hasattr(torch.ops.pllm, "wgrad_set_hy"):
+                    torch.ops.pllm.wgrad_set_hy(int(os.environ["PLLM_WGRAD_HY"]))
                 # PLLM_GEMM_KERNEL=pp|r3: main loop of the fused-epilogue TN GEMM (ops.gemm_config);
                 # PLLM_GEMM_RESERVE_CUS=n: CUs its persistent grid leaves to concurrent RCCL kernels;
                 # PLLM_GEMM_SPLIT=0|1: the ping-pong kernel's desynchronising tile split

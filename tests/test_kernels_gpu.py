@@ -981,6 +981,33 @@ def _rope_case(D, Hkv):
         assert _rel(a, b) < 3e-2, (n, _rel(a, b))
 
 
+@pytest.mark.parametrize("M,P,Q", [(4096, 50304, 768), (2048, 50304, 2048), (1024, 11008, 2048), (8192, 65536, 256),
+                                   (4096, 4104, 4104), (1024, 4352, 4096)])
+def test_wgrad_hybrid(M, P, Q):
+    """Hybrid weight gradients (wgrad_set_hy(1), csrc/wgrad_pp.hip: more tiles than workgroups -> whole tiles for
+    the grid's whole rounds, the remaining tiles as slices of the last round, finished by the ordered fix-up;
+    edge tiles included): fp64 reference, accumulation into a non-zero gradient, run-to-run determinism, and
+    agreement with the slice kernel."""
+    torch.manual_seed(31)
+    dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
+    x = torch.randn(M, Q, device=DEV).bfloat16()
+    w0 = torch.randn(P, Q, device=DEV)
+    ref = w0.double() + dy.double().t() @ x.double()
+    try:
+        torch.ops.pllm.wgrad_set_hy(1)
+        acc = w0.clone()
+        torch.ops.pllm.wgrad(dy, x, acc)
+        acc2 = w0.clone()
+        torch.ops.pllm.wgrad(dy, x, acc2)
+    finally:
+        torch.ops.pllm.wgrad_set_hy(0)
+    assert _rel(acc.double(), ref) < 1e-5, _rel(acc.double(), ref)
+    assert torch.equal(acc, acc2)  # deterministic
+    acc3 = w0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc3)  # slice kernel
+    assert _rel(acc.double(), acc3.double()) < 1e-6
+
+
 @pytest.mark.parametrize("M,P,Q", [(4096, 4096, 8192), (8192, 2304, 768), (4096, 50304, 768), (2048, 200, 136)])
 def test_wgrad_pp_kernel(M, P, Q):
     """The ping-pong weight-gradient kernel (csrc/wgrad_pp.hip; wgrad's default for fp32 targets):
