@@ -261,6 +261,11 @@ class GPT(nn.Module):
             self.lm_head = None
         else:
             self.lm_head = nn.Linear(C, V, bias=cfg.head_bias)
+            # an untied token table is only gathered from, never a GEMM operand: no transposed bf16
+            # shadow for the optimizer to refresh every step (train/optim.py)
+            self.token_embed.weight._pllm_no_shadow = True
+        if self.position_embed is not None:
+            self.position_embed.weight._pllm_no_shadow = True
         if cfg.arch == "ref":
             # persistent like the reference (transformer.py:39) so checkpoints match key-for-key
             self.register_buffer("pos_idxs", torch.arange(cfg.context_length), persistent=True)

@@ -127,7 +127,8 @@ class FlatAdamW:
         if transposed_shadow is None:
             import os as _os
             transposed_shadow = self.use_hip and _os.environ.get("PLLM_WT_SHADOW", "1") == "1"
-        self.shadowed = [p for p in params if transposed_shadow and p.dim() == 2]
+        self.shadowed = [p for p in params if transposed_shadow and p.dim() == 2
+                         and not getattr(p, "_pllm_no_shadow", False)]
         sh_off, o = [], 0
         for p in self.shadowed:
             sh_off.append(o)
