@@ -260,6 +260,7 @@ def main(argv=None):
                        "step_mode": "graph" if args.cuda_graph else "eager",
                        "gemm_reserve_cus": args.reserve_cus,
                        "gemm_persistent": gemm_persistent,
+                       "lazy_grad_zeroing": bool(getattr(opt, "lazy_zero", False)),
                        "activation_checkpointing": bool(model.use_checkpointing(torch.empty(B, T, device=dev))),
                        "checkpointed_blocks": int(model.checkpointed_blocks(torch.empty(B, T, device=dev)))},
             "mfu": round(tps / world * flops_tok / 2.5e15, 4),

@@ -172,8 +172,9 @@ Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc) {
 // bias_acc (requires out_acc): the bias gradient column sums of dy are added into it too -- inside the
 // GEMM when its kernel can (wgrad_kernel's all-ones MFMAs), else by the bias_grad kernels
 Tensor bias_grad(const Tensor& dy, const std::optional<Tensor>& out_acc);
+// overwrite (with out_acc): store dW into out_acc instead of adding (its first write of a step)
 Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out_acc,
-             const std::optional<Tensor>& bias_acc) {
+             const std::optional<Tensor>& bias_acc, bool overwrite) {
   check_bf16(dy, "dy");
   check_bf16(x, "x");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "wgrad: dy [M,P], x [M,Q]");
@@ -211,10 +212,10 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
   bool fused_b = false;
   if (M > 0)
     fused_b = pllm::wgrad(dy.data_ptr(), dy.stride(0), x.data_ptr(), x.stride(0), (int)M, (int)P, (int)Q,
-                          part.data_ptr<float>(), out.data_ptr(), of32, out_acc.has_value(),
+                          part.data_ptr<float>(), out.data_ptr(), of32, out_acc.has_value() && !overwrite,
                           cur_stream(), bias_acc ? bpart.data_ptr<float>() : nullptr,
                           bias_acc ? bias_acc->data_ptr() : nullptr, bf32);
-  else if (!out_acc)
+  else if (!out_acc || overwrite)
     out.zero_();
   if (bias_acc && M > 0 && !fused_b) bias_grad(dy.is_contiguous() ? dy : dy.contiguous(), bias_acc);
   return out_acc ? at::empty({0}, dy.options()) : out;
@@ -540,6 +541,21 @@ void scale_(Tensor& x, const Tensor& s) {
 
 // ring attention: fold a partial block result (o [B, T, H, D] bf16, lse [B, H, T] fp32) into the
 // fp32 accumulators o_acc [B, T, H, D] / lse_acc [B, H, T] in place (views with any row strides)
+// ranges: int64 [n, 2] element ranges [start, end) of buf, every bound 16-B aligned; max_len: longest range
+void zero_ranges_(Tensor& buf, const Tensor& ranges, int64_t max_len) {
+  check_gpu(buf, "buf");
+  check_contig(buf, "buf");
+  TORCH_CHECK(ranges.is_cuda() && ranges.scalar_type() == at::kLong && ranges.dim() == 2 && ranges.size(1) == 2 &&
+                  ranges.is_contiguous(), "zero_ranges_: ranges int64 [n, 2] on the GPU");
+  TORCH_CHECK(ranges.size(0) <= 65535, "zero_ranges_: at most 65535 ranges");
+  const int64_t es = buf.element_size();
+  TORCH_CHECK((max_len * es) % 16 == 0 || max_len == 0, "zero_ranges_: 16-B multiples");
+  if (ranges.size(0) == 0 || max_len == 0) return;
+  // the kernel reads byte offsets: scale the element ranges on the device (host never syncs)
+  Tensor bytes = ranges * es;
+  pllm::zero_ranges(buf.data_ptr(), bytes.data_ptr<int64_t>(), (int)ranges.size(0), max_len * es, cur_stream());
+}
+
 void lse_merge_(Tensor& o_acc, Tensor& lse_acc, const Tensor& o, const Tensor& lse) {
   TORCH_CHECK(o_acc.scalar_type() == at::kFloat && lse_acc.scalar_type() == at::kFloat && lse.scalar_type() == at::kFloat,
               "lse_merge_: o_acc / lse_acc / lse fp32");
@@ -1012,7 +1028,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms) -> (Tensor, Tensor, Tensor)");
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
-  m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None) -> Tensor");
+  m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None, bool overwrite=False) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int split=-1, int persistent=-1) -> ()",
@@ -1034,6 +1050,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("rope_qk(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("lse_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o, Tensor lse) -> ()");
+  m.def("zero_ranges_(Tensor(a!) buf, Tensor ranges, int max_len) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
@@ -1064,6 +1081,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("rope_qk", rope_qk);
   m.impl("scale_", scale_);
   m.impl("lse_merge_", lse_merge_);
+  m.impl("zero_ranges_", zero_ranges_);
   m.impl("cross_entropy", cross_entropy);
   m.impl("adamw_", adamw_);
   m.impl("sumsq", sumsq);

@@ -9,6 +9,8 @@
 // thread; the loops still grid-stride for safety): a grid capped at 2048 blocks with
 // grid-stride loops streamed 5.1 TB/s where the full grid streams 6.0-6.2 TB/s on MI355X
 // (GELU fwd / bwd at 402 MB, bench/hbm_probe.py, profiles/r2_elementwise_grid_ab.txt).
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -245,9 +247,28 @@ __global__ __launch_bounds__(256) void lse_merge_kernel(LseMergeArgs a) {
   if (c == 0) *lap = nw;
 }
 
+// zero [start, end) ranges of a buffer (byte offsets, 16-B aligned; ranges int64 [n][2]): blockIdx.y =
+// range, 16-B vectors grid-strided over it -- the optimizer's lazily zeroed gradient buffer clears its
+// accumulate-only segments in one launch (train/optim.py)
+__global__ __launch_bounds__(256) void zero_ranges_kernel(char* __restrict__ buf, const int64_t* __restrict__ ranges) {
+  const int64_t a = ranges[2 * blockIdx.y], b = ranges[2 * blockIdx.y + 1];
+  const u32x4 z = {0u, 0u, 0u, 0u};
+  for (int64_t i = a + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < b;
+       i += (int64_t)gridDim.x * blockDim.x * 16)
+    *reinterpret_cast<u32x4*>(buf + i) = z;
+}
+
 }  // namespace
 
 namespace pllm {
+
+void zero_ranges(void* buf, const int64_t* ranges, int n, int64_t max_bytes, hipStream_t st) {
+  if (n <= 0) return;
+  const int64_t vec = (max_bytes + 15) / 16;
+  const int gx = (int)std::min<int64_t>(std::max<int64_t>(1, (vec + 255) / 256), 4096);
+  hipLaunchKernelGGL(zero_ranges_kernel, dim3(gx, n), dim3(256), 0, st, (char*)buf, ranges);
+}
+
 
 void act_fwd(int op, const void* x, void* y, size_t n, hipStream_t st) {
   const size_t nv = n / 8;

@@ -81,9 +81,29 @@ def _ops():
 # post-accumulate-grad hook for these).
 # ---------------------------------------------------------------------------
 def _acc_target(p):
+    """The flat-gradient slot a writer ADDS into.  A slot the optimizer left uncleared (lazy zeroing,
+    ``FlatAdamW(lazy_zero=True)``: it expects an overwriting first write, see ``_set_target``) is
+    zeroed here first, so every accumulating writer stays correct whatever runs first."""
     if p is None or not getattr(p, "_pllm_flat_grad", False):
         return None
-    return getattr(p, "_pllm_gradbuf", None)
+    buf = getattr(p, "_pllm_gradbuf", None)
+    if buf is not None and getattr(p, "_pllm_grad_fresh", False):
+        p._pllm_grad_fresh = False
+        buf.zero_()
+    return buf
+
+
+def _set_target(p):
+    """(slot, overwrite) for a writer that produces a weight's whole gradient at once (the weight-
+    gradient GEMMs): when the optimizer left the slot uncleared this step, the writer stores instead of
+    adding -- no zero fill and no read of zeros (train/optim.py lazy zeroing)."""
+    if p is None or not getattr(p, "_pllm_flat_grad", False):
+        return None, False
+    buf = getattr(p, "_pllm_gradbuf", None)
+    fresh = buf is not None and getattr(p, "_pllm_grad_fresh", False)
+    if fresh:
+        p._pllm_grad_fresh = False
+    return buf, fresh
 
 
 def _notify(p):
@@ -120,19 +140,19 @@ class _LinearFn(torch.autograd.Function):
             btgt = _acc_target(ctx.b)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
-            tgt = _acc_target(ctx.w)
+            tgt, fresh = _set_target(ctx.w)
             if tgt is None:
                 btgt = None
             if WGRAD_STREAM and tgt is not None and dy2.is_cuda:
                 main, side = torch.cuda.current_stream(), _side_stream(dy2.device)
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
-                    _weight_grad(dy2, x2, tgt)
+                    _weight_grad(dy2, x2, tgt, overwrite=fresh)
                 dy2.record_stream(side)
                 x2.record_stream(side)
                 dw = None
             else:
-                dw = _weight_grad(dy2, x2, tgt, btgt)
+                dw = _weight_grad(dy2, x2, tgt, btgt, overwrite=fresh)
             if tgt is not None:
                 _notify(ctx.w)
         if btgt is not None:
@@ -204,8 +224,9 @@ def _dgrad(dy, weight):
     return dy @ weight
 
 
-def _weight_grad(dy2, x2, tgt, btgt=None):
-    """dW = dy2^T @ x2, added into ``tgt`` (bf16 or fp32) when given (returns None) else returned.
+def _weight_grad(dy2, x2, tgt, btgt=None, overwrite: bool = False):
+    """dW = dy2^T @ x2, added into ``tgt`` (bf16 or fp32) when given (returns None) else returned;
+    ``overwrite``: stored into ``tgt`` instead (its first write of the step, ``_set_target``).
     ``btgt`` (with ``tgt``): the bias gradient (column sums of dy2) is added into it as well -- on the
     hand-written kernel inside the GEMM (its all-ones MFMAs), else by the bias_grad kernels."""
     hip_ok = dy2.shape[1] % 8 == 0 and x2.shape[1] % 8 == 0 and dy2.shape[0] % 64 == 0
@@ -216,15 +237,18 @@ def _weight_grad(dy2, x2, tgt, btgt=None):
     if use_hip:
         dy2, x2 = dy2.contiguous(), x2.contiguous()
         if tgt is not None:
-            _ops().wgrad(dy2, x2, tgt.view(dy2.shape[1], x2.shape[1]), btgt)
+            _ops().wgrad(dy2, x2, tgt.view(dy2.shape[1], x2.shape[1]), btgt, overwrite)
             return None
         return _ops().wgrad(dy2, x2)
     if btgt is not None:
         _ops().bias_grad(dy2.contiguous(), btgt)
     if tgt is not None:
         if f32_tgt:
-            tgt.add_(torch.mm(dy2.t(), x2, out_dtype=torch.float32) if dy2.is_cuda
-                     else dy2.t().float() @ x2.float())
+            dw = (torch.mm(dy2.t(), x2, out_dtype=torch.float32) if dy2.is_cuda
+                  else dy2.t().float() @ x2.float())
+            tgt.copy_(dw.view_as(tgt)) if overwrite else tgt.add_(dw.view_as(tgt))
+        elif overwrite:
+            torch.mm(dy2.t(), x2, out=tgt.view(dy2.shape[1], x2.shape[1]))
         else:
             tgt.addmm_(dy2.t(), x2)
         return None
@@ -354,8 +378,8 @@ class _FusedMLPFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
         dw1 = db1 = dw2 = db2 = None
         # down projection: weight and bias gradients
-        tgt = _acc_target(w2)
-        dw2 = _weight_grad(dy2, a, tgt)
+        tgt, fresh = _set_target(w2)
+        dw2 = _weight_grad(dy2, a, tgt, overwrite=fresh)
         if tgt is not None:
             _notify(w2)
         if b2 is not None and not ctx.ext:
@@ -378,8 +402,8 @@ class _FusedMLPFn(torch.autograd.Function):
             db1 = bacc.to(b1.dtype)
         # up projection
         dx = _dgrad(dpre, w1) if ctx.needs_input_grad[0] else None
-        tgt = _acc_target(w1)
-        dw1 = _weight_grad(dpre, x2, tgt)
+        tgt, fresh = _set_target(w1)
+        dw1 = _weight_grad(dpre, x2, tgt, overwrite=fresh)
         if tgt is not None:
             _notify(w1)
         if dx is not None:
@@ -439,8 +463,8 @@ class _FusedSwiGLUMLPFn(torch.autograd.Function):
         w1, w2 = ctx.params
         ctx.params = None
         dy2 = dy.reshape(-1, dy.shape[-1]).contiguous()
-        tgt = _acc_target(w2)
-        dw2 = _weight_grad(dy2, a, tgt)
+        tgt, fresh = _set_target(w2)
+        dw2 = _weight_grad(dy2, a, tgt, overwrite=fresh)
         if tgt is not None:
             _notify(w2)
         w2t = getattr(w2, "_pllm_wT", None)
@@ -448,8 +472,8 @@ class _FusedSwiGLUMLPFn(torch.autograd.Function):
             w2t = w2.t().contiguous()
         dgu = _ops().gemm_tn(dy2, w2t, None, 5, gu, None)[0]
         dx = _dgrad(dgu, w1) if ctx.needs_input_grad[0] else None
-        tgt = _acc_target(w1)
-        dw1 = _weight_grad(dgu, x2, tgt)
+        tgt, fresh = _set_target(w1)
+        dw1 = _weight_grad(dgu, x2, tgt, overwrite=fresh)
         if tgt is not None:
             _notify(w1)
         if dx is not None:
@@ -714,9 +738,9 @@ class _AttnProjFn(torch.autograd.Function):
         dw = db = None
         need_b = b is not None and ctx.needs_input_grad[8] and not ctx.bias_ext
         if ctx.needs_input_grad[7]:
-            tgt = _acc_target(w)
+            tgt, fresh = _set_target(w)
             btgt = _acc_target(b) if (need_b and tgt is not None and FUSED_WGRAD_BIAS) else None
-            dw = _weight_grad(dy2, o2, tgt, btgt)
+            dw = _weight_grad(dy2, o2, tgt, btgt, overwrite=fresh)
             if tgt is not None:
                 _notify(w)
             if btgt is not None:
@@ -1169,9 +1193,12 @@ class _LMHeadCEFn(torch.autograd.Function):
             gh = dh.mul_(g.to(dh.dtype))
         gw = gb = None
         if dw is not None:
-            tgt = _acc_target(ctx.w)
+            tgt, fresh = _set_target(ctx.w)
             if tgt is not None:
-                tgt.view(-1).addcmul_(dw.view(-1), g)
+                if fresh:
+                    torch.mul(dw.view(-1), g, out=tgt.view(-1))
+                else:
+                    tgt.view(-1).addcmul_(dw.view(-1), g)
                 _notify(ctx.w)
             else:
                 gw = dw.mul_(g).to(ctx.wdtype)

@@ -49,10 +49,14 @@ def register() -> None:
         return dy.new_empty((dy.shape[-1],))
 
     @_reg("wgrad")
-    def _(dy, x, out_acc=None, bias_acc=None):
+    def _(dy, x, out_acc=None, bias_acc=None, overwrite=False):
         if out_acc is not None:
             return dy.new_empty((0,))
         return dy.new_empty((dy.shape[1], x.shape[1]))
+
+    @_reg("zero_ranges_")
+    def _(buf, ranges, max_len):
+        return None
 
     @_reg("gemm_lt")
     def _(x, w, bias, epi, tune=True, residual=None):

@@ -60,8 +60,10 @@ class ShardedFlatAdamW(FlatAdamW):
         self.pg = process_group
         self.world, self.rank = _world_rank(process_group)
         unit = self.world * ALIGN
+        # lazy gradient zeroing off: the reduce-scattered buckets are read by this class's own step
         super().__init__(model, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay, decay_filter=decay_filter,
-                         max_grad_norm=max_grad_norm, transposed_shadow=transposed_shadow, pad_multiple=unit)
+                         max_grad_norm=max_grad_norm, transposed_shadow=transposed_shadow, pad_multiple=unit,
+                         lazy_zero=False)
         esz = self.flat_grad.element_size()
         # buckets from the end of the buffer, each a multiple of world*ALIGN elements
         buckets = []

@@ -50,7 +50,8 @@ def _round_up(n: int, a: int) -> int:
 class FlatAdamW:
     def __init__(self, model: nn.Module, lr: float = 5e-4, betas=(0.9, 0.999), eps: float = 1e-8,
                  weight_decay: float = 0.01, decay_filter=None, grad_dtype: Optional[torch.dtype] = None,
-                 max_grad_norm: float = 0.0, transposed_shadow: Optional[bool] = None, pad_multiple: int = ALIGN):
+                 max_grad_norm: float = 0.0, transposed_shadow: Optional[bool] = None, pad_multiple: int = ALIGN,
+                 lazy_zero: Optional[bool] = None):
         self.model = model
         self.lr = lr
         self.betas = betas
@@ -145,6 +146,40 @@ class FlatAdamW:
                                                           [p._pllm_wT for p in self.shadowed])
             self._tp_tiles = sum(((p.shape[0] + 63) // 64) * ((p.shape[1] + 63) // 64) for p in self.shadowed)
         self.refresh_shadows()
+        # Lazy zeroing (HIP path): zero_grad clears only the slots that accumulating writers fill (norms,
+        # biases, embedding tables) in one launch, and marks the weight-GEMM slots "fresh": their first
+        # writer of the step -- the weight-gradient GEMM, which produces the whole gradient at once --
+        # stores instead of adding (ops._set_target), so those slots are never zero-filled nor read back
+        # as zeros.  Any other writer zeroes a fresh slot before adding (ops._acc_target); a slot no
+        # writer touched is zeroed before the step reads it (_clear_unwritten).
+        if lazy_zero is None:
+            import os as _os
+            lazy_zero = _os.environ.get("PLLM_LAZY_ZERO", "0") == "1"
+        # (fp32 gradients of bf16 params only: with grad dtype == param dtype autograd may accumulate
+        # into p.grad, which aliases the slot)
+        self.lazy_zero = bool(lazy_zero) and self.use_hip and not self.grad_is_param_grad
+        self._fresh_params = [p for p in params if p.dim() == 2 and not getattr(p, "_pllm_no_shadow", False)]
+        if self.lazy_zero:
+            fresh = {id(p) for p in self._fresh_params}
+            runs, pos = [], 0
+            for i, p in enumerate(params):
+                o = self.offsets[i]
+                if id(p) in fresh:
+                    if o > pos:
+                        runs.append((pos, o))
+                    pos = o + _round_up(p.numel(), ALIGN)
+            if total > pos:
+                runs.append((pos, total))
+            self._zero_runs = torch.tensor(runs if runs else [[0, 0]], dtype=torch.int64, device=dev)
+            self._zero_max = max([b - a for a, b in runs], default=0)
+
+    def _clear_unwritten(self):
+        """Fresh slots no writer touched this step (an unused weight) hold last step's gradient: zero them."""
+        if self.lazy_zero:
+            for p in self._fresh_params:
+                if getattr(p, "_pllm_grad_fresh", False):
+                    p._pllm_grad_fresh = False
+                    p._pllm_gradbuf.zero_()
 
     @torch.no_grad()
     def refresh_shadows(self):
@@ -165,7 +200,12 @@ class FlatAdamW:
 
     def zero_grad(self, set_to_none: bool = False):
         # set_to_none is ignored on purpose: grads are views into the flat buffer
-        self.flat_grad.zero_()
+        if self.lazy_zero:
+            _lib.require().zero_ranges_(self.flat_grad, self._zero_runs, self._zero_max)
+            for p in self._fresh_params:
+                p._pllm_grad_fresh = True
+        else:
+            self.flat_grad.zero_()
         for i, p in enumerate(self.params):
             if self.grad_is_param_grad:
                 if p.grad is None or p.grad.data_ptr() != self.grad_view(i).data_ptr():
@@ -215,6 +255,7 @@ class FlatAdamW:
         return ss
 
     def grad_norm(self, grad_scale: float = 1.0) -> torch.Tensor:
+        self._clear_unwritten()
         ss = self._sumsq(self.flat_grad)
         if getattr(self, "tp", 1) > 1:
             import torch.distributed as dist
@@ -259,6 +300,7 @@ class FlatAdamW:
         if not graph:
             self._sync_lr()
             self.step_count += 1
+        self._clear_unwritten()
         clip = None
         if self.max_grad_norm and self.max_grad_norm > 0:
             norm = self.grad_norm(grad_scale)
@@ -347,7 +389,11 @@ def _fold_grad(p):
     """Post-accumulate hook (grad dtype != param dtype): add the gradient autograd produced
     for ``p`` into its slot of the flat gradient buffer and release it."""
     if p.grad is not None:
-        p._pllm_gradbuf.add_(p.grad)
+        if getattr(p, "_pllm_grad_fresh", False):  # lazily zeroed slot: this is its first write
+            p._pllm_grad_fresh = False
+            p._pllm_gradbuf.copy_(p.grad)
+        else:
+            p._pllm_gradbuf.add_(p.grad)
         p.grad = None
 
 
