@@ -172,6 +172,11 @@ class FlatAdamW:
                 runs.append((pos, total))
             self._zero_runs = torch.tensor(runs if runs else [[0, 0]], dtype=torch.int64, device=dev)
             self._zero_max = max([b - a for a, b in runs], default=0)
+            # the buffer starts zeroed, so the first step may store too -- and must: a step captured
+            # into a hipGraph before any zero_grad would otherwise bake the accumulating form, and its
+            # replays would add onto the slots the partial zero_grad leaves alone
+            for p in self._fresh_params:
+                p._pllm_grad_fresh = True
 
     def _clear_unwritten(self):
         """Fresh slots no writer touched this step (an unused weight) hold last step's gradient: zero them."""
