@@ -160,16 +160,7 @@ class FlatAdamW:
         self.lazy_zero = bool(lazy_zero) and self.use_hip and not self.grad_is_param_grad
         self._fresh_params = [p for p in params if p.dim() == 2 and not getattr(p, "_pllm_no_shadow", False)]
         if self.lazy_zero:
-            fresh = {id(p) for p in self._fresh_params}
-            runs, pos = [], 0
-            for i, p in enumerate(params):
-                o = self.offsets[i]
-                if id(p) in fresh:
-                    if o > pos:
-                        runs.append((pos, o))
-                    pos = o + _round_up(p.numel(), ALIGN)
-            if total > pos:
-                runs.append((pos, total))
+            runs = accumulate_only_runs(params, self.offsets, total, {id(p) for p in self._fresh_params})
             self._zero_runs = torch.tensor(runs if runs else [[0, 0]], dtype=torch.int64, device=dev)
             self._zero_max = max([b - a for a, b in runs], default=0)
             # the buffer starts zeroed, so the first step may store too -- and must: a step captured
@@ -388,6 +379,22 @@ class FlatAdamW:
         """Call after loading model weights directly into the params."""
         self.master.copy_(self.flat_param.float())
         self.refresh_shadows()
+
+
+def accumulate_only_runs(params, offsets, total: int, fresh_ids) -> list:
+    """[start, end) element ranges of the flat gradient buffer NOT owned by a lazily zeroed (fresh) slot:
+    the accumulate-only parameters, the alignment padding between slots and the tail padding, merged
+    where adjacent (every bound a multiple of ALIGN)."""
+    runs, pos = [], 0
+    for i, p in enumerate(params):
+        o = offsets[i]
+        if id(p) in fresh_ids:
+            if o > pos:
+                runs.append((pos, o))
+            pos = o + _round_up(p.numel(), ALIGN)
+    if total > pos:
+        runs.append((pos, total))
+    return runs
 
 
 def _fold_grad(p):

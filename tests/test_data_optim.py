@@ -159,3 +159,27 @@ def test_workspace_budgets_follow_free_hbm():
         assert M.workspace_budget(dev, M.CE_CAP, M.CE_FRACTION, M.CE_FLOOR, free_fn=lambda d: 1 * GiB) == M.CE_CAP
     finally:
         M.live_budgets()
+
+
+def test_lazy_zero_accumulate_only_runs():
+    """train/optim.accumulate_only_runs: the ranges lazy zeroing clears cover every slot except the fresh
+    (weight-GEMM) ones, padding included, merged and ALIGN-aligned."""
+    import torch.nn as nn
+    from pretraining_llm_amd.train.optim import ALIGN, _round_up, accumulate_only_runs
+    ps = [nn.Parameter(torch.zeros(n)) for n in (10, 64 * 3, 70, 5, 128, 1)]
+    offs, o = {}, 0
+    for i, p in enumerate(ps):
+        offs[i] = o
+        o += _round_up(p.numel(), ALIGN)
+    total = _round_up(o, 4 * ALIGN)
+    fresh = {id(ps[1]), id(ps[4])}
+    runs = accumulate_only_runs(ps, offs, total, fresh)
+    covered = torch.zeros(total, dtype=torch.bool)
+    for a, b in runs:
+        assert a % ALIGN == 0 and b % ALIGN == 0 and a < b
+        covered[a:b] = True
+    for i, p in enumerate(ps):
+        seg = covered[offs[i]:offs[i] + p.numel()]
+        assert (not seg.any()) if id(p) in fresh else seg.all()
+    assert covered[o:].all()  # tail padding
+    assert all(runs[k][1] < runs[k + 1][0] for k in range(len(runs) - 1))  # merged, ordered
