@@ -38,8 +38,12 @@ def test_lazy_zero_matches_full_zero(preset, compile_, tmp_path, monkeypatch):
         tr.metrics.log = recs.append
         tr.train()
         out[lazy] = ([r["train_loss"] for r in recs], tr.opt.master.clone())
-    assert out["0"][0] == out["1"][0]
-    assert torch.equal(out["0"][1], out["1"][1])
+    # the same sums in the same order (a store where the other adds onto zero): equal to rounding noise at
+    # most; a stale or doubled gradient slot would be off by orders of magnitude more
+    for a, b in zip(out["0"][0], out["1"][0]):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(b)), (out["0"][0], out["1"][0])
+    rel = ((out["0"][1] - out["1"][1]).norm() / out["0"][1].norm()).item()
+    assert rel < 1e-6, rel
 
 
 def test_lazy_zero_unwritten_weight_reads_zero():
