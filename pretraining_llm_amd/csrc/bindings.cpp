@@ -541,19 +541,21 @@ void scale_(Tensor& x, const Tensor& s) {
 
 // ring attention: fold a partial block result (o [B, T, H, D] bf16, lse [B, H, T] fp32) into the
 // fp32 accumulators o_acc [B, T, H, D] / lse_acc [B, H, T] in place (views with any row strides)
-// ranges: int64 [n, 2] element ranges [start, end) of buf, every bound 16-B aligned; max_len: longest range
-void zero_ranges_(Tensor& buf, const Tensor& ranges, int64_t max_len) {
+// ranges: int64 [n, 2] element ranges [start, end) of buf, every bound 16-B aligned, ascending;
+// total_len: their summed length (host-known, sizes the grid)
+void zero_ranges_(Tensor& buf, const Tensor& ranges, int64_t total_len) {
   check_gpu(buf, "buf");
   check_contig(buf, "buf");
   TORCH_CHECK(ranges.is_cuda() && ranges.scalar_type() == at::kLong && ranges.dim() == 2 && ranges.size(1) == 2 &&
                   ranges.is_contiguous(), "zero_ranges_: ranges int64 [n, 2] on the GPU");
-  TORCH_CHECK(ranges.size(0) <= 65535, "zero_ranges_: at most 65535 ranges");
   const int64_t es = buf.element_size();
-  TORCH_CHECK((max_len * es) % 16 == 0 || max_len == 0, "zero_ranges_: 16-B multiples");
-  if (ranges.size(0) == 0 || max_len == 0) return;
-  // the kernel reads byte offsets: scale the element ranges on the device (host never syncs)
-  Tensor bytes = ranges * es;
-  pllm::zero_ranges(buf.data_ptr(), bytes.data_ptr<int64_t>(), (int)ranges.size(0), max_len * es, cur_stream());
+  TORCH_CHECK((total_len * es) % 16 == 0, "zero_ranges_: 16-B multiples");
+  if (ranges.size(0) == 0 || total_len == 0) return;
+  // descriptors (start, end, bytes before) in bytes, built on the device (the host never syncs)
+  Tensor b = ranges * es;
+  Tensor len = b.select(1, 1) - b.select(1, 0);
+  Tensor desc = at::cat({b, (at::cumsum(len, 0) - len).unsqueeze(1)}, 1).contiguous();
+  pllm::zero_ranges(buf.data_ptr(), desc.data_ptr<int64_t>(), (int)ranges.size(0), total_len * es, cur_stream());
 }
 
 void lse_merge_(Tensor& o_acc, Tensor& lse_acc, const Tensor& o, const Tensor& lse) {
@@ -1050,7 +1052,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("rope_qk(Tensor x, Tensor cos, Tensor sin, int n_heads_total, int n_rot, int T) -> Tensor");
   m.def("scale_(Tensor(a!) x, Tensor s) -> ()");
   m.def("lse_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o, Tensor lse) -> ()");
-  m.def("zero_ranges_(Tensor(a!) buf, Tensor ranges, int max_len) -> ()");
+  m.def("zero_ranges_(Tensor(a!) buf, Tensor ranges, int total_len) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");

@@ -247,26 +247,30 @@ __global__ __launch_bounds__(256) void lse_merge_kernel(LseMergeArgs a) {
   if (c == 0) *lap = nw;
 }
 
-// zero [start, end) ranges of a buffer (byte offsets, 16-B aligned; ranges int64 [n][2]): blockIdx.y =
-// range, 16-B vectors grid-strided over it -- the optimizer's lazily zeroed gradient buffer clears its
-// accumulate-only segments in one launch (train/optim.py)
-__global__ __launch_bounds__(256) void zero_ranges_kernel(char* __restrict__ buf, const int64_t* __restrict__ ranges) {
-  const int64_t a = ranges[2 * blockIdx.y], b = ranges[2 * blockIdx.y + 1];
+// zero n [start, end) byte ranges of a buffer (16-B aligned; desc int64 [n][3] = start, end, bytes of the
+// ranges before this one): ONE flat grid over the ranges' total bytes, each thread finding its range by a
+// scan of the (few) descriptors -- the optimizer's lazily zeroed gradient buffer clears its accumulate-only
+// slots in one launch whose size follows the bytes, not the range count (train/optim.py)
+__global__ __launch_bounds__(256) void zero_ranges_kernel(char* __restrict__ buf, const int64_t* __restrict__ desc,
+                                                          int n, int64_t total) {
   const u32x4 z = {0u, 0u, 0u, 0u};
-  for (int64_t i = a + ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; i < b;
-       i += (int64_t)gridDim.x * blockDim.x * 16)
-    *reinterpret_cast<u32x4*>(buf + i) = z;
+  for (int64_t v = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; v < total;
+       v += (int64_t)gridDim.x * blockDim.x * 16) {
+    int r = 0;
+    while (r + 1 < n && desc[3 * (r + 1) + 2] <= v) ++r;
+    *reinterpret_cast<u32x4*>(buf + desc[3 * r] + (v - desc[3 * r + 2])) = z;
+  }
 }
 
 }  // namespace
 
 namespace pllm {
 
-void zero_ranges(void* buf, const int64_t* ranges, int n, int64_t max_bytes, hipStream_t st) {
-  if (n <= 0) return;
-  const int64_t vec = (max_bytes + 15) / 16;
-  const int gx = (int)std::min<int64_t>(std::max<int64_t>(1, (vec + 255) / 256), 4096);
-  hipLaunchKernelGGL(zero_ranges_kernel, dim3(gx, n), dim3(256), 0, st, (char*)buf, ranges);
+void zero_ranges(void* buf, const int64_t* desc, int n, int64_t total_bytes, hipStream_t st) {
+  if (n <= 0 || total_bytes <= 0) return;
+  const int64_t vec = (total_bytes + 15) / 16;
+  const int gx = (int)std::min<int64_t>(std::max<int64_t>(1, (vec + 255) / 256), 1 << 20);
+  hipLaunchKernelGGL(zero_ranges_kernel, dim3(gx), dim3(256), 0, st, (char*)buf, desc, n, total_bytes);
 }
 
 

@@ -84,8 +84,9 @@ void rope(const void* in, void* out, const float* cosb, const float* sinb, size_
           int n_rot, int D, int pos_offset, bool inverse, hipStream_t st, int out_heads = 0);
 void scale_bf16(void* x, const float* s, size_t n, hipStream_t st);
 // ring-attention LSE merge; st: element strides of o_acc (b, t, h), lse_acc (b, h, t), o (b, t, h), lse (b, h, t)
-// zero n byte ranges [start, end) of buf (int64 [n][2] on the device, 16-B aligned); max_bytes: longest range
-void zero_ranges(void* buf, const int64_t* ranges, int n, int64_t max_bytes, hipStream_t st);
+// zero n byte ranges of buf (desc int64 [n][3] on the device = start, end, bytes of the ranges before; 16-B
+// aligned); total_bytes: all ranges together
+void zero_ranges(void* buf, const int64_t* desc, int n, int64_t total_bytes, hipStream_t st);
 void lse_merge(float* o_acc, float* lse_acc, const void* o, const float* lse, const int64_t* st, int B, int T, int H,
                int D, hipStream_t stream);
 

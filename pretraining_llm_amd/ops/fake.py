@@ -55,7 +55,7 @@ def register() -> None:
         return dy.new_empty((dy.shape[1], x.shape[1]))
 
     @_reg("zero_ranges_")
-    def _(buf, ranges, max_len):
+    def _(buf, ranges, total_len):
         return None
 
     @_reg("gemm_lt")

@@ -162,7 +162,7 @@ class FlatAdamW:
         if self.lazy_zero:
             runs = accumulate_only_runs(params, self.offsets, total, {id(p) for p in self._fresh_params})
             self._zero_runs = torch.tensor(runs if runs else [[0, 0]], dtype=torch.int64, device=dev)
-            self._zero_max = max([b - a for a, b in runs], default=0)
+            self._zero_len = sum(b - a for a, b in runs)
             # the buffer starts zeroed, so the first step may store too -- and must: a step captured
             # into a hipGraph before any zero_grad would otherwise bake the accumulating form, and its
             # replays would add onto the slots the partial zero_grad leaves alone
@@ -197,7 +197,7 @@ class FlatAdamW:
     def zero_grad(self, set_to_none: bool = False):
         # set_to_none is ignored on purpose: grads are views into the flat buffer
         if self.lazy_zero:
-            _lib.require().zero_ranges_(self.flat_grad, self._zero_runs, self._zero_max)
+            _lib.require().zero_ranges_(self.flat_grad, self._zero_runs, self._zero_len)
             for p in self._fresh_params:
                 p._pllm_grad_fresh = True
         else:

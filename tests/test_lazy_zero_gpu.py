@@ -74,3 +74,20 @@ def test_lazy_zero_unwritten_weight_reads_zero():
     assert not getattr(m.b.weight, "_pllm_grad_fresh", True)
     assert (m.b.weight._pllm_gradbuf == 0).all()
     assert (m.a.weight._pllm_gradbuf != 0).any()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_zero_ranges_kernel(dtype):
+    """torch.ops.pllm.zero_ranges_: exactly the listed 16-B aligned ranges become zero, nothing else moves."""
+    torch.manual_seed(2)
+    n = 1 << 20
+    buf = torch.randn(n, device=DEV).to(dtype) + 3
+    ranges = [(0, 64), (128, 4096), (8192, 8192 + 64), (100000 // 64 * 64, 300000 // 64 * 64), (n - 640, n)]
+    before = buf.clone()
+    r = torch.tensor(ranges, dtype=torch.int64, device=DEV)
+    torch.ops.pllm.zero_ranges_(buf, r, sum(b - a for a, b in ranges))
+    mask = torch.zeros(n, dtype=torch.bool, device=DEV)
+    for a, b in ranges:
+        mask[a:b] = True
+    assert (buf[mask] == 0).all()
+    assert torch.equal(buf[~mask], before[~mask])
