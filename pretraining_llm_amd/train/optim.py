@@ -154,7 +154,7 @@ class FlatAdamW:
         # writer touched is zeroed before the step reads it (_clear_unwritten).
         if lazy_zero is None:
             import os as _os
-            lazy_zero = _os.environ.get("PLLM_LAZY_ZERO", "0") == "1"
+            lazy_zero = _os.environ.get("PLLM_LAZY_ZERO", "1") == "1"
         # (fp32 gradients of bf16 params only: with grad dtype == param dtype autograd may accumulate
         # into p.grad, which aliases the slot)
         self.lazy_zero = bool(lazy_zero) and self.use_hip and not self.grad_is_param_grad
