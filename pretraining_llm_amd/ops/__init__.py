@@ -1120,7 +1120,7 @@ def _lm_head_ce_pipelined(h, weight, bias, targets, ignore_index, inv_n, ws, row
         if dh is not None:
             torch.mm(lg, wt.t() if wt is not None else weight, out=dh[r0:r1])
         if dw is not None:
-            _weight_grad(lg, h[r0:r1], dw)
+            _weight_grad(lg, h[r0:r1], dw, overwrite=i == 0)
         if db is not None:
             _ops().bias_grad(lg, db)
 
@@ -1154,7 +1154,8 @@ class _LMHeadCEFn(torch.autograd.Function):
         R = _ce_chunk_rows(N, V, _ce_budget_bytes(h.device))
         ws = torch.empty(R, V, dtype=h.dtype, device=h.device)
         dh = torch.empty_like(h) if need_h else None
-        dw = torch.zeros(V, C, dtype=torch.float32, device=h.device) if need_w else None
+        # the first chunk's weight gradient stores into dw (no zero fill, no read of zeros), later ones add
+        dw = torch.empty(V, C, dtype=torch.float32, device=h.device) if need_w else None
         db = torch.zeros(V, dtype=torch.float32, device=h.device) if need_b else None
         rows = torch.empty(N, dtype=torch.float32, device=h.device)
         wt = getattr(weight, "_pllm_wT", None)
@@ -1176,7 +1177,7 @@ class _LMHeadCEFn(torch.autograd.Function):
             if need_h:  # dh = dlogits @ W (through the W^T shadow when present, see _dgrad)
                 torch.mm(lg, wt.t() if wt is not None else weight, out=dh[r0:r1])
             if need_w:
-                _weight_grad(lg, hc, dw)
+                _weight_grad(lg, hc, dw, overwrite=r0 == 0)
             if need_b:
                 _ops().bias_grad(lg, db)
         ctx.save_for_backward(dh, dw, db)
