@@ -436,25 +436,20 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
 }
 
 // hybrid fix-up: the last hy_rem tiles get out (+)= their hy_s pieces in slice order; one block per
-// (tile, 16 rows), 16 columns per thread
+// (tile, 4 rows), one 16-B column group per thread (all of a thread's loads independent)
 __global__ __launch_bounds__(256) void wgrad_hy_reduce_kernel(const float* __restrict__ part, float* __restrict__ out,
                                                               int P, int Q, int tiles_q, int hy_full, int hy_rem,
                                                               int hy_s, int accumulate) {
   const int j = blockIdx.x, t = hy_full + j;
   const int tp = t / tiles_q, tq = t - tp * tiles_q;
-  const int row = blockIdx.y * 16 + (threadIdx.x >> 4), col = (threadIdx.x & 15) * 16;
-  const int grow = tp * WT + row;
-  if (grow >= P) return;
-#pragma unroll
-  for (int c4 = 0; c4 < 4; ++c4) {
-    const int gcol = tq * WT + col + 4 * c4;
-    if (gcol >= Q) break;
-    f32x4* o = reinterpret_cast<f32x4*>(out + (int64_t)grow * Q + gcol);
-    f32x4 f = accumulate ? *o : f32x4{0.f, 0.f, 0.f, 0.f};
-    for (int sl = 0; sl < hy_s; ++sl)
-      f += *reinterpret_cast<const f32x4*>(part + (int64_t)(sl * hy_rem + j) * (WT * WT) + row * WT + col + 4 * c4);
-    *o = f;
-  }
+  const int row = blockIdx.y * 4 + (threadIdx.x >> 6), col = (threadIdx.x & 63) * 4;
+  const int grow = tp * WT + row, gcol = tq * WT + col;
+  if (grow >= P || gcol >= Q) return;
+  f32x4* o = reinterpret_cast<f32x4*>(out + (int64_t)grow * Q + gcol);
+  f32x4 f = accumulate ? *o : f32x4{0.f, 0.f, 0.f, 0.f};
+  const float* pp = part + (int64_t)j * (WT * WT) + row * WT + col;
+  for (int sl = 0; sl < hy_s; ++sl) f += *reinterpret_cast<const f32x4*>(pp + (int64_t)sl * hy_rem * (WT * WT));
+  *o = f;
 }
 
 }  // namespace
@@ -506,7 +501,7 @@ void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M,
   const int items = full + rem * S;
   hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), dim3(items < ctas ? items : ctas), dim3(WNT), 0, st, g);
   if (rem > 0)
-    hipLaunchKernelGGL(wgrad_hy_reduce_kernel, dim3(rem, WT / 16), dim3(256), 0, st, part, out, P, Q,
+    hipLaunchKernelGGL(wgrad_hy_reduce_kernel, dim3(rem, WT / 4), dim3(256), 0, st, part, out, P, Q,
                        (Q + WT - 1) / WT, full, rem, S, g.accumulate);
 }
 
