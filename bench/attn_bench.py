@@ -36,6 +36,9 @@ def main():
     ap.add_argument("--only", default="", help="fwd|bwd: run only our kernel (for profiling)")
     ap.add_argument("--rope-ab", action="store_true", help="our fwd/bwd with vs without fused RoPE tables")
     ap.add_argument("--ours", action="store_true", help="time only the HIP kernels (fwd_us / bwd_us), no SDPA")
+    ap.add_argument("--ks-ab", action="store_true",
+                    help="backward only: key-stationary kernel (attn_bwd_set_ks(3)) vs the previous kernels "
+                         "(set_ks(0)), interleaved rounds")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
@@ -74,6 +77,19 @@ def main():
             res["prepass_us"] = min(1e6 * timeit(pre) for _ in range(args.rounds))
             res["prepass_fwd_us"] = min(1e6 * timeit(f_) for _ in range(args.rounds))
             res["prepass_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
+            print(json.dumps(res), flush=True)
+            continue
+        if args.ks_ab:
+            flops_b = 2.5 * 2 * 2 * B * H * T * T * D / 2
+            res = {"cfg": cfg, "ks_bwd_us": [], "old_bwd_us": []}
+            for _ in range(args.rounds):
+                torch.ops.pllm.attn_bwd_set_ks(3)
+                res["ks_bwd_us"].append(1e6 * timeit(ours_b))
+                torch.ops.pllm.attn_bwd_set_ks(0)
+                res["old_bwd_us"].append(1e6 * timeit(ours_b))
+            torch.ops.pllm.attn_bwd_set_ks(2)
+            for k_ in ("ks", "old"):
+                res[k_ + "_tflops"] = flops_b / (min(res[k_ + "_bwd_us"]) * 1e-6) / 1e12
             print(json.dumps(res), flush=True)
             continue
         if args.ours:

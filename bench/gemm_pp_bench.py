@@ -3,8 +3,7 @@
 data, the variants INTERLEAVED round by round in one process (cdna_hip_programming.md §5.4 rule 24).
 One JSON line per shape: median and min microseconds per variant, TF/s of the medians.
 
-Variants: pp (ping-pong kernel with the opt-in desynchronising tile split where it applies),
-pp_ns (the default: without the split), r3, blas.
+Variants: pp (ping-pong kernel, the default), r3, blas.
 
 usage: python bench/gemm_pp_bench.py [--rounds 7] [--fused] [--shapes gpt2|llama|all] [--no-r3]"""
 import argparse
@@ -45,9 +44,9 @@ def main():
     P = torch.ops.pllm
     shapes = (GPT2 if args.shapes != "llama" else []) + (LLAMA if args.shapes != "gpt2" else [])
 
-    def with_cfg(ph, fn, split=1):
+    def with_cfg(ph, fn):
         def run():
-            P.gemm_set_config(16, args.group, ph, -1, split)
+            P.gemm_set_config(16, args.group, ph, -1)
             fn()
         return run
 
@@ -57,7 +56,6 @@ def main():
         w = (torch.empty(N, K, device="cuda").uniform_(-1, 1, generator=g) / K ** 0.5).bfloat16()
         b = torch.empty(N, device="cuda").uniform_(-1, 1, generator=g).bfloat16()
         var = {"pp": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0)),
-               "pp_ns": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0), 0),
                "r3": with_cfg(0, lambda: P.gemm_tn(a, w, b, 0)),
                "blas": lambda: F.linear(a, w, b)}
         extra = {}
@@ -67,7 +65,6 @@ def main():
             wdt = (torch.empty(N, K, device="cuda").uniform_(-1, 1, generator=g) / N ** 0.5).bfloat16()
             acc = torch.zeros(N, device="cuda")
             extra = {"pp_gelu": with_cfg(4, lambda: P.gemm_tn(a, w, b, 1)),
-                     "pp_ns_gelu": with_cfg(4, lambda: P.gemm_tn(a, w, b, 1), 0),
                      "r3_gelu": with_cfg(0, lambda: P.gemm_tn(a, w, b, 1)),
                      "blas_gelu": lambda: P.act_fwd(F.linear(a, w, b), 1),
                      "pp_dgelu": with_cfg(4, lambda: P.gemm_tn(dy, wdt, None, 3, pre, acc)),
@@ -83,14 +80,14 @@ def main():
         for _ in range(args.rounds):
             for k, fn in var.items():
                 ts[k].append(once(fn, args.reps))
-        P.gemm_set_config(16, 4, 4, -1, 0)  # the default kernel
+        P.gemm_set_config(16, 4, 4, -1)  # the default kernel
         fl = 2 * M * N * K
         rec = {"M": M, "N": N, "K": K}
         for k, v in ts.items():
             med = statistics.median(v)
             rec[k + "_us"] = round(med, 1)
             rec[k + "_min_us"] = round(min(v), 1)
-            if k in ("pp", "pp_ns", "r3", "blas"):
+            if k in ("pp", "r3", "blas"):
                 rec[k + "_tflops"] = round(fl / med / 1e6, 1)
         rec["pp_vs_blas"] = round(rec["blas_us"] / rec["pp_us"], 3)
         print(json.dumps(rec), flush=True)

@@ -59,7 +59,7 @@ COMMON_FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsaf
 # per-file flags.  attention.hip: no SLP vectorisation -- it packs pairs of independent f32
 # multiplies of the softmax / dS math into v_pk_mul_f32 plus two v_mov each to gather the
 # operands, more vector issue beside the MFMAs than the scalar multiplies
-FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"attention.hip": ["-fno-slp-vectorize"], "attn_bwd_ks.hip": ["-fno-slp-vectorize"]}
 
 
 def _needs(obj: str, deps) -> bool:

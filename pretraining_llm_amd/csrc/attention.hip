@@ -30,142 +30,14 @@
 //    (deterministic; the first version's fp32 atomics were its floor).  The key blocks run
 //    in passes so the slab workspace is bounded independently of T (O(T) memory).
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
+#include "attn_common.h"
 #include "common.h"
 #include "kernels.h"
 
 namespace {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
-
-PLLM_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
-}
-PLLM_DEV s16x4 ds_tr(const uint16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
-PLLM_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
-  s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-  return __builtin_bit_cast(bf16x8, v);
-}
-PLLM_DEV bf16x8 as_frag(const u32x4& v) { return __builtin_bit_cast(bf16x8, v); }
-PLLM_DEV bf16x8 zero_frag() { return __builtin_bit_cast(bf16x8, u32x4{0u, 0u, 0u, 0u}); }
-PLLM_DEV f32x16 zero16() {
-  f32x16 z;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z[i] = 0.f;
-  return z;
-}
-// element i of a 32x32 accumulator lives at row (i&3) + 8*(i>>2) + 4*half, column lane&31
-PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
-PLLM_DEV bf16x8 pack_frag(const f32x16& x, int s) {
-  bf16x8 f;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = (bf16)x[8 * s + j];
-  return f;
-}
-
-// ---------------------------------------------------------------------------
-// Fused RoPE (rotate-half convention, ops/reference.py rope): element i < D/2 of a head row
-// pairs with i + D/2; a' = a cos - b sin, b' = b cos + a sin at the row's position.  The kernels
-// rotate q and k while staging them (registers / LDS images) and un-rotate dq and dk before
-// the final stores, so the packed QKV tensor and its gradient stay unrotated and no separate
-// RoPE pass over [B, T, H, D] exists in forward or backward.
-// Rotates 8 + 8 bf16 values (a = elements i0..i0+7, b = i0+D/2..) held as two 16-B chunks.
-PLLM_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, float dir) {
-  float a[8], b[8], c[8], sn[8];
-  unpack8(lo, a);
-  unpack8(hi, b);
-  const f32x4* cp = reinterpret_cast<const f32x4*>(cosr);
-  const f32x4* sp = reinterpret_cast<const f32x4*>(sinr);
-  const f32x4 c0 = cp[0], c1 = cp[1], s0 = sp[0], s1 = sp[1];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    c[e] = c0[e];
-    c[4 + e] = c1[e];
-    sn[e] = s0[e] * dir;
-    sn[4 + e] = s1[e] * dir;
-  }
-  float o1[8], o2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    o1[e] = a[e] * c[e] - b[e] * sn[e];
-    o2[e] = b[e] * c[e] + a[e] * sn[e];
-  }
-  lo = pack8(o1);
-  hi = pack8(o2);
-}
-
-// Row-per-lane epilogue of 32x32 accumulator tiles (guide T21): acc[db] holds, for the lane's
-// row, columns db*32 + 8g + 4hh + e (e < 4), the two half-waves sharing each row.  Packs to
-// bf16 (times sc), swaps group pairs (k, k+1) across the half-waves with v_permlane32_swap and
-// stores one contiguous 16-B chunk per pair: 2*NDB dwordx4 stores instead of 4*NDB dwordx2 (the
-// store tail is issue-bound, per instruction).  row: 16-B aligned.
-template <int NDB>
-PLLM_DEV void store_row_bf16(uint16_t* row, const f32x16 (&acc)[NDB], float sc, int hh) {
-  u32x2 pk[4 * NDB];
-#pragma unroll
-  for (int db = 0; db < NDB; ++db)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      pk[4 * db + g][0] = pack_bf16x2(acc[db][4 * g] * sc, acc[db][4 * g + 1] * sc);
-      pk[4 * db + g][1] = pack_bf16x2(acc[db][4 * g + 2] * sc, acc[db][4 * g + 3] * sc);
-    }
-#pragma unroll
-  for (int k = 0; k < 4 * NDB; k += 2) {
-#pragma unroll
-    for (int d = 0; d < 2; ++d) {
-      const auto sw = __builtin_amdgcn_permlane32_swap(pk[k][d], pk[k + 1][d], false, false);
-      pk[k][d] = sw[0];
-      pk[k + 1][d] = sw[1];
-    }
-    *reinterpret_cast<u32x4*>(row + 8 * k + 8 * hh) = u32x4{pk[k][0], pk[k][1], pk[k + 1][0], pk[k + 1][1]};
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Swizzled LDS image of a [rows][W] bf16 tile (W = 32, 64 or 128 elements).
-// Chunk ch (16 B) of row r lives at chunk position ch ^ f(r):
-//   W=128 (256 B rows): f = ((r&3)<<2) | ((r>>2)&3)       (guide T10 layout (b))
-//   W=64  (128 B rows): f = bitrev3((r>>1)&7)
-//   W=32  ( 64 B rows): f = (r>>2)&3
-// For the 16-lane groups of ds_read_b128 (16 distinct rows, same chunk) and the
-// 32-lane halves of ds_read_b64_tr_b16 (4 consecutive rows x 64 contiguous bytes)
-// every f above maps the accesses to distinct 16-B bank slots.
-// ---------------------------------------------------------------------------
-template <int W>
-struct Img {
-  static PLLM_DEV int f(int r) {
-    if constexpr (W == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
-    else if constexpr (W == 64) {
-      const int b = (r >> 1) & 7;
-      return ((b & 1) << 2) | (b & 2) | ((b >> 2) & 1);
-    } else return (r >> 2) & 3;
-  }
-  // element offset of (row, col); col's 8-aligned chunk is swizzled, col&7 kept
-  static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
-  // a row's two RoPE-partner halves (chunks c and c + W/16) stored so that every 8-lane group
-  // of ds_write_b128 (bank = byte address mod 128) covers 128 distinct bytes: at W = 64 rows 2k
-  // and 2k+1 share f, so an odd row stores its upper half first (same image, same reads)
-  static PLLM_DEV void st_pair(uint16_t* base, int r, int c, const u32x4& lo, const u32x4& hi) {
-    constexpr int H = W / 16;
-    const bool sw = W == 64 && (r & 1);
-    st16(base + off(r, (sw ? c + H : c) * 8), sw ? hi : lo);
-    st16(base + off(r, (sw ? c : c + H) * 8), sw ? lo : hi);
-  }
-};
-
-// The fused-role backward's dS^T image [keys][128 queries] (256-B rows): chunk ch of row r at
-// ch ^ fs(r), fs linear in r's bits 0..2 (4, 9, 2).  Conflict-free both for the dQ task's
-// ds_read_b64_tr_b16 (4 consecutive rows x 4 aligned chunks -> 16 distinct positions) and for the
-// 16-B dS stores, whose 8-lane ds_write_b128 groups are 8 consecutive rows at one chunk (bank =
-// address mod 128 B: fs mod 8 is a permutation over any 8 aligned rows).  Img<128>'s swizzle gave
-// the former 8-B dS stores a 2-way conflict on every store (16 rows per ds_write_b64 group onto
-// 8 slots mod 128 B): ~64 conflict cycles per wave and iteration (profiles/r3_pmc_attn_*_bwd.md).
-struct ImgS {
-  static PLLM_DEV int f(int r) { return ((r & 1) ? 4 : 0) ^ ((r & 2) ? 9 : 0) ^ ((r & 4) ? 2 : 0); }
-  static PLLM_DEV int off(int r, int col) { return r * 128 + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
-};
 
 // ============================================================================
 // forward
@@ -179,74 +51,35 @@ struct ImgS {
 // past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
 // lazy-max threshold of the forward's online softmax, log2 units (p <= 2^8)
 constexpr float kLazyThr = 8.f;
-#ifndef PLLM_FWD_V3
-#define PLLM_FWD_V3 0
-#endif
-#ifndef PLLM_FWD_SCHED
-#define PLLM_FWD_SCHED 1
-#endif
-#ifndef PLLM_FWD_SGB
-#define PLLM_FWD_SGB 1  // read-ahead interleave (sched_group_barrier) in the plain forward loop
-#endif
-constexpr bool kFwdSgb = PLLM_FWD_SGB != 0;
-#ifndef PLLM_FWD_DMA
-#define PLLM_FWD_DMA 1  // plain forward loop: K/V tiles by LDS DMA (buffer_load ... lds)
-#endif
-constexpr bool kFwdDma = PLLM_FWD_DMA != 0;
 #ifndef PLLM_FWD_STAMPS
-#define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the plain forward loop
+#define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the forward loop
 #endif
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
 #endif
-#ifndef PLLM_BWD_QASYM
-#define PLLM_BWD_QASYM 0  // 1: waves 0-3 issue every Q / dO DMA piece, 4-7 start their dQ tasks at once (A/B build)
-#endif
-#ifndef PLLM_BWD_QSPREAD
-#define PLLM_BWD_QSPREAD 0  // 1: the next Q / dO tile's DMA pieces spread over the dQ task's MFMAs (A/B build)
-#endif
-#ifndef PLLM_BWD_STAGGER
-#define PLLM_BWD_STAGGER 0  // diagnostic: s_sleep units (64 cycles) for waves 4-7 per backward iteration
-#endif
-#ifndef PLLM_ABL
-#define PLLM_ABL 0  // diagnostic ablations of the pipelined forward (scripts/gpu/r3_attn_abl.sh)
-#endif
-// explicit instruction interleave (sched_group_barrier) in the pipelined forward's tile regions
-constexpr bool kFwdSched = PLLM_FWD_SCHED != 0;
-
-#ifndef PLLM_FWD64_QB
-#define PLLM_FWD64_QB 2  // query blocks per wave at D <= 64 (A/B builds)
-#endif
-#ifndef PLLM_FWD_MINW
-#define PLLM_FWD_MINW 2  // __launch_bounds__ minimum waves per SIMD of the forward (A/B builds)
-#endif
-#ifndef PLLM_FWD128_NW
-#define PLLM_FWD128_NW 4  // waves per workgroup at D = 128 (8: 256 query rows share each K/V tile)
-#endif
+// Measured and removed in round 5 (records kept in profiles/): a software-pipelined forward tile loop
+// (no faster, r3_attn_fwd_experiments.md), an exponent-ready "V3" forward, the 8-wave D = 128 forward
+// (neutral, r4_attn_experiments.md), register-staged K/V tiles instead of LDS DMA in the forward, and in
+// the backward the spread / asymmetric Q-dO DMA issue and the wave-4-7 stagger (r4_attn_experiments.md).
 
 template <int D>
 struct FwdCfg {
-  static constexpr int NW = D == 128 ? PLLM_FWD128_NW : 4;
-  static constexpr int MINB = NW == 8 ? 1 : PLLM_FWD_MINW;  // launch bounds: 2 waves per SIMD either way
-  static constexpr int QB = D <= 64 ? PLLM_FWD64_QB : 1;
+  static constexpr int NW = 4;
+  static constexpr int MINB = 2;  // launch bounds: 2 waves per SIMD
+  static constexpr int QB = D <= 64 ? 2 : 1;
   static constexpr int BM = NW * 32 * QB, BN = 64;
   static constexpr int CPR = D / 8;   // 16 B chunks per row
   static constexpr int TILE = BN * D;  // elements per K (or V) tile
   static constexpr int LDS_ELEMS = 4 * TILE;
-  // pipelined loop (QB = 2): two K buffers and THREE V buffers -- a tile's V is still read by the
-  // deferred P.V of the next tile while the tile after that is being staged
-  static constexpr int LDS_ELEMS_PIPE = 5 * TILE;
 };
 
-template <int D, bool ROPE, bool PIPE = false, bool V3 = false>
+template <int D, bool ROPE>
 __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_kernel(AttnFwdArgs a) {
-  static_assert(!PIPE || (FwdCfg<D>::QB == 2 && !ROPE), "pipelined tile loop: QB = 2, no fused RoPE");
-  static_assert(!V3 || (!PIPE && !ROPE), "sum-checked softmax: plain tile loop, no fused RoPE");
   using C = FwdCfg<D>;
   using I = Img<D>;
   constexpr int BM = C::BM, BN = C::BN, CPR = C::CPR, TILE = C::TILE, QB = C::QB, NW = C::NW;
   constexpr int NKS = D / 16, NDB = D / 32;
-  __shared__ __attribute__((aligned(16))) uint16_t smem[PIPE ? C::LDS_ELEMS_PIPE : C::LDS_ELEMS];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[C::LDS_ELEMS];
 
   const int nqb = (a.T + BM - 1) / BM;
   // heaviest (last) query blocks of every head first.  A head-local order (a head's blocks
@@ -286,17 +119,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
       for (int ks = 0; ks < NKS / 2; ++ks)
         rope8(raw[ks], raw[ks + NKS / 2], a.rope_cos + tab + 16 * ks + 8 * hh, a.rope_sin + tab + 16 * ks + 8 * hh,
               1.f);
-    }
-    if constexpr (V3) {
-      // scores straight in log2 units: Q x (scale log2 e), rounded once to bf16
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        float f[8];
-        unpack8(raw[ks], f);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) f[e] *= a.scale_log2;
-        raw[ks] = pack8(f);
-      }
     }
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) qf[j][ks] = as_frag(raw[ks]);
@@ -351,7 +173,7 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
   // tile straight into the swizzled image -- lane l of a piece fills LDS chunk 64 p + l, so it
   // loads the logical chunk that the image stores there (row g / CPR, chunk (g % CPR) ^ f(row)).
   // No staging registers, no ds_write restage; rows past S read as zeros (descriptor range).
-  constexpr bool DMA = kFwdDma && !ROPE && !PIPE && !V3;
+  constexpr bool DMA = !ROPE;
   constexpr int PCS = BN * CPR / 64;  // pieces per tile
   constexpr int PPW = 2 * PCS / NW;   // K + V pieces per wave
   static_assert(2 * PCS % NW == 0 && PCS % PPW == 0, "a wave's pieces lie in one operand");
@@ -410,343 +232,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
     }
   }
   __syncthreads();
-  if constexpr (PIPE) {
-    // ---- software-pipelined tile loop (QB = 2) ------------------------------------------
-    // A tile's work is split in two scheduling regions separated only by the (rare) lazy-max
-    // rescale branch:
-    //   region 1: S^T of both blocks (16 MFMAs, one K fragment read feeding two), mask, row max;
-    //   region 2: the PREVIOUS tile's P.V of block 1 (8 MFMAs) beside the exponentials of block
-    //             0 (VALU), then block 0's P.V (8 MFMAs) beside the exponentials of block 1.
-    // So each wave keeps its matrix pipe fed while its own softmax runs, instead of a QK^T burst,
-    // an MFMA-idle softmax and a PV burst per tile.  Block 1's P.V is deferred one tile: its P
-    // fragments live across the barrier and its V tile stays in one of three rotating V buffers
-    // (the stage of tile t+1 must not overwrite V(t-1) while a slower wave still runs its
-    // deferred P.V of tile t-1: K is read only in region 1, so two K buffers suffice).  A rescale
-    // of block 1 first retires the pending P.V (it was exponentiated against the old max: guide
-    // T13 hazard (a)).
-    bf16x8 pfp[4];       // P of block 1 from the previous tile (P.V pending)
-#pragma unroll
-    for (int kst = 0; kst < 4; ++kst) pfp[kst] = zero_frag();
-    bool pend = false;
-    auto pv = [&](auto j_c, const bf16x8 (&pf)[4], const uint16_t* Vb) {
-      constexpr int J = decltype(j_c)::value;
-#pragma unroll
-      for (int kst = 0; kst < 4; ++kst)
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-          const int rb = kst * 16 * D;
-          const bf16x8 va = cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
-          o[J][db] = mfma32(va, pf[kst], o[J][db]);
-        }
-    };
-    auto sexp = [&](auto j_c, f32x16 (&sj)[2], bf16x8 (&pf)[4]) {
-      constexpr int J = decltype(j_c)::value;
-      const float mc = m[J] == -INFINITY ? 0.f : m[J];
-      float ls0 = 0.f, ls1 = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float p0 = fast_exp2(__builtin_fmaf(sj[0][i], c2, -mc));
-        const float p1 = fast_exp2(__builtin_fmaf(sj[1][i], c2, -mc));
-        sj[0][i] = p0;
-        sj[1][i] = p1;
-        ls0 += p0;
-        ls1 += p1;
-      }
-      l[J] += ls0 + ls1;
-      pf[0] = pack_frag(sj[0], 0);
-      pf[1] = pack_frag(sj[0], 1);
-      pf[2] = pack_frag(sj[1], 0);
-      pf[3] = pack_frag(sj[1], 1);
-    };
-    // P.V of block J (fragments pf, V image Vb) interleaved with the exponentials + row sum of
-    // block E (scores se, in place) -- see the MASK == 3 region 2 below
-    auto pvx = [&](auto j_c, const bf16x8 (&pf)[4], const uint16_t* Vb, auto e_c, f32x16 (&se)[2]) {
-      constexpr int J = decltype(j_c)::value;
-      constexpr int E = decltype(e_c)::value;
-      constexpr int NSTEP = 4 * NDB, PER = 32 / NSTEP;  // MFMAs, softmax elements per MFMA
-      const float mc = m[E] == -INFINITY ? 0.f : m[E];
-      auto vread = [&](int step) {
-        const int kst = step / NDB, db = step % NDB, rb = kst * 16 * D;
-        return cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
-      };
-      float ls0 = 0.f, ls1 = 0.f;
-      bf16x8 va = vread(0);
-#pragma unroll
-      for (int step = 0; step < NSTEP; ++step) {
-        const bf16x8 vcur = va;
-        if (step + 1 < NSTEP) va = vread(step + 1);
-        o[J][step % NDB] = mfma32(vcur, pf[step / NDB], o[J][step % NDB]);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int e = 0; e < PER; ++e) {
-          const int i = step * PER + e;  // elements i of key half 0 and i of key half 1... (i < 16)
-          const int kb = i >> 4, ii = i & 15;
-          const float p = fast_exp2(__builtin_fmaf(se[kb][ii], c2, -mc));
-          se[kb][ii] = p;
-          if (e & 1) ls1 += p;
-          else ls0 += p;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      l[E] += ls0 + ls1;
-    };
-    auto packp = [&](f32x16 (&sj)[2], bf16x8 (&pf)[4]) {
-      pf[0] = pack_frag(sj[0], 0);
-      pf[1] = pack_frag(sj[0], 1);
-      pf[2] = pack_frag(sj[1], 0);
-      pf[3] = pack_frag(sj[1], 1);
-    };
-    auto rescale = [&](auto j_c, float mx2) {
-      constexpr int J = decltype(j_c)::value;
-      const float mnew = fmaxf(m[J], mx2);
-      const float alpha = mnew == -INFINITY ? 1.f : fast_exp2(m[J] - mnew);
-#pragma unroll
-      for (int db = 0; db < NDB; ++db)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[J][db][i] = o[J][db][i] * alpha;
-      l[J] *= alpha;
-      m[J] = mnew;
-    };
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    int vcur = 0, vprev = 2;  // V buffers of tiles t and t-1 (t % 3, (t-1) % 3)
-    for (int t = 0; t < ntiles; ++t) {
-      const int buf = t & 1;
-      const int vnext = 3 - vcur - vprev;  // (t+1) % 3: neither V(t) nor V(t-1)
-#if PLLM_ABL == 1  // diagnostic: no K/V loads after the first tile (stale registers restaged)
-      if (t == 0 && t + 1 < ntiles) gload(t + 1);
-#else
-      if (t + 1 < ntiles) gload(t + 1);
-#endif
-      const int kv0 = t * BN;
-      const int mask = (kv0 < qend[0] ? 1 : 0) | (kv0 < qend[1] ? 2 : 0);
-      const uint16_t* Kb = smem + buf * TILE;
-      const uint16_t* Vb = smem + 2 * TILE + vcur * TILE;
-      const uint16_t* Vp = smem + 2 * TILE + vprev * TILE;
-      auto tile = [&](auto mask_c) {
-        constexpr int MASK = decltype(mask_c)::value;
-        f32x16 s[2][2];
-        s[0][0] = s[0][1] = s[1][0] = s[1][1] = zero16();
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-          for (int ks = 0; ks < NKS; ++ks) {
-            const bf16x8 kf = as_frag(ld16(Kb + kb * 32 * D + (fk ^ (ks << 4))));
-#pragma unroll
-            for (int j = 0; j < 2; ++j)
-              if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
-          }
-        if constexpr (MASK == 3 && kFwdSched) {
-          // K fragment reads one to two fragments ahead of the MFMAs that consume them (left to
-          // itself hipcc waited lgkmcnt(0) right before each pair of MFMAs)
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-#pragma unroll
-          for (int i = 0; i < 2 * NKS - 2; ++i) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
-        }
-        float mx2[2] = {-INFINITY, -INFINITY};
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          if (!((MASK >> j) & 1)) continue;
-          const int qi = qw[j] + r;
-          if ((kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off)) {
-            const int lim0 = (a.causal ? min(a.S - 1, qi + off) : a.S - 1) - (kv0 + 4 * hh);
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) s[j][kb][i] = acc_row(i, 0) > lim0 - 32 * kb ? -INFINITY : s[j][kb][i];
-          }
-          float mx0 = -INFINITY, mx1 = -INFINITY;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            mx0 = fmaxf(mx0, s[j][0][i]);
-            mx1 = fmaxf(mx1, s[j][1][i]);
-          }
-          float mx = fmaxf(mx0, mx1);
-          mx2[j] = fmaxf(mx, __shfl_xor(mx, 32, 64)) * c2;
-        }
-        const bool r0 = (MASK & 1) && __any(mx2[0] - m[0] > kLazyThr);
-        const bool r1 = (MASK & 2) && __any(mx2[1] - m[1] > kLazyThr);
-        if (r0 || r1) {  // rare
-          if (pend && r1) {  // retire the pending P.V at the old max, then region 2 adds zeros
-            pv(I1{}, pfp, Vp);
-#pragma unroll
-            for (int kst = 0; kst < 4; ++kst) pfp[kst] = zero_frag();
-          }
-          if (r0) rescale(I0{}, mx2[0]);
-          if (r1) rescale(I1{}, mx2[1]);
-        }
-        // region 2 (one code path per MASK: a second variant of it doubled the live ranges the
-        // register allocator saw and spilled).  Without a pending P.V (first tile of block 1),
-        // pfp is zero and the current V tile stands in (finite data, adds nothing).
-        if constexpr (MASK == 3 && kFwdSched) {
-          // hand interleave (sched_barrier fences: hipcc otherwise clusters the MFMAs and the
-          // exponentials): each of the 4 NDB MFMAs of one block's P.V is followed by the softmax
-          // of 32 / (4 NDB) elements of the other block, with the next V fragment read issued one
-          // MFMA ahead
-          pvx(I1{}, pfp, pend ? Vp : Vb, I0{}, s[0]);
-          bf16x8 pf0[4];
-          packp(s[0], pf0);
-          pvx(I0{}, pf0, Vb, I1{}, s[1]);
-          packp(s[1], pfp);
-        } else {
-          if constexpr ((MASK & 2) != 0) pv(I1{}, pfp, pend ? Vp : Vb);
-          if constexpr ((MASK & 1) != 0) {
-            bf16x8 pf0[4];
-            sexp(I0{}, s[0], pf0);
-            pv(I0{}, pf0, Vb);
-          }
-          if constexpr ((MASK & 2) != 0) sexp(I1{}, s[1], pfp);
-        }
-        pend = (MASK & 2) != 0;
-      };
-      if (mask == 3) tile(std::integral_constant<int, 3>{});
-      else if (mask == 1) tile(std::integral_constant<int, 1>{});
-      else if (mask == 2) tile(std::integral_constant<int, 2>{});
-      else if (pend) {  // both blocks done with keys: retire the pending P.V
-        pv(I1{}, pfp, Vp);
-        pend = false;
-      }
-#if PLLM_ABL == 2  // diagnostic: no LDS restage, no barrier (every tile reads tile 0's images)
-      (void)vnext;
-#elif PLLM_ABL == 3  // diagnostic: restage without the barrier
-      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, vnext);
-#else
-      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, vnext);
-      __syncthreads();
-#endif
-      vprev = vcur;
-      vcur = vnext;
-    }
-    if (pend) pv(I1{}, pfp, smem + 2 * TILE + vprev * TILE);
-  } else if constexpr (V3) {
-    // ---- exponent-ready scores ---------------------------------------------------------------
-    // Q is prescaled by scale log2(e), so S' = Q'K^T - m is already the exponent: the MFMA chain
-    // of every score block starts from a register block holding -m (nm, the chain's C operand)
-    // and p = exp2(S') needs no per-element multiply-add.  m is set from the row max on a block's
-    // first live tile and moved lazily (when a row's tile max exceeds it by kLazyThr, as in the
-    // plain loop), the rare move shifting S' and the -m block.
-    f32x16 nm[QB];
-    bool started[QB];
-#pragma unroll
-    for (int j = 0; j < QB; ++j) {
-      nm[j] = zero16();
-      started[j] = false;
-    }
-    for (int t = 0; t < ntiles; ++t) {
-      const int buf = t & 1;
-      if (t + 1 < ntiles) gload(t + 1);
-      const int kv0 = t * BN;
-      const int mask = (kv0 < qend[0] ? 1 : 0) | (QB > 1 && kv0 < qend[QB - 1] ? 2 : 0);
-      const uint16_t* Kb = smem + buf * TILE;
-      const uint16_t* Vb = smem + 2 * TILE + buf * TILE;
-      auto tile = [&](auto mask_c) {
-        constexpr int MASK = decltype(mask_c)::value;
-        f32x16 s[QB][2];
-        auto qk = [&](auto only_c) {  // only_c: -1 = every live block, else that block alone
-          constexpr int ONLY = decltype(only_c)::value;
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int ks = 0; ks < NKS; ++ks) {
-              const bf16x8 kf = as_frag(ld16(Kb + kb * 32 * D + (fk ^ (ks << 4))));
-#pragma unroll
-              for (int j = 0; j < QB; ++j)
-                if (((MASK >> j) & 1) && (ONLY < 0 || ONLY == j))
-                  s[j][kb] = mfma32(kf, qf[j][ks], ks == 0 ? nm[j] : s[j][kb]);
-            }
-        };
-        qk(std::integral_constant<int, -1>{});
-        bf16x8 pf[QB][4];
-#pragma unroll
-        for (int j = 0; j < QB; ++j) {
-          if (!((MASK >> j) & 1)) continue;
-          const int qi = qw[j] + r;
-          const bool need_mask = (kv0 + BN > a.S) || (a.causal && kv0 + BN - 1 > qw[j] + off);
-          const int lim0 = (a.causal ? min(a.S - 1, qi + off) : a.S - 1) - (kv0 + 4 * hh);
-          auto apply_mask = [&]() {
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) s[j][kb][i] = acc_row(i, 0) > lim0 - 32 * kb ? -INFINITY : s[j][kb][i];
-          };
-          auto rowmax = [&]() {
-            float mx0 = -INFINITY, mx1 = -INFINITY;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              mx0 = fmaxf(mx0, s[j][0][i]);
-              mx1 = fmaxf(mx1, s[j][1][i]);
-            }
-            const float mx = fmaxf(mx0, mx1);
-            return fmaxf(mx, __shfl_xor(mx, 32, 64));
-          };
-          auto shift = [&](float dm) {  // S' -= dm, m += dm, -m block follows
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) s[j][kb][i] -= dm;
-            m[j] += dm;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) nm[j][i] = -m[j];
-          };
-          auto expsum = [&]() {
-            float ls0 = 0.f, ls1 = 0.f;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const float p0 = fast_exp2(s[j][0][i]);
-              const float p1 = fast_exp2(s[j][1][i]);
-              s[j][0][i] = p0;
-              s[j][1][i] = p1;
-              ls0 += p0;
-              ls1 += p1;
-            }
-            return ls0 + ls1;
-          };
-          if (need_mask) apply_mask();
-          const float mx = rowmax();  // relative to the current reference m
-          if (!started[j]) {  // wave-uniform: the block's first live tile sets m
-            m[j] = 0.f;
-            shift(mx == -INFINITY ? 0.f : mx);
-            started[j] = true;
-          } else if (__any(mx > kLazyThr)) {  // rare: move the reference max
-            const float dm = fmaxf(mx, 0.f);
-            const float alpha = fast_exp2(-dm);
-#pragma unroll
-            for (int db = 0; db < NDB; ++db)
-#pragma unroll
-              for (int i = 0; i < 16; ++i) o[j][db][i] = o[j][db][i] * alpha;
-            l[j] *= alpha;
-            shift(dm);
-          }
-          const float ls = expsum();
-          l[j] += ls;
-#pragma unroll
-          for (int kb = 0; kb < 2; ++kb) {
-            pf[j][2 * kb] = pack_frag(s[j][kb], 0);
-            pf[j][2 * kb + 1] = pack_frag(s[j][kb], 1);
-          }
-        }
-#pragma unroll
-        for (int kst = 0; kst < 4; ++kst)
-#pragma unroll
-          for (int db = 0; db < NDB; ++db) {
-            const int rb = kst * 16 * D;
-            const bf16x8 va = cat_tr(ds_tr(Vb + rb + (fv0 ^ (db << 5))), ds_tr(Vb + rb + (fv8 ^ (db << 5))));
-#pragma unroll
-            for (int j = 0; j < QB; ++j)
-              if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
-          }
-      };
-      if (mask == 3) tile(std::integral_constant<int, 3>{});
-      else if (mask == 1) tile(std::integral_constant<int, 1>{});
-      else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
-      if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
-      __syncthreads();
-    }
-  } else
   for (int t = 0; t < ntiles; ++t) {
 #if PLLM_FWD_STAMPS
     uint64_t ts_prev = __builtin_amdgcn_s_memtime();
@@ -786,7 +271,7 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
             if ((MASK >> j) & 1) s[j][kb] = mfma32(kf, qf[j][ks], s[j][kb]);
         }
       }
-      if constexpr (MASK == 3 && QB == 2 && kFwdSgb) {
+      if constexpr (MASK == 3 && QB == 2) {
         // K fragment reads issued ahead of the MFMA pairs that consume them (hipcc's own order
         // waited lgkmcnt(0) before every pair)
         __builtin_amdgcn_sched_group_barrier(0x100, 2, 2);
@@ -867,7 +352,7 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
             if ((MASK >> j) & 1) o[j][db] = mfma32(va, pf[j][kst], o[j][db]);
         }
       }
-      if constexpr (MASK == 3 && QB == 2 && kFwdSgb) {
+      if constexpr (MASK == 3 && QB == 2) {
         // V transposed reads two steps (4 reads) ahead of their MFMA pairs
         __builtin_amdgcn_sched_group_barrier(0x100, 4, 3);
 #pragma unroll
@@ -957,7 +442,6 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnBwdArgs a) {
 //     (profiles/r2_attn_bwd_persistent_negative.jsonl);
 //   * delta = rowsum(dO O) formed in this kernel from O rows staged beside dO, instead of the
 //     attn_bwd_pre_kernel pass: 3-4 % slower (profiles/r2_attn_delta_fused_negative.txt).
-constexpr float kLog2e = 1.4426950408889634f;
 
 template <int D>
 struct BwdCfg {
@@ -1073,18 +557,13 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // Pieces of 1 KiB = QRP rows; lane l fills row blk * QRP + l / CPR at chunk position l % CPR,
   // which holds logical chunk (l % CPR) ^ I::f(row) (the image's swizzle, applied to the source)
   constexpr bool QDMA = ROPE == 0;
-  constexpr bool kQSpread = QDMA && PLLM_BWD_QSPREAD != 0;
-  // kQAsym: the older half of the waves issues every piece (twice as many each) while the SIMD
-  // partners of the other half (priority 1) start their dQ tasks on the matrix pipe
-  constexpr bool kQAsym = QDMA && !kQSpread && PLLM_BWD_QASYM != 0;
-  constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW * (kQAsym ? 2 : 1);
+  constexpr int QRP = 512 / D, QNP = BQ / QRP, QPPW = 2 * QNP / C::NW;
   static_assert(2 * QNP % C::NW == 0, "Q/dO pieces per wave");
   u32x4 qr[QDMA ? 1 : 2 * QPAIR], dor[QDMA ? 1 : 2 * QPAIR];
   uint32_t qvo[QPPW];
-  const bool qloader = !kQAsym || w < C::NW / 2;
 #pragma unroll
   for (int k = 0; k < QPPW; ++k) {
-    const int pc = (kQAsym ? (w % (C::NW / 2)) : w) * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;
     const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
     qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
   }
@@ -1104,7 +583,6 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
   };
   auto qdma = [&](int it) {
-    if (!qloader) return;
     i32x4v qs, os;
     qdma_srd(it, qs, os);
 #pragma unroll
@@ -1253,10 +731,6 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       if (it + 1 < total) gload(it + 1);
     }
     PLLM_BSTAMP(2);
-#if PLLM_BWD_STAGGER > 0
-    // diagnostic: delay the second half of the workgroup (the SIMD partners of waves 0-3)
-    if (__builtin_amdgcn_readfirstlane(w) >= 4) __builtin_amdgcn_s_sleep(PLLM_BWD_STAGGER);
-#endif
 
     // rows past T need no mask: their Q / dO rows are zero-filled, their row constants 0
     const bool need_mask = (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
@@ -1413,15 +887,9 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
           const bool live = qn + (tid & (BQ - 1)) < a.T;
           rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
         }
-        if constexpr (!kQSpread) qdma(it + 1);
+        qdma(it + 1);
       }
     }
-    // kQSpread: the pieces go out one per BK / 16 / QPPW MFMAs of the dQ task below (a burst of
-    // them here cost ~190 cycles each, profiles/r3_attn_bwd_stamps.md)
-    i32x4v nqs, nos;
-    int nsent = 0;
-    const bool spread = kQSpread && it + 1 < total;
-    if (spread) qdma_srd(it + 1, nqs, nos);
     PLLM_BSTAMP(4);
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
@@ -1449,13 +917,6 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
         const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
-        if constexpr (kQSpread) {
-          constexpr int EVERY = BK / 16 / QPPW;
-          if (spread && ti == 0 && ks % EVERY == EVERY - 1) {
-            qdma_piece(nqs, nos, ks / EVERY);
-            ++nsent;
-          }
-        }
       }
       float lo[8], hi[8];
 #pragma unroll
@@ -1467,13 +928,6 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       dqv[ti][1] = pack8(hi);
       dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
                 ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
-    }
-    if constexpr (kQSpread) {
-      // a wave whose dQ task did not run (ragged last query block) sends its pieces here
-      if (spread && nsent == 0) {
-#pragma unroll
-        for (int k = 0; k < QPPW; ++k) qdma_piece(nqs, nos, k);
-      }
     }
     PLLM_BSTAMP(5);
 #if PLLM_BWD_STAMPS
@@ -1971,27 +1425,31 @@ namespace pllm {
 
 bool attn_supported_head_dim(int D) { return D == 32 || D == 64 || D == 128; }
 
-int attn_bwd_key_block(int D) { return D == 128 ? RsCfg<128>::BK : BwdCfg<64>::BK; }
-
-// PLLM_ATTN_FWD_PIPE=1 selects the software-pipelined tile loop for D <= 64 (A/B switch)
-static bool attn_fwd_pipe() {
-  static const bool on = [] {
-    const char* e = std::getenv("PLLM_ATTN_FWD_PIPE");
-    return e && e[0] == '1';  // opt-in: measured no faster than the plain loop (profiles/r3_attn_fwd_*)
-  }();
-  return on;
+// key-stationary backward (attn_bwd_ks.hip) per head dim, a bit mask (1: D = 64, 2: D = 128): initial
+// value from PLLM_ATTN_BWD_KS (comma list of head dims, default "128"), runtime A/B via attn_bwd_set_ks
+static int g_attn_ks = -1;
+static bool attn_bwd_ks(int D) {
+  if (g_attn_ks < 0) {
+    const char* e = std::getenv("PLLM_ATTN_BWD_KS");
+    const char* v = e ? e : "128";
+    g_attn_ks = (std::strstr(v, "64") ? 1 : 0) | (std::strstr(v, "128") ? 2 : 0);
+  }
+  return (D == 64 && (g_attn_ks & 1)) || (D == 128 && (g_attn_ks & 2));
 }
+void attn_bwd_set_ks(int mask) { g_attn_ks = mask & 3; }
+
+int attn_bwd_key_block(int D) {
+  if (attn_bwd_ks(D)) return attn_bwd_ks_key_block();
+  return D == 128 ? RsCfg<128>::BK : BwdCfg<64>::BK;
+}
+bool attn_bwd_uses_ks(int D) { return attn_bwd_ks(D); }
 
 template <int D>
 static void attn_fwd_t(const AttnFwdArgs& a, hipStream_t st) {
   const int nqb = (a.T + FwdCfg<D>::BM - 1) / FwdCfg<D>::BM;
   const dim3 grid(nqb * a.B * a.H), blk(64 * FwdCfg<D>::NW);
   if (a.rope_cos) hipLaunchKernelGGL((attn_fwd_kernel<D, true>), grid, blk, 0, st, a);
-  else if constexpr (PLLM_FWD_V3 != 0) hipLaunchKernelGGL((attn_fwd_kernel<D, false, false, true>), grid, blk, 0, st, a);
-  else if constexpr (FwdCfg<D>::QB == 2) {
-    if (attn_fwd_pipe()) hipLaunchKernelGGL((attn_fwd_kernel<D, false, true>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, blk, 0, st, a);
-  } else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, blk, 0, st, a);
+  else hipLaunchKernelGGL((attn_fwd_kernel<D, false>), grid, blk, 0, st, a);
 }
 
 template <int D, int ROPE>
@@ -2053,8 +1511,35 @@ static void attn_bwd_rs_r(const AttnBwdArgs& a, hipStream_t st) {
   else attn_bwd_rs_t<D, 2>(a, st);
 }
 
-// D = 32 / 64: fused-role kernel; D = 128: role-split kernel
+// key-stationary backward (attn_bwd_ks.hip): delta pre-pass, then per pass of key blocks the main kernel
+// and the ordered slab reduce
+template <int D>
+static void attn_bwd_ks_t(AttnBwdArgs a, hipStream_t st) {
+  const int64_t nrows = (int64_t)a.B * a.T * a.H;
+  const int pre_grid = (int)((nrows * (D / 8) + 255) / 256);
+  const int BK = attn_bwd_ks_key_block();
+  const int nkb = (a.S + BK - 1) / BK;
+  const int red_grid = a.B * a.H * a.nqt;  // one workgroup per 32-query tile
+  if (!a.delta_ready) hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  const int per = a.nkb_pass;
+  for (int kb0 = 0; kb0 < nkb; kb0 += per) {
+    a.kb0 = kb0;
+    a.nkb_pass = min(per, nkb - kb0);
+    attn_bwd_ks_launch(a, st);
+    if (a.rope_cos) hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, 256, 2>), dim3(red_grid), dim3(64 * (D / 32)), 0, st, a);
+    else hipLaunchKernelGGL((attn_dq_reduce_frag_kernel<D, 256, 0>), dim3(red_grid), dim3(64 * (D / 32)), 0, st, a);
+    a.nkb_pass = per;
+  }
+}
+
+// D = 32 / 64: fused-role kernel; D = 128: role-split kernel; the key-stationary kernel where
+// attn_bwd_ks(D) (q / k pre-rotated: the binding rotates them first when rope_in is set)
 void attn_bwd(const AttnBwdArgs& a, hipStream_t st) {
+  if (attn_bwd_ks(a.D) && !(a.rope_cos && a.rope_in)) {
+    if (a.D == 64) attn_bwd_ks_t<64>(a, st);
+    else attn_bwd_ks_t<128>(a, st);
+    return;
+  }
   if (a.D == 32) attn_bwd_r<32>(a, st);
   else if (a.D == 64) attn_bwd_r<64>(a, st);
   else attn_bwd_rs_r<128>(a, st);

@@ -1,0 +1,408 @@
+// Key-stationary causal flash-attention backward for gfx950 (round 5; D = 64 / 128), replacing the
+// role-split D = 128 kernel of attention.hip.  Reference math: /root/reference/src/models/attention.py:47-57
+// (q k^T * hd^-1/2, causal masked_fill, softmax, @ v), whose backward this is.
+//
+// Register-class discipline (the reason this file exists apart from attention.hip): every MFMA is an
+// inline-asm statement with an explicit register class -- the dK^T / dV^T accumulators ("+a") own
+// the 256 AGPRs, the S / dP / dQ chains ("+v") the arch VGPRs.  Left to itself hipcc put the S and dQ
+// accumulators into AGPRs, pushed dK / dV into VGPRs and spilled 400-1000 registers at D = 128, or
+// copied all 256 accumulators between the two files at every join of the per-case code paths.
+// Hazards the compiler does not pad for asm (cdna_hip_programming.md §5.7): each MFMA statement opens
+// with s_nop 1 (a VALU-written A / B / C operand; free while the previous MFMA occupies the pipe), an
+// accumulate chain into the same C needs nothing, and mfma_settle() (18 wait states, taking the
+// result as an operand so every consumer is ordered after it) precedes any non-MFMA reader.
+#include <type_traits>
+
+#include "attn_common.h"
+#include "common.h"
+#include "kernels.h"
+
+namespace {
+
+// v_mfma_f32_32x32x16_bf16 with the accumulator in arch VGPRs: acc (+)= A B
+PLLM_DEV void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+}
+PLLM_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+}
+// ... with the accumulator pinned to the accumulator file
+PLLM_DEV void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+}
+// an MFMA result read by anything but the next MFMA of its chain: 16-pass XDL -> 18 wait states
+PLLM_DEV void mfma_settle(f32x16& x) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x)); }
+PLLM_DEV void mfma_settle(f32x16& x, f32x16& y) {
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x), "+v"(y));
+}
+
+// ---------------------------------------------------------------------------
+// Key-stationary backward ("KS", round 5; D = 64 / 128): one workgroup = 4 waves, ONE per SIMD
+// (512 registers each) = 256 keys of one (batch, kv-head).  Wave w owns keys k0 + 64 w + [0, 64) as
+// two 32-key blocks and keeps, across the whole sweep over the query slices of every query head of
+// the group, their dK^T / dV^T accumulators (D = 128: 256 registers) and their V rows as MFMA B
+// fragments in registers; K lives in one LDS image (S's B fragments by row reads, dQ's A operand by
+// transposed reads).  A slice is BQ = 128 / NDB queries (D = 128: 32, D = 64: 64), so the slice's dQ
+// tile is exactly 4 tasks of 32 queries x 32 head dims: one per wave, summed over all 256 keys
+// (16 MFMAs) from the slice's dS^T image and stored as one bf16 fragment block per key block (the
+// same slab format as the other kernels, reduced by attn_dq_reduce_frag_kernel<D, 256>).
+// vs the role-split kernel it replaces at D = 128 (128 keys, 8 waves, P handed between wave pairs
+// through LDS behind a barrier per 32-query sub-block, Q / dO staged through registers): ONE barrier
+// per slice (double-buffered Q / dO / dS^T images and row constants: the next slice's Q / dO DMA is
+// issued right after the barrier and waited just before the next one), half the dQ slab bytes
+// (256-key blocks), no P hand-off, and every Q / dO / K fragment read feeds both key blocks.
+// Guide: cdna_hip_programming.md Appendix B 'Attention backward' (key on the lane, row constants as
+// the initial accumulator, one LDS image per operand for row and transposed reads).
+template <int D>
+struct KsCfg {
+  static_assert(D == 64 || D == 128, "key-stationary backward: D = 64 / 128");
+  static constexpr int NW = 4, NT = 256, BK = 256;
+  static constexpr int NDB = D / 32, NKS = D / 16;
+  static constexpr int NQB = 4 / NDB;        // 32-query sub-blocks per slice (one dQ task per wave)
+  static constexpr int BQ = 32 * NQB;        // queries per slice
+  static constexpr int CPR = D / 8;          // 16-B chunks per row
+  static constexpr int QRP = 512 / D;        // rows per 1-KiB DMA piece
+  static constexpr int QNP = BQ / QRP;       // pieces per Q (or dO) tile
+  static constexpr int QPPW = 2 * QNP / NW;  // Q + dO pieces per wave and slice
+  static constexpr int KPPW = BK / QRP / NW; // K image pieces per wave
+  static constexpr int TILE = BQ * D;        // elements of one Q (dO) tile
+  static constexpr int SIMG = BK * BQ;       // elements of one dS^T image [keys][BQ]
+  static constexpr int LDS_ELEMS = BK * D + 4 * TILE + 2 * SIMG;  // 128 KiB at D = 64 and 128
+};
+
+// dS^T image [256 keys][W = BQ queries] of the KS kernel: chunk ch (16 B) of row r at ch ^ f(r).
+// Stores: 16 B per lane, 8 consecutive key rows per 8-lane group at one logical chunk -> f is a
+// bijection on 8 consecutive rows modulo the 128-B bank window.  Transposed dQ reads: 4 consecutive
+// rows x the sub-block's 64 B; W = 32: 4 rows = 256 contiguous bytes (any f); W = 64: rows r and r+2
+// share banks, so f(r) ^ f(r + 2) has bit 2 set.  f depends on row bits 0..2 only: +16-row steps are
+// plain additions.
+template <int W>
+struct ImgT {
+  static PLLM_DEV int f(int r) {
+    if constexpr (W == 32) return (r >> 1) & 3;
+    else return (((r >> 1) & 1) << 2) | ((r & 1) << 1) | ((r >> 2) & 1);
+  }
+  static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+};
+
+template <int D, int ROPE>
+__global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
+  static_assert(ROPE != 1, "KS backward: q / k pre-rotated (ROPE 0 or 2)");
+  using C = KsCfg<D>;
+  using I = Img<D>;
+  using IT = ImgT<C::BQ>;
+  constexpr int BK = C::BK, BQ = C::BQ, NQB = C::NQB, NKS = C::NKS, NDB = C::NDB, CPR = C::CPR;
+  constexpr int TILE = C::TILE, SIMG = C::SIMG, QRP = C::QRP, QNP = C::QNP, QPPW = C::QPPW;
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[C::LDS_ELEMS];
+  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BQ];  // per slot: -lse log2(e), -delta
+  uint16_t* const Kl = smem;
+  uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
+  uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
+
+  const int BH = a.B * a.Hkv;
+  const int id = blockIdx.x;
+  const int kb = a.kb0 + id / BH;  // lowest key blocks (longest causal sweeps) of every head first
+  const int bh = id % BH;
+  const int b = bh / a.Hkv, hk = bh % a.Hkv;
+  const int G = a.H / a.Hkv;
+  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = kb * BK, kw0 = k0 + 64 * w;
+  const int off = a.S - a.T;
+  const unsigned lds0 = (unsigned)(uintptr_t)smem;
+  const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
+  const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
+
+  // ---- sweep bounds: (query head of the group, BQ-query slice), causal slices from the key block on
+  const int nqs = (a.T + BQ - 1) / BQ;
+  const int qs_start = a.causal ? max(0, k0 - off) / BQ : 0;
+  const int per_head = max(0, nqs - qs_start);
+  const int total = per_head * G;
+
+  // ---- K image by LDS DMA (lane l of piece p fills row p QRP + l / CPR at chunk position l % CPR,
+  // which holds logical chunk (l % CPR) ^ f(row): the swizzle applied to the source); keys past S
+  // read zeros (descriptor range)
+  {
+    const int rows = min(BK, a.S - k0);
+    const i32x4v ks = srd_of(kp + (int64_t)k0 * a.k_st, (uint32_t)(((int64_t)(rows - 1) * a.k_st + D) * 2));
+#pragma unroll
+    for (int k = 0; k < C::KPPW; ++k) {
+      const int p = w * C::KPPW + k, row = p * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
+      blds16(ks, (uint32_t)((row * a.k_st + 8 * ch) * 2), lds0 + 1024u * (unsigned)p);
+    }
+  }
+  // ---- Q / dO DMA of slice it into slot sl; per-lane source offsets: piece pc = w QPPW + k of the
+  // slice's 2 QNP pieces (first QNP: Q, then dO)
+  uint32_t qvo[QPPW];
+#pragma unroll
+  for (int k = 0; k < QPPW; ++k) {
+    const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
+    qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
+  }
+  auto slice_of = [&](int it, int& h, int& q0) {
+    h = hk * G + it / per_head;
+    q0 = (qs_start + it % per_head) * BQ;
+  };
+  auto qdma = [&](int it, int sl) {
+    int h, q0;
+    slice_of(it, h, q0);
+    const int rows = a.T - q0;
+    const i32x4v qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
+                             (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
+    const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
+                             (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
+#pragma unroll
+    for (int k = 0; k < QPPW; ++k) {
+      const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;  // wave-uniform
+      blds16(img == 0 ? qs : os, qvo[k], lds0 + 2u * (unsigned)(BK * D + 2 * sl * TILE + img * TILE) + 1024u * blk);
+    }
+  };
+  // row constants of slice it (threads < 2 BQ: -lse log2 e for rows [0, BQ), -delta after)
+  float rc = 0.f;
+  auto rload = [&](int it) {
+    if (tid < 2 * BQ) {
+      int h, q0;
+      slice_of(it, h, q0);
+      const float* base = tid < BQ ? a.lse : a.delta;
+      const int q = min(q0 + (tid & (BQ - 1)), a.T - 1);
+      rc = base[((int64_t)b * a.H + h) * a.T + q];
+    }
+  };
+  auto rstore = [&](int it) {
+    if (tid < 2 * BQ) {
+      int h, q0;
+      slice_of(it, h, q0);
+      const bool live = q0 + (tid & (BQ - 1)) < a.T;
+      rowc[it & 1][tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
+    }
+  };
+
+  // ---- V rows of this wave's keys as B fragments (k = head dim), zero past S
+  bf16x8 vf[2][NKS];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int key = kw0 + 32 * kh + r;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+      vf[kh][ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
+  }
+  if (total > 0) {
+    qdma(0, 0);
+    if (total > 1) qdma(1, 1);
+    rload(0);
+  }
+  vm_wait_all();
+  if (total > 0) {
+    rstore(0);
+    if (total > 1) rload(1);
+  }
+  __syncthreads();  // K image, slice 0 (and its row constants) landed for every wave
+
+  f32x16 dk[2][NDB], dv[2][NDB];
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      dk[kh][db] = zero16();
+      dv[kh][db] = zero16();
+    }
+  const float c2 = a.scale_log2;
+  const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
+  // per-lane LDS element offsets, swizzle applied once (see attn_bwd_kernel): row fragment reads
+  // fq ^ (ks << 4) + row-block base, transposed reads ft0 / ft8 ^ (db << 5) + (32 j + 16 st) D
+  const int fq0 = I::off(r, 8 * hh);
+  const int ft00 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft80 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
+  const bool aligned = (off & 31) == 0 && kw0 + 64 <= a.S;
+  // dQ task of this wave: (32-query sub-block, 32-dim block)
+  const int tq_blk = w / NDB, tdb = w % NDB;
+  const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = 32 * tdb + 16 * g1 + 4 * tp;
+  const int sa00 = IT::off(8 * hh + tq, qc), sa40 = IT::off(8 * hh + tq + 4, qc);
+  const int ka00 = I::off(8 * hh + tq, dc), ka40 = I::off(8 * hh + tq + 4, dc);
+
+  int h = hk * G, qi = qs_start;  // (head, slice) of iteration it, advanced incrementally
+  for (int it = 0; it < total; ++it, (++qi == nqs) ? (qi = qs_start, ++h) : 0) {
+    const int sl = it & 1;
+    const int q0 = qi * BQ;
+    // per-lane offsets made opaque per slice: the XOR-swizzled addresses derived from them are then
+    // formed next to their reads instead of being hoisted out of the loop as ~50 live registers
+    int fq = fq0, ft0 = ft00, ft8 = ft80, sa0 = sa00, sa4 = sa40, ka0 = ka00, ka4 = ka40;
+    asm volatile("" : "+v"(fq), "+v"(ft0), "+v"(ft8), "+v"(sa0), "+v"(sa4), "+v"(ka0), "+v"(ka4));
+    const uint16_t* Ql = QOl + 2 * sl * TILE;
+    const uint16_t* Ol = Ql + TILE;
+    const float* rl = rowc[sl];
+    uint16_t* Sd = Sl + sl * SIMG;
+#pragma unroll
+    for (int j = 0; j < NQB; ++j) {
+      const int qj0 = q0 + 32 * j;
+      // body<L1, M0, M1>: key block 1 live (else its dS^T rows are zeros), per-element masks on the
+      // key blocks (compile-time per code path; lo: element i dead iff acc_row(i, 0) < lo)
+      // one key block (KH) of this wave: S = Q K^T, dP = dO V^T (key on the lane), P / dS, dV^T / dK^T
+      // updates, dS^T image rows.  ONE code path for every sub-block that has a live key: the
+      // causal / ragged-end mask is a wave-uniform branch around a VALU-only fix-up of P (element i
+      // dead iff acc_row(i, 0) < lo), and a fully masked key block simply adds zeros.  (Per-case code
+      // paths made hipcc copy the 256 dK / dV accumulator registers at every join.)  Key blocks run one
+      // after the other, each re-reading the Q / dO fragments: with both in flight it spilled.
+      const bool mask_j = !aligned || (a.causal && kw0 + 63 > qj0 + off);  // wave-uniform
+      auto block = [&](auto kh_c) {
+        constexpr int KH = decltype(kh_c)::value;
+        f32x16 sc, dp;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 rd = *reinterpret_cast<const f32x4*>(&rl[BQ + 32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) dp[4 * g + e] = rd[e];  // dP accumulated onto -delta
+        }
+#pragma unroll
+        for (int ks = 0; ks < NKS; ++ks) {
+          const int fo = fq ^ (ks << 4);
+          const bf16x8 qa = as_frag(ld16(Ql + 32 * j * D + fo));
+          const bf16x8 oa = as_frag(ld16(Ol + 32 * j * D + fo));
+          const bf16x8 kf = as_frag(ld16(Kl + (64 * w + 32 * KH) * D + fo));
+          if (ks == 0) mfma_v0(sc, qa, kf);
+          else mfma_v(sc, qa, kf);
+          mfma_v(dp, oa, vf[KH][ks]);
+        }
+        mfma_settle(sc, dp);
+        // P = exp2(S c2 - lse log2 e)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sc[4 * g + e] = fast_exp2(__builtin_fmaf(sc[4 * g + e], c2, rs[e]));
+        }
+        if (mask_j) {
+          const int key = kw0 + 32 * KH + r;
+          const int lo = key >= a.S ? 64 : (a.causal ? key - off - (qj0 + 4 * hh) : -64);
+#pragma unroll
+          for (int i = 0; i < 16; ++i) sc[i] = acc_row(i, 0) < lo ? 0.f : sc[i];
+        }
+        // dS = P (dP - delta)   (unscaled)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) dp[i] = sc[i] * dp[i];
+        const bf16x8 pf0 = pack_frag(sc, 0), pf1 = pack_frag(sc, 1);
+        const bf16x8 sf0 = pack_frag(dp, 0), sf1 = pack_frag(dp, 1);
+        // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] images)
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const int rb = (32 * j + 16 * st) * D, o0 = rb + (ft0 ^ (db << 5)), o8 = rb + (ft8 ^ (db << 5));
+            const bf16x8 oA = cat_tr(ds_tr(Ol + o0), ds_tr(Ol + o8));
+            const bf16x8 qA = cat_tr(ds_tr(Ql + o0), ds_tr(Ql + o8));
+            mfma_a(dv[KH][db], oA, st == 0 ? pf0 : pf1);
+            mfma_a(dk[KH][db], qA, st == 0 ? sf0 : sf1);
+          }
+        }
+        // dS^T image rows of these keys: group pairs of 4 queries swapped across the half-waves
+        // (v_permlane32_swap), one 16-B store of 8 consecutive queries per pair
+        const int row = 64 * w + 32 * KH + r;
+        u32x2 v[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const u32x4 w4 = __builtin_bit_cast(u32x4, g < 2 ? sf0 : sf1);
+          v[g] = u32x2{w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k += 2) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const auto sw = __builtin_amdgcn_permlane32_swap(v[k][d], v[k + 1][d], false, false);
+            v[k][d] = sw[0];
+            v[k + 1][d] = sw[1];
+          }
+          *reinterpret_cast<u32x4*>(Sd + IT::off(row, 32 * j + 8 * k + 8 * hh)) =
+              u32x4{v[k][0], v[k][1], v[k + 1][0], v[k + 1][1]};
+        }
+      };
+      // A sub-block whose keys all follow its queries (causal) is not skipped: its mask zeroes every
+      // P, so it adds nothing -- and with one wave per SIMD a skip saves no wall time (wave 0 is
+      // never dead and the slice ends at the barrier), while a branch around the dK / dV updates
+      // made hipcc copy the 256 accumulators at the join
+      block(std::integral_constant<int, 0>{});
+      block(std::integral_constant<int, 1>{});
+    }
+    // ---- hand-off: this slice's dS^T image and the next slice's Q / dO / row constants
+    vm_wait_all();  // own DMA pieces of slice it + 1, its row constants, this wave's previous dQ stores
+    if (it + 1 < total) rstore(it + 1);
+    __syncthreads();
+    if (it + 2 < total) {
+      qdma(it + 2, sl);  // every wave is past its reads of slot sl (slice it)
+      rload(it + 2);
+    }
+    // ---- dQ partial of this key block: dQ^T tile (32 dims x 32 queries) = K^T dS^T over 256 keys
+    const int qt0 = q0 + 32 * tq_blk;
+    if (qt0 < a.T) {
+      f32x16 acc;
+#pragma unroll
+      for (int ks = 0; ks < BK / 16; ++ks) {
+        const bf16x8 A = cat_tr(ds_tr(Sd + 16 * ks * BQ + sa0), ds_tr(Sd + 16 * ks * BQ + sa4));
+        const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
+        if (ks == 0) mfma_v0(acc, Bf, A);
+        else mfma_v(acc, Bf, A);
+        if (ks % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      }
+      mfma_settle(acc);
+      float lo[8], hi[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        lo[e] = acc[e];
+        hi[e] = acc[8 + e];
+      }
+      uint16_t* dqp = a.dq_acc + (kb - a.kb0) * a.slab +
+                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
+      st16(dqp, pack8(lo));
+      st16(dqp + 8, pack8(hi));
+    }
+  }
+  // ---- dK (scaled; RoPE: rotated back, R^T) and dV of this lane's keys: the accumulators settle
+  // (18 wait states after the last MFMA), then every one is pinned behind that statement
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh)
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) asm volatile("" : "+a"(dk[kh][db]), "+a"(dv[kh][db]));
+#pragma unroll
+  for (int kh = 0; kh < 2; ++kh) {
+    const int key = kw0 + 32 * kh + r;
+    if (key >= a.S) continue;
+    if (ROPE != 0) {
+      const float* cr = a.rope_cos + (int64_t)key * (D / 2);
+      const float* sr = a.rope_sin + (int64_t)key * (D / 2);
+#pragma unroll
+      for (int db = 0; db < NDB / 2; ++db)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int d = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
+          const float c = cr[d], sn = sr[d];
+          const float x = dk[kh][db][i], y = dk[kh][db + NDB / 2][i];
+          dk[kh][db][i] = x * c + y * sn;
+          dk[kh][db + NDB / 2][i] = y * c - x * sn;
+        }
+    }
+    store_row_bf16<NDB>(a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh, dk[kh], a.scale, hh);
+    store_row_bf16<NDB>(a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh, dv[kh], 1.f, hh);
+  }
+}
+
+
+}  // namespace
+
+namespace pllm {
+
+int attn_bwd_ks_key_block() { return KsCfg<128>::BK; }
+
+// one pass of key blocks [a.kb0, a.kb0 + a.nkb_pass) (the caller runs the delta pre-pass before and the
+// slab reduce after)
+void attn_bwd_ks_launch(const AttnBwdArgs& a, hipStream_t st) {
+  const dim3 grid(a.nkb_pass * a.B * a.Hkv), blk(256);
+  if (a.D == 64) {
+    if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks_kernel<64, 2>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_ks_kernel<64, 0>), grid, blk, 0, st, a);
+  } else {
+    if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks_kernel<128, 2>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((attn_bwd_ks_kernel<128, 0>), grid, blk, 0, st, a);
+  }
+}
+
+}  // namespace pllm

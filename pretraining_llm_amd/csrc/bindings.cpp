@@ -312,13 +312,7 @@ std::tuple<Tensor, Tensor> gemm_tn(const Tensor& a, const Tensor& b, const std::
     of32 = check_grad(*bias_acc, "bias_acc");
     TORCH_CHECK(bias_acc->numel() == N && bias_acc->is_contiguous(), "gemm_tn: bias_acc [N]");
   }
-  Tensor splitws;
   if (M > 0) {
-    const int64_t wsf = pllm::gemm_split_ws_floats((int)M, (int)N, (int)K, (int)epi, (int)T);
-    if (wsf > 0) {
-      splitws = at::empty({wsf}, a.options().dtype(at::kFloat));
-      g.splitws = splitws.data_ptr<float>();
-    }
     pllm::gemm_tn(g, (int)epi, cur_stream());
     if (bias_acc)
       pllm::col_reduce(g.colpart, pllm::gemm_colsum_groups((int)M, (int)K), (int)N, bias_acc->data_ptr(), of32, true,
@@ -566,7 +560,10 @@ void lse_merge_(Tensor& o_acc, Tensor& lse_acc, const Tensor& o, const Tensor& l
   const int64_t B = o.size(0), T = o.size(1), H = o.size(2), D = o.size(3);
   TORCH_CHECK(lse_acc.dim() == 3 && lse_acc.size(0) == B && lse_acc.size(1) == H && lse_acc.size(2) == T &&
                   lse.sizes() == lse_acc.sizes(), "lse_merge_: lse_acc / lse [B, H, T]");
-  TORCH_CHECK(D % 8 == 0 && D <= 128 && o_acc.stride(3) == 1 && o.stride(3) == 1, "lse_merge_: D % 8, unit head stride");
+  // a row's D / 8 lanes must sit in ONE wave (64 % (D / 8) == 0): every lane reads lse_acc before lane 0
+  // of the row writes the merged value (D = 48 / 80 / 96 would straddle two waves and race)
+  TORCH_CHECK(D % 8 == 0 && D <= 128 && 64 % (D / 8) == 0 && o_acc.stride(3) == 1 && o.stride(3) == 1,
+              "lse_merge_: D in {8, 16, 32, 64, 128}, unit head stride");
   for (int d = 0; d < 3; ++d)
     TORCH_CHECK(o_acc.stride(d) % 4 == 0 && o.stride(d) % 8 == 0, "lse_merge_: 16-B aligned rows");
   check_aligned16(o_acc, "o_acc");
@@ -971,9 +968,26 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   const int64_t per = std::max<int64_t>(1, std::min<int64_t>(nkb, ws_budget / std::max<int64_t>(1, slab_bytes)));
   Tensor dq_acc = at::empty({per, slab_elems}, q.options());  // bf16 partial slabs
   Tensor dq_sum = per < nkb ? at::empty({slab_elems}, q.options().dtype(at::kFloat)) : Tensor();
+  // the key-stationary backward stages q / k by LDS DMA: with in-kernel RoPE requested, rotate them
+  // here once (positions t + S - T for queries, s for keys) and run it on the rotated copies
+  Tensor qrot, krot;
+  const bool ks_rot = rope_cos && rope_in && pllm::attn_bwd_uses_ks((int)D);
+  if (ks_rot) {
+    const Tensor qc = q.contiguous(), kc = k.contiguous();
+    qrot = at::empty_like(qc);
+    krot = at::empty_like(kc);
+    if (B * T > 0)
+      pllm::rope(qc.data_ptr(), qrot.data_ptr(), rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), B * T,
+                 (int)T, (int)H, (int)H, (int)D, (int)(S - T), false, cur_stream());
+    if (B * S > 0)
+      pllm::rope(kc.data_ptr(), krot.data_ptr(), rope_cos->data_ptr<float>(), rope_sin->data_ptr<float>(), B * S,
+                 (int)S, (int)Hkv, (int)Hkv, (int)D, 0, false, cur_stream());
+  }
+  const Tensor& qx = ks_rot ? qrot : q;
+  const Tensor& kx = ks_rot ? krot : k;
   AttnBwdArgs a{};
-  a.q = (const uint16_t*)q.data_ptr();
-  a.k = (const uint16_t*)k.data_ptr();
+  a.q = (const uint16_t*)qx.data_ptr();
+  a.k = (const uint16_t*)kx.data_ptr();
   a.v = (const uint16_t*)v.data_ptr();
   a.o = (const uint16_t*)o.data_ptr();
   a.dO = (const uint16_t*)dout.data_ptr();
@@ -984,7 +998,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.dq_acc = (uint16_t*)dq_acc.data_ptr();
   a.dq_sum = dq_sum.defined() ? dq_sum.data_ptr<float>() : nullptr;
   a.kb0 = 0;
-  a.rope_in = rope_in ? 1 : 0;
+  a.rope_in = rope_in && !ks_rot ? 1 : 0;
   a.slab = slab_elems;
   a.nqt = (int)nqt;
   a.nkb_pass = (int)per;
@@ -992,8 +1006,8 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.dk = (uint16_t*)dk.data_ptr();
   a.dv = (uint16_t*)dv.data_ptr();
   a.B = B; a.H = H; a.Hkv = Hkv; a.T = T; a.S = S; a.D = D;
-  a.q_sb = q.stride(0); a.q_st = q.stride(1); a.q_sh = q.stride(2);
-  a.k_sb = k.stride(0); a.k_st = k.stride(1); a.k_sh = k.stride(2);
+  a.q_sb = qx.stride(0); a.q_st = qx.stride(1); a.q_sh = qx.stride(2);
+  a.k_sb = kx.stride(0); a.k_st = kx.stride(1); a.k_sh = kx.stride(2);
   a.v_sb = v.stride(0); a.v_st = v.stride(1); a.v_sh = v.stride(2);
   a.o_sb = o.stride(0); a.o_st = o.stride(1); a.o_sh = o.stride(2);
   a.do_sb = dout.stride(0); a.do_st = dout.stride(1); a.do_sh = dout.stride(2);
@@ -1033,13 +1047,13 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None, bool overwrite=False) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
-  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int split=-1, int persistent=-1) -> ()",
-        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc, int64_t sp, int64_t pe) {
-          pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc, (int)sp, (int)pe);
+  m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int persistent=-1) -> ()",
+        [](int64_t mf, int64_t gm, int64_t ph, int64_t rc, int64_t pe) {
+          pllm::gemm_set_config((int)mf, (int)gm, (int)ph, (int)rc, (int)pe);
         });
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
-  m.def("gemm_pp_set_stagger(int n) -> ()", [](int64_t n) { pllm::gemm_pp_set_stagger((int)n); });
   m.def("wgrad_set_hy(int on) -> ()", [](int64_t on) { pllm::wgrad_set_hy((int)on); });
+  m.def("attn_bwd_set_ks(int mask) -> ()", [](int64_t m) { pllm::attn_bwd_set_ks((int)m); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");

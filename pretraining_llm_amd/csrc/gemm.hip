@@ -400,19 +400,14 @@ static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
 static int g_gemm_phased = 4;
 // CUs the persistent grids leave free, for RCCL kernels overlapping the backward (world > 1)
 static int g_gemm_reserve = 0;
-// the ping-pong kernel's desynchronising tile split (end-of-tile epilogues 0/1/2/5/6/7), opt-in:
-// measured 6-10 % SLOWER at K = 768 (293 -> 311 us, GELU 376 -> 411), +2.5 % only on the plain
-// 32768x11008x2048 (profiles/r4_gemm_pp.md): the store bursts are not what a half-tile shift fixes
-static int g_gemm_split = 0;
 // 0: the persistent kernels (gemm_pp / wgrad_pp / this file's) launch one workgroup per tile instead
 // of one per CU, so the hardware deals tiles to whichever CUs are free (e.g. beside RCCL kernels)
 static int g_gemm_persistent = 1;
-void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus, int split, int persistent) {
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus, int persistent) {
   if (mfma == 16 || mfma == 32) g_gemm_mfma = mfma;
   if (group_m > 0) g_gemm_group_m = group_m;
   if (phased >= 0) g_gemm_phased = phased;
   if (reserve_cus >= 0) g_gemm_reserve = reserve_cus;
-  if (split >= 0) g_gemm_split = split;
   if (persistent >= 0) g_gemm_persistent = persistent;
 }
 
@@ -441,13 +436,6 @@ static int gemm_ctas() {
   return num_cus() - g_gemm_reserve > 8 ? num_cus() - g_gemm_reserve : 8;
 }
 int gemm_grid_cap() { return gemm_ctas(); }
-
-// workspace (floats) of the ping-pong kernel's desynchronising tile split for this call; 0 when
-// the call does not split
-int64_t gemm_split_ws_floats(int M, int N, int K, int epi, int T) {
-  if (!g_gemm_split || !gemm_uses_pp(K, epi, T)) return 0;
-  return gemm_pp_split_ws_floats(M, N, K, epi, gemm_ctas());
-}
 
 void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
   GemmArgs a = a0;

@@ -41,25 +41,11 @@
 #include "common.h"
 #include "kernels.h"
 
-// Ablation builds (scripts/build_variant.py gemm_pp.hip x.so -DPLLM_PP_EXP=n; numerics WRONG):
-// bit 0: the epilogue computes but stores nothing; bit 1: the main loop issues no DMA (stale LDS);
-// bit 2: non-temporal stores; bit 5: odd workgroups sleep ~half a tile first (epilogue bursts
-// desynchronised across CUs, at the price of the sleep); bit 6: s_memtime stamps of workgroup 0 (two K-tiles of its third
-// tile, 6 points per phase) written over the start of C (diagnostic: bench/gemm_pp_stamps.py);
-// bit 7: waves 4-7 at static priority 1 instead of per-segment flips.
-#ifndef PLLM_PP_EXP
-#define PLLM_PP_EXP 0
-#endif
-constexpr bool kPPStamps = (PLLM_PP_EXP & 64) != 0;
-#ifndef PLLM_PP_DMA_MFMA
-#define PLLM_PP_DMA_MFMA 0
-#endif
-// the K-tile DMA pieces issued between the phase's own MFMAs (after MFMAs 4 and 12) instead of in
-// its LOAD segment: an LDS-DMA piece costs ~60 cycles among bare MFMAs but 100-185 in a LOAD segment
-// that also carries fragment reads (MI355X_MICROARCH.md, per-instruction constants)
-constexpr bool kPPDmaMfma = PLLM_PP_DMA_MFMA != 0;
-constexpr bool kPPStaticPrio = (PLLM_PP_EXP & 128) != 0;  // bit 7: waves 4-7 at priority 1, no flips
-constexpr int kPPStampN = 52;  // per wave
+// Measured and removed in round 5 (records kept in profiles/): a desynchronising tile split (odd
+// workgroups run half of their last tile first and park it; slower, r4_gemm_pp_split_ab.jsonl), a
+// start-time stagger of odd workgroups, the K-tile DMA pieces issued among the MFMAs instead of in the
+// LOAD segment (PLLM_PP_DMA_MFMA), a static priority for waves 4-7 instead of per-segment flips, and the
+// ablation / s_memtime-stamp diagnostic builds.
 
 namespace {
 
@@ -120,11 +106,7 @@ constexpr int kStQ(int q) {
 }
 
 PLLM_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
-  if constexpr (PLLM_PP_EXP & 1) {
-    asm volatile("" ::"v"(v), "v"(off));
-  } else {
-    __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, (PLLM_PP_EXP & 4) ? 2 : 0);
-  }
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
 PLLM_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
 PLLM_DEV float pp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
@@ -355,8 +337,6 @@ struct PPCtx {
   int w, wr, wc, lane;
   unsigned lds;           // byte address of the LDS array
   uint16_t* aux;          // this wave's 4 KiB bias / aux staging area (after the two K-tile slots)
-  bool stamp;             // kPPStamps: this workgroup records
-  uint64_t* stamp_at;     // kPPStamps: this wave's stamp area (in the LDS array)
   uint32_t vo[2][2];      // per-lane DMA source offsets of this wave's pieces of groups 0 (A) / 1 (B)
                           // (groups 3 / 2 are the same rows + 64 (A) / + 32 (B): descriptor base)
   uint32_t vaux;          // per-lane source offset of the aux DMA (row lane / 4, 16-B chunk lane % 4)
@@ -367,49 +347,6 @@ struct PPEpi {  // the tile whose (quadrant) epilogue is in flight
   int tm, tn;
   bool valid;   // false: the kernel's first tile has no predecessor (stores go nowhere)
 };
-
-PLLM_DEV void pp_stamp(const PPCtx& c, int idx) {
-  if constexpr (kPPStamps) {
-    if (c.stamp && idx >= 0) {
-      const uint64_t t = __builtin_amdgcn_s_memtime();
-      if (c.lane == 0) c.stamp_at[idx] = t;
-    }
-  }
-}
-
-// The desynchronising split's parked partial tile: this wave's 128 accumulator floats per lane in
-// their register order, 32 x 1 KiB coalesced stores into the workgroup's 256 KiB workspace slot (as
-// many as an end-of-tile epilogue: the following counted waits still hold), added back before the
-// same tile's epilogue at the end of the workgroup's work.
-// (not with the column-sum epilogues 3 / 4: their branch around the 16 aux rows spills)
-template <int EPI, bool QE>
-constexpr bool kPPSplit = !QE && EPI != 3 && EPI != 4;
-PLLM_DEV __amdgpu_buffer_rsrc_t pp_park_rsrc(const PPCtx& c, int lid) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(c.g->splitws + (int64_t)lid * PT * PT), (short)0, PT * PT * 4,
-                                           0x00020000);
-}
-PLLM_DEV void pp_park(f32x4 (&acc)[4][8], const PPCtx& c, int lid) {
-  const __amdgpu_buffer_rsrc_t r = pp_park_rsrc(c, lid);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), r,
-                                             (uint32_t)((((c.w * 4 + i) * 8 + j) * 64 + c.lane) * 16), 0, 0);
-}
-PLLM_DEV void pp_unpark(f32x4 (&acc)[4][8], const PPCtx& c, int lid) {
-  const __amdgpu_buffer_rsrc_t r = pp_park_rsrc(c, lid);
-  // the accumulators START from the parked partial (the finishing segment's first K-tile is a
-  // plain accumulating one).  Device-scope loads: the partial was written by this same wave long
-  // before, only this CU's L1 could hold a stale copy of the lines
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      acc[i][j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                r, (uint32_t)((((c.w * 4 + i) * 8 + j) * 64 + c.lane) * 16), 0, 16));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // Descriptors of the DMA target K-tile's A and B panels (256 rows from the K-tile's first column,
 // range-checked: rows past M / N read zeros); valid = false: empty ranges (the same instructions
@@ -471,7 +408,6 @@ PLLM_DEV void pp_group(const PPCtx& c, const PPSrd& srd, int sl, i32x4v& r, unsi
 template <int PH>
 PLLM_DEV void pp_piece(const PPCtx& c, const i32x4v& r, unsigned lds0, int q) {
   constexpr bool isA = PH == 0 || PH == 3;
-  if constexpr ((PLLM_PP_EXP & 2) != 0) return;  // ablation: no DMA in the main loop
   blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
 }
 template <int PH, int EPI = 0>
@@ -672,8 +608,7 @@ constexpr int pp_phase_ops(bool F, bool L, int q) {
 // the DMA wait of phase PH (piece group PH - 2 landed): everything issued in phases PH - 1, PH
 template <int EPI, bool QE, bool F, bool L, int PH>
 constexpr int pp_dma_wait() {
-  // (kPPDmaMfma: this phase's 2 DMA ops are issued after the wait, among its MFMAs)
-  int n = pp_phase_ops<EPI, QE>(F, L, PH) - (kPPDmaMfma ? 2 : 0);
+  int n = pp_phase_ops<EPI, QE>(F, L, PH);
   n += PH >= 1 ? pp_phase_ops<EPI, QE>(F, L, PH - 1) : pp_phase_ops<EPI, QE>(false, F, 3);
   if constexpr (!QE) {
     if (F && PH < 2) n += kEndStores<EPI>;  // the end-of-tile epilogue's stores
@@ -692,11 +627,9 @@ constexpr int pp_aux_wait() {
 // The epilogue goes first: the fragments it would otherwise overlap are not live yet.
 template <int PH, bool FIRST, bool LAST, int EPI, bool QE>
 PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
-                       const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl, int sk,
+                       const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl,
                        const PPEpi& pe, const PPEpi& ce, float (&dsum)[4]) {
   const int wr = c.wr, wc = c.wc;
-  const int st0 = sk < 0 ? -1 : 24 * sk + 6 * PH;  // stamp indices of this phase (kPPStamps)
-  pp_stamp(c, st0);
   if constexpr (QE) {
     u32x4 ax[4];
     if constexpr (FIRST) {
@@ -708,7 +641,6 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
     if constexpr (FIRST) pp_epi_quad<EPI, PH>(acc, c, pe, ax, dsum);
     __builtin_amdgcn_sched_barrier(0);
   }
-  pp_stamp(c, st0 < 0 ? -1 : st0 + 1);
   // ---- fragment reads: 12 / 4 / 8 / 4 (snake order: A rows half + column pair, then pair 1,
   // rows half 1, pair 0 again; one column-pair set of registers)
   {
@@ -735,20 +667,15 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   i32x4v gr;
   unsigned glds;
   pp_group<PH, EPI>(c, srd, nsl, gr, glds);
-  if constexpr (!kPPDmaMfma) {
-    pp_piece<PH>(c, gr, glds, 0);
-    pp_piece<PH>(c, gr, glds, 1);
-  }
-  pp_stamp(c, st0 < 0 ? -1 : st0 + 2);
+  pp_piece<PH>(c, gr, glds, 0);
+  pp_piece<PH>(c, gr, glds, 1);
   pp_vmwait<pp_dma_wait<EPI, QE, FIRST, LAST, PH>()>();
-  pp_stamp(c, st0 < 0 ? -1 : st0 + 3);
   pp_barrier();
-  pp_stamp(c, st0 < 0 ? -1 : st0 + 4);
   // ---- MFMA segment: quadrant (rows half jh, column pair p): (0,0) (0,1) (1,1) (1,0)
   {
     constexpr int jh = pp_qjh(PH);
     constexpr int p = pp_qp(PH);
-    if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -758,18 +685,9 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
           f32x4& a = acc[2 * p + ii][4 * jh + jj];
           if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
           else a = mfma16(fb[k][ii], fa[k][jj], a);
-          if constexpr (kPPDmaMfma) {
-            const int idx = 8 * k + 2 * jj + ii;
-            if (idx == 3 || idx == 11) {
-              __builtin_amdgcn_sched_barrier(0);
-              pp_piece<PH>(c, gr, glds, idx == 3 ? 0 : 1);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
         }
-    if constexpr (!kPPStaticPrio) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   }
-  pp_stamp(c, st0 < 0 ? -1 : st0 + 5);
   pp_barrier();
 }
 
@@ -781,14 +699,10 @@ PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   const int nsl = (s + 1) & 1;
   const uint16_t* nslotp = smem + nsl * PSLOT;
   const PPSrd srd = pp_srds<EPI>(c, ntm, ntn, nkt, nvalid);  // the DMA carries the next K-tile
-  // kPPStamps: the third tile's K-tile 0 (its first phases carry the second tile's epilogue) and
-  // its K-tile S / 2
-  const int S = c.g->K / PBK;
-  const int sk = !kPPStamps ? -1 : s == 2 * S ? 0 : s == 2 * S + S / 2 ? 1 : -1;
-  pp_phase<0, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<1, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<2, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
-  pp_phase<3, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, sk, pe, ce, dsum);
+  pp_phase<0, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, pe, ce, dsum);
+  pp_phase<1, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, pe, ce, dsum);
+  pp_phase<2, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, pe, ce, dsum);
+  pp_phase<3, FIRST, LAST, EPI, QE>(c, acc, fa, fb, slotp, nslotp, srd, nsl, pe, ce, dsum);
 }
 
 template <int EPI, bool QE>
@@ -796,14 +710,11 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   // all LDS in ONE array (a second __shared__ object can make hipcc drain the DMA before reads):
   // two 64 KiB K-tile slots, then 8 x 4 KiB per-wave bias / aux areas (quadrant epilogues)
   constexpr int kAuxElems = QE ? 8 * 2048 : 0;
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + kAuxElems + (kPPStamps ? 8 * kPPStampN * 4 : 0)];
+  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * PSLOT + kAuxElems];
   const int tiles_m = (g.M + PT - 1) / PT, tiles_n = (g.N + kNT<EPI> - 1) / kNT<EPI>, ntiles = tiles_m * tiles_n;
   const int G = gridDim.x;
   const int lid = xcd_remap(blockIdx.x, G);
   if (lid >= ntiles) return;
-  if (g.stagger > 0 && (lid & 1)) {
-    for (int i = 0; i < g.stagger; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   PPCtx c;
   c.g = &g;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -813,8 +724,6 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   c.lane = lane;
   c.lds = (unsigned)(uintptr_t)smem;
   c.aux = smem + 2 * PSLOT + 2048 * c.w;
-  c.stamp = kPPStamps && blockIdx.x == 0;
-  c.stamp_at = reinterpret_cast<uint64_t*>(smem + 2 * PSLOT + kAuxElems) + kPPStampN * c.w;
   c.vaux = (uint32_t)(((int64_t)(lane >> 2) * g.ldaux + 8 * (lane & 3)) * 2);
   {
     // per-lane source offsets of this wave's pieces: lane l of piece blk fills image row
@@ -850,38 +759,13 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     }
   }
   const int S = g.K / PBK;
-  if constexpr ((PLLM_PP_EXP & 32) != 0) {
-    if (lid & 1)
-      for (int i = 0; i < S / 3; ++i) __builtin_amdgcn_s_sleep(63);  // ~4k cycles each
-  }
-  // Segments: (tile, K-tile range, mode).  Normally one full-K segment per tile.  With the
-  // desynchronising split (end-of-tile epilogues; odd workgroups with >= 2 tiles; a workspace), the
-  // workgroup first runs the SECOND half of the K range of its last tile and parks that partial
-  // fp32 tile in its own workspace slot, then its other tiles, then the first half of the last tile,
-  // adding the parked partial before the epilogue: same work per workgroup, but its tile
-  // boundaries -- and the epilogue store bursts -- fall half a tile after the even workgroups'
-  // (measured: every CU storing its 128 KiB at once parked both wave groups ~4.5k cycles a tile)
+  // one full-K segment per tile: tiles lid, lid + G, ...
   const int R = (ntiles - lid + G - 1) / G;
-  const bool split = kPPSplit<EPI, QE> && g.splitws != nullptr && (lid & 1) && R >= 2 && S >= 4;
-  const int nseg = split ? R + 1 : R;
-  auto segment = [&](int i, int& t, int& kb, int& ke, int& mode) {  // mode 0 full, 1 park, 2 finish
-    if (!split) {
-      t = lid + i * G, kb = 0, ke = S, mode = 0;
-    } else if (i == 0) {
-      t = lid + (R - 1) * G, kb = S / 2, ke = S, mode = 1;
-    } else if (i == R) {
-      t = lid + (R - 1) * G, kb = 0, ke = S / 2, mode = 2;
-    } else {
-      t = lid + (i - 1) * G, kb = 0, ke = S, mode = 0;
-    }
-  };
   int tm, tn;
   // prologue: the first segment's first K-tile, all four piece groups, fully landed
   {
-    int t0, kb0, ke0, mode0;
-    segment(0, t0, kb0, ke0, mode0);
-    pp_tile(t0, tiles_m, tiles_n, g.group_m, tm, tn);
-    const PPSrd srd = pp_srds<EPI>(c, tm, tn, kb0, true);
+    pp_tile(lid, tiles_m, tiles_n, g.group_m, tm, tn);
+    const PPSrd srd = pp_srds<EPI>(c, tm, tn, 0, true);
     pp_issue<0, EPI>(c, srd, 0);
     pp_issue<1, EPI>(c, srd, 0);
     pp_issue<2, EPI>(c, srd, 0);
@@ -890,9 +774,6 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   pp_vmwait<0>();
   pp_barrier();
   if (c.wr == 1) pp_barrier();  // the stagger: rows 128-255 run one barrier behind rows 0-127
-  if constexpr (kPPStaticPrio) {
-    if (c.wr == 1) __builtin_amdgcn_s_setprio(1);  // the younger half keeps priority (no flips)
-  }
 
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
@@ -900,46 +781,27 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
   float dsum[4] = {0.f, 0.f, 0.f, 0.f};
   int s = 0;
   PPEpi pe{tm, tn, false};  // the previous tile (none yet)
-  for (int i = 0; i < nseg; ++i) {
-    int t, kb, ke, mode;
-    segment(i, t, kb, ke, mode);
-    pp_tile(t, tiles_m, tiles_n, g.group_m, tm, tn);
+  for (int i = 0; i < R; ++i) {
+    pp_tile(lid + i * G, tiles_m, tiles_n, g.group_m, tm, tn);
     const PPEpi ce{tm, tn, true};
-    const bool more = i + 1 < nseg;
-    int tm2 = tm, tn2 = tn, kb2 = 0;
-    if (more) {
-      int t2, ke2, mode2;
-      segment(i + 1, t2, kb2, ke2, mode2);
-      pp_tile(t2, tiles_m, tiles_n, g.group_m, tm2, tn2);
-    }
+    const bool more = i + 1 < R;
+    int tm2 = tm, tn2 = tn;
+    if (more) pp_tile(lid + (i + 1) * G, tiles_m, tiles_n, g.group_m, tm2, tn2);
     // K-tile kt's DMA carries K-tile kt + 1, or the next segment's first K-tile after the last one.
     // The first K-tile is peeled: its MFMAs start the accumulators from zero (with quadrant
     // epilogues: each quadrant right after that quadrant's epilogue of the previous tile).
-    // (>= 2 K-tiles per segment: gemm_tn sends K < 128 to the round-3 kernel; split needs S >= 4)
-    if constexpr (kPPSplit<EPI, QE>) {
-      if (mode == 2) {
-        pp_unpark(acc, c, lid);
-        pp_ktile<false, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
-      } else {
-        pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
-      }
-    } else {
-      pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kb + 1, true, pe, ce, dsum);
-    }
+    // (>= 2 K-tiles per tile: gemm_tn sends K < 128 to the round-3 kernel)
+    pp_ktile<true, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, 1, true, pe, ce, dsum);
     ++s;
-    for (int kt = kb + 1; kt + 1 < ke; ++kt, ++s)
+    for (int kt = 1; kt + 1 < S; ++kt, ++s)
       pp_ktile<false, false, EPI, QE>(c, acc, fa, fb, smem, s, tm, tn, kt + 1, true, pe, ce, dsum);
-    pp_ktile<false, true, EPI, QE>(c, acc, fa, fb, smem, s, tm2, tn2, kb2, more, pe, ce, dsum);
+    pp_ktile<false, true, EPI, QE>(c, acc, fa, fb, smem, s, tm2, tn2, 0, more, pe, ce, dsum);
     ++s;
     if constexpr (!QE) {
       // the end-of-tile epilogue, in this wave's next LOAD slot
       __builtin_amdgcn_sched_barrier(0);
-      if (mode == 1) {
-        pp_park(acc, c, lid);
-      } else {
-        if constexpr (EPI == 7) pp_epilogue_swiglu(acc, g, tm, tn, c.wr, c.wc, lane);
-        else pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
-      }
+      if constexpr (EPI == 7) pp_epilogue_swiglu(acc, g, tm, tn, c.wr, c.wc, lane);
+      else pp_epilogue<EPI>(acc, g, tm, tn, c.wr, c.wc, lane);
       __builtin_amdgcn_sched_barrier(0);
     }
     pe = ce;
@@ -964,31 +826,11 @@ __global__ __launch_bounds__(PNT) void gemm_pp_kernel(pllm::GemmArgs g) {
     pp_epi_quad<EPI, 3>(acc, c, pe, ax, dsum);
   }
   if (c.wr == 0) pp_barrier();  // balance the stagger
-  if constexpr (kPPStamps) {
-    if (c.stamp) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc((void*)g.C, (short)0, 1 << 30, 0x00020000);
-      if (lane < kPPStampN) {
-        const uint64_t v = c.stamp_at[lane];
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, v), crs,
-                                              (uint32_t)((c.w * kPPStampN + lane) * 8), 0, 0);
-      }
-    }
-  }
 }
 
 }  // namespace
 
 namespace pllm {
-
-int64_t gemm_pp_split_ws_floats(int M, int N, int K, int epi, int ctas) {
-  const int nt = epi == 7 ? 128 : PT;
-  const int ntiles = ((M + PT - 1) / PT) * ((N + nt - 1) / nt);
-  const int grid = ntiles < ctas ? ntiles : ctas;
-  // end-of-tile epilogues only, >= 4 K-tiles, and odd workgroups with >= 2 tiles must exist
-  if (gemm_pp_quad_epilogue(K, epi) || epi == 3 || epi == 4 || K / PBK < 4 || ntiles < 2 * grid || grid < 2) return 0;
-  return (int64_t)grid * PT * PT;
-}
 
 // EPI 3 / 4 column-sum partial rows: 4 per tile row with quadrant epilogues, 2 otherwise
 int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 4 : 2) * ((M + PT - 1) / PT); }
@@ -998,12 +840,7 @@ int gemm_pp_colsum_groups(int M, int K) { return (gemm_pp_quad_epilogue(K, 3) ? 
 // shape 32768 x 11008 x 2048, gpurun_out/r4pp7_bench.jsonl)
 bool gemm_pp_quad_epilogue(int K, int epi) { return K >= 2048 && epi != 5 && epi != 1; }
 
-static int g_pp_stagger = 0;
-void gemm_pp_set_stagger(int n) { g_pp_stagger = n > 0 ? n : 0; }
-
-void gemm_tn_pp(const GemmArgs& a0, int epi, int ctas, hipStream_t st) {
-  GemmArgs a = a0;
-  a.stagger = g_pp_stagger;
+void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
   const int nt = epi == 7 ? 128 : PT;
   const int ntiles = ((a.M + PT - 1) / PT) * ((a.N + nt - 1) / nt);
   if (ntiles == 0) return;

@@ -49,34 +49,10 @@
 #include "common.h"
 #include "kernels.h"
 
-#ifndef PLLM_WGRAD_STAMPS
-#define PLLM_WGRAD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the stage loop
-#endif
-#if PLLM_WGRAD_STAMPS
-__device__ unsigned long long g_wg_stamps[8];
-#endif
-#ifndef PLLM_WGRAD_SPREAD
-#define PLLM_WGRAD_SPREAD 0  // 1: spread the next stage's DMA over the k-steps (measured 0-6 % slower)
-#endif
-constexpr bool kWgradSpread = PLLM_WGRAD_SPREAD != 0;
-#ifndef PLLM_WGRAD_LOADERS
-#define PLLM_WGRAD_LOADERS 0  // 1: loader / consumer waves (wgrad_ld_kernel): measured 12-14 % slower
-#endif
-constexpr bool kWgradLoaders = PLLM_WGRAD_LOADERS != 0;
-#ifndef PLLM_WGRAD_BUFLDS
-#define PLLM_WGRAD_BUFLDS 1  // buffer_load ... lds (SRD + 32-bit offsets) instead of global_load_lds
-#endif
-constexpr bool kWgradBufLds = PLLM_WGRAD_BUFLDS != 0;
-#ifndef PLLM_WGRAD_XCD_ALIGN
-#define PLLM_WGRAD_XCD_ALIGN 0
-#ifndef PLLM_WGRAD_HY_DEFAULT
-#define PLLM_WGRAD_HY_DEFAULT 1
-#endif  // 1: wgrad_plan prefers slice counts giving every XCD whole slices (measured slower in the step)
-#endif
-#ifndef PLLM_WGRAD_STAGGER
-#define PLLM_WGRAD_STAGGER 0  // n > 0: waves 4-7 (the SIMD partners of 0-3) issue the next stage's DMA before k-step n
-#endif
-constexpr int kWgradStagger = PLLM_WGRAD_STAGGER;
+// Measured and removed (records kept in profiles/): spreading the next stage's DMA over the k-steps
+// (0-6 % slower), loader / consumer waves (12-14 % slower), global_load_lds instead of buffer_load ... lds,
+// a wave-4-7 DMA stagger, XCD-aligned slice counts (slower in the step, r3s3_wgrad_slices.jsonl) and the
+// symmetric (every wave loading) DMA plan (1-8 % slower than the asymmetric one, r3_wgrad_asym_ab.md).
 
 namespace {
 
@@ -94,16 +70,6 @@ PLLM_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
   s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
-// global -> LDS DMA of 16 B per lane into [m0 + 16*lane] (m0 = wave-uniform LDS byte address).
-// Written as inline asm on purpose: for the builtin, hipcc's waitcnt pass cannot tell the
-// buffer being filled from the one being read and drains the prefetch (vmcnt(0)) before
-// the first ds_read of every stage.  The caller retires these loads with an explicit
-// "s_waitcnt vmcnt(0)" ahead of the barrier that publishes the stage.
-PLLM_DEV void glds16(const void* src, unsigned lds_byte) {
-  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src),
-               "s"(__builtin_amdgcn_readfirstlane(lds_byte))
-               : "memory", "m0");
-}
 // buffer-descriptor form (srd_of / blds16): common.h
 PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
 
@@ -117,15 +83,15 @@ constexpr int NT = 512;             // 8 waves
 constexpr int HALF = BKM * 128;     // elements of one [64][128] image
 constexpr int STAGE = 4 * HALF;     // A halves 0,1 then B halves 2,3 (64 KiB)
 
-template <int MF, bool OF32, bool ASYM>
+template <int MF, bool OF32>
 __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ A, int64_t lda,
                                                    const uint16_t* __restrict__ B, int64_t ldb, int M, int P, int Q,
                                                    int S, int slice, float* __restrict__ part, void* __restrict__ out,
                                                    int accumulate, float* __restrict__ bpart) {
   constexpr int QUADS = BKM / 4;  // row-quads per image
-  // 1-KiB pieces per wave and stage; ASYM: waves 0-3 issue all 64 (16 each) and waves 4-7 none,
-  // so each SIMD's partner wave computes while the loader wave is stuck issuing its burst
-  constexpr int PPW = ASYM ? BKM / 4 : BKM / 8;
+  // 1-KiB pieces per wave and stage: waves 0-3 issue all 64 (16 each) and waves 4-7 none, so each
+  // SIMD's partner wave computes while the loader wave is stuck issuing its burst
+  constexpr int PPW = BKM / 4;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
   const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
   const int ntiles = tiles_p * tiles_q;
@@ -142,18 +108,12 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   // Lane l of a piece fills image row 4*quad + l/16, chunk position l%16, which holds
   // logical chunk (l%16) ^ swz(row).  Columns past P/Q are clamped to a valid chunk:
   // they only feed output rows/columns that are never stored.
-  const uint16_t* src[PPW];
   int dst[PPW];
 #pragma unroll
   for (int k = 0; k < PPW; ++k) {
     const int pc = w * PPW + k, opnd = pc / (2 * QUADS), half = (pc / QUADS) & 1, quad = pc % QUADS;
-    const int row = 4 * quad + (lane >> 4);
-    const int col = half * 128 + (((lane & 15) ^ swz(row)) << 3);
-    if (opnd == 0) src[k] = A + (int64_t)(m_begin + row) * lda + min(p0 + col, P - 8);
-    else src[k] = B + (int64_t)(m_begin + row) * ldb + min(q0 + col, Q - 8);
     dst[k] = (opnd * 2 + half) * HALF + quad * 512;
   }
-  const int64_t astep = (int64_t)BKM * lda, bstep = (int64_t)BKM * ldb;
   const unsigned lds_base = (unsigned)(uintptr_t)smem;
   // buffer form: per-lane byte offsets within a stage (< 64 rows x ld x 2 B), loop-invariant
   uint32_t voff[PPW];
@@ -166,31 +126,19 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
                         : (uint32_t)((row * ldb + min(q0 + col, Q - 8)) * 2);
   }
   // pieces [k0, k1) of stage st's DMA plan
-  const bool loader = !ASYM || w < 4;
-  auto issue_part = [&](int st, int k0, int k1) {
+  const bool loader = w < 4;
+  auto issue = [&](int st) {
     if (!loader) return;
     const int slot = st & 1;
-    if constexpr (kWgradBufLds) {
-      const int64_t m0 = (int64_t)m_begin + (int64_t)st * BKM;
-      const i32x4v sa = srd_of(A + m0 * lda, (uint32_t)(BKM * lda * 2));
-      const i32x4v sb = srd_of(B + m0 * ldb, (uint32_t)(BKM * ldb * 2));
-#pragma unroll
-      for (int k = 0; k < PPW; ++k) {
-        if (k < k0 || k >= k1) continue;
-        const int opnd = (w * PPW + k) / (2 * QUADS);
-        blds16(opnd == 0 ? sa : sb, voff[k], lds_base + 2u * (unsigned)(slot * STAGE + dst[k]));
-      }
-      return;
-    }
+    const int64_t m0 = (int64_t)m_begin + (int64_t)st * BKM;
+    const i32x4v sa = srd_of(A + m0 * lda, (uint32_t)(BKM * lda * 2));
+    const i32x4v sb = srd_of(B + m0 * ldb, (uint32_t)(BKM * ldb * 2));
 #pragma unroll
     for (int k = 0; k < PPW; ++k) {
-      if (k < k0 || k >= k1) continue;
       const int opnd = (w * PPW + k) / (2 * QUADS);
-      const uint16_t* g = src[k] + st * (opnd == 0 ? astep : bstep);
-      glds16(g, lds_base + 2u * (unsigned)(slot * STAGE + dst[k]));
+      blds16(opnd == 0 ? sa : sb, voff[k], lds_base + 2u * (unsigned)(slot * STAGE + dst[k]));
     }
   };
-  auto issue = [&](int st) { issue_part(st, 0, PPW); };
 
   // MF = 32: 4x2 v_mfma_f32_32x32x16_bf16 accumulators per wave (128x64 sub-tile);
   // MF = 16: 8x4 v_mfma_f32_16x16x32_bf16 accumulators -- same LDS traffic per FLOP.
@@ -213,36 +161,14 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   const bool do_b = MF == 16 && bpart != nullptr && (t % tiles_q) == 0;
   f32x4 bacc[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
   const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
-#if PLLM_WGRAD_STAMPS
-  uint64_t st_acc[4] = {0, 0, 0, 0};
-  uint64_t ts_prev = __builtin_amdgcn_s_memtime();
-  auto stamp = [&](int i) {
-    const uint64_t now = __builtin_amdgcn_s_memtime();
-    st_acc[i] += now - ts_prev;
-    ts_prev = now;
-  };
-#define PLLM_WSTAMP(i) stamp(i)
-#else
-#define PLLM_WSTAMP(i)
-#endif
   if (nstage > 0) issue(0);
   for (int st = 0; st < nstage; ++st) {
     const int slot = st & 1;
-    PLLM_WSTAMP(3);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PLLM_WSTAMP(0);
     __syncthreads();  // stage st landed for every wave; nobody still reads the other slot
-    PLLM_WSTAMP(1);
-    // the next stage's DMA: eight 1-KiB pieces per wave, issued as one burst after the barrier.
-    // Issuing them costs a wave ~1.1k cycles per stage (~140 per piece); spreading them over the
-    // k-steps (kWgradSpread) moves that cost into the compute segment and measured 0-6 % slower
-    // (profiles/r3_wgrad_stamps.md)
-    const bool pre = st + 1 < nstage;
-    // stagger: the SIMD partners (waves w and w + 4) issue their bursts at different times, so one of
-    // them keeps the matrix pipe busy while the other is stuck issuing pieces
-    const bool late = kWgradStagger > 0 && w >= 4;
-    if (!kWgradSpread && pre && !late) issue(st + 1);
-    PLLM_WSTAMP(2);
+    // the next stage's DMA: sixteen 1-KiB pieces per loader wave, issued as one burst after the
+    // barrier (profiles/r3_wgrad_stamps.md)
+    if (st + 1 < nstage) issue(st + 1);
     const uint16_t* Ai = smem + slot * STAGE + wp * HALF;
     const uint16_t* Bi = smem + slot * STAGE + (2 + (wq >> 1)) * HALF;
     const int bcol = (wq & 1) * 64;
@@ -261,8 +187,6 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           const int col = bcol + 32 * j + 16 * g1 + 4 * tp;
           bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
         }
-        if (kWgradSpread && pre) issue_part(st + 1, k16 * (PPW / (BKM / 16)), (k16 + 1) * (PPW / (BKM / 16)));
-        if (late && pre && k16 == kWgradStagger) issue(st + 1);
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -285,8 +209,6 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
           const int col = 16 * i + 4 * tp;
           af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
         }
-        if (kWgradSpread && pre) issue_part(st + 1, k32 * (PPW / (BKM / 32)), (k32 + 1) * (PPW / (BKM / 32)));
-        if (late && pre && k32 == (kWgradStagger + 1) / 2) issue(st + 1);
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -301,15 +223,6 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
       }
     }
   }
-#if PLLM_WGRAD_STAMPS
-  if (lane == 0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) atomicAdd(&g_wg_stamps[i], (unsigned long long)st_acc[i]);
-    atomicAdd(&g_wg_stamps[4], (unsigned long long)nstage);
-    atomicAdd(&g_wg_stamps[5], 1ull);
-  }
-#endif
-#undef PLLM_WSTAMP
   // accumulator element e of fragment (i, j) -> output (row p, column q) of the tile
   auto prow = [&](int i, int e) {
     return MF == 32 ? p0 + wp * 128 + 32 * i + acc_row(e, hh) : p0 + wp * 128 + 16 * i + 4 * (lane >> 4) + e;
@@ -364,156 +277,6 @@ __global__ __launch_bounds__(NT) void wgrad_kernel(const uint16_t* __restrict__ 
   }
 }
 
-// Loader / consumer variant: 12 waves, three per SIMD -- the eight compute waves of wgrad_kernel
-// (same tile, same LDS images, same MFMA loop) never issue a DMA; four loader waves issue every
-// piece of the next stage right after each barrier and then wait for it.  Per-wave stamps put
-// the compute waves' own DMA issue at a third of each stage (profiles/r3_wgrad_stamps.md): a wave
-// stuck issuing pieces issues no MFMAs.  Three waves per SIMD cap the registers at 168.
-constexpr int NTL = 768;
-
-template <int MF, bool OF32>
-__global__ __launch_bounds__(NTL) void wgrad_ld_kernel(const uint16_t* __restrict__ A, int64_t lda,
-                                                       const uint16_t* __restrict__ B, int64_t ldb, int M, int P,
-                                                       int Q, int S, int slice, float* __restrict__ part,
-                                                       void* __restrict__ out, int accumulate) {
-  constexpr int QUADS = BKM / 4;          // row-quads per image
-  constexpr int PPL = 4 * QUADS / 4;      // 1-KiB pieces per loader wave and stage (64 / 4)
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * STAGE];
-  const int tiles_q = (Q + BT - 1) / BT, tiles_p = (P + BT - 1) / BT;
-  const int ntiles = tiles_p * tiles_q;
-  const int lid = xcd_remap(blockIdx.x, gridDim.x);
-  const int s = lid / ntiles, t = lid % ntiles;
-  const int p0 = (t / tiles_q) * BT, q0 = (t % tiles_q) * BT;
-  const int m_begin = s * slice;
-  const int nstage = (min(M, m_begin + slice) - m_begin) / BKM;
-  const int tid = threadIdx.x, w = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
-  const unsigned lds_base = (unsigned)(uintptr_t)smem;
-  if (w >= 8) {
-    // ---- loader wave ----
-    const int lw = w - 8;
-    auto issue = [&](int st) {
-      const int slot = st & 1;
-#pragma unroll
-      for (int k = 0; k < PPL; ++k) {
-        const int pc = lw * PPL + k, opnd = pc / (2 * QUADS), half = (pc / QUADS) & 1, quad = pc % QUADS;
-        const int row = 4 * quad + (lane >> 4);
-        const int col = half * 128 + (((lane & 15) ^ swz(row)) << 3);
-        const int64_t m = (int64_t)m_begin + st * BKM + row;
-        const uint16_t* g = opnd == 0 ? A + m * lda + min(p0 + col, P - 8) : B + m * ldb + min(q0 + col, Q - 8);
-        glds16(g, lds_base + 2u * (unsigned)(slot * STAGE + (opnd * 2 + half) * HALF + quad * 512));
-      }
-    };
-    if (nstage > 0) issue(0);
-    for (int st = 0; st < nstage; ++st) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // stage st landed; the compute waves are done with the other slot
-      if (st + 1 < nstage) issue(st + 1);
-    }
-    return;
-  }
-  // ---- compute wave (as wgrad_kernel) ----
-  const int r = lane & 31, hh = lane >> 5;
-  const int wp = w >> 2, wq = w & 3;
-  const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-  constexpr int NI = MF == 32 ? 4 : 8, NJ = MF == 32 ? 2 : 4;
-  using Acc = typename std::conditional<MF == 32, f32x16, f32x4>::type;
-  constexpr int NE = MF == 32 ? 16 : 4;
-  Acc acc[NI][NJ];
-#pragma unroll
-  for (int i = 0; i < NI; ++i)
-#pragma unroll
-    for (int j = 0; j < NJ; ++j)
-#pragma unroll
-      for (int e = 0; e < NE; ++e) acc[i][j][e] = 0.f;
-  for (int st = 0; st < nstage; ++st) {
-    const int slot = st & 1;
-    __syncthreads();
-    const uint16_t* Ai = smem + slot * STAGE + wp * HALF;
-    const uint16_t* Bi = smem + slot * STAGE + (2 + (wq >> 1)) * HALF;
-    const int bcol = (wq & 1) * 64;
-    if constexpr (MF == 32) {
-#pragma unroll
-      for (int k16 = 0; k16 < BKM / 16; ++k16) {
-        const int row = k16 * 16 + 8 * hh + tq;
-        bf16x8 af[4], bfr[2];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int col = 32 * i + 16 * g1 + 4 * tp;
-          af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int col = bcol + 32 * j + 16 * g1 + 4 * tp;
-          bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bfr[j], acc[i][j]);
-      }
-    } else {
-      const int gq = lane >> 4;
-#pragma unroll
-      for (int k32 = 0; k32 < BKM / 32; ++k32) {
-        const int row = k32 * 32 + 8 * gq + tq;
-        bf16x8 af[8], bfr[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = bcol + 16 * j + 4 * tp;
-          bfr[j] = cat_tr(ds_tr(Bi + img_off(row, col)), ds_tr(Bi + img_off(row + 4, col)));
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int col = 16 * i + 4 * tp;
-          af[i] = cat_tr(ds_tr(Ai + img_off(row, col)), ds_tr(Ai + img_off(row + 4, col)));
-        }
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfr[j], acc[i][j]);
-      }
-    }
-  }
-  auto prow = [&](int i, int e) {
-    return MF == 32 ? p0 + wp * 128 + 32 * i + acc_row(e, hh) : p0 + wp * 128 + 16 * i + 4 * (lane >> 4) + e;
-  };
-  auto qcol = [&](int j) { return MF == 32 ? q0 + wq * 64 + 32 * j + r : q0 + wq * 64 + 16 * j + (lane & 15); };
-  if (S == 1) {
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int q = qcol(j), qc = min(q, Q - 1);
-        float old[NE];
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int p = min(prow(i, e), P - 1);
-          old[e] = accumulate ? ldg1<OF32>(out, (int64_t)p * Q + qc) : 0.f;
-        }
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-          const int p = prow(i, e);
-          if (p < P && q < Q) stg1<OF32>(out, (int64_t)p * Q + q, acc[i][j][e] + old[e]);
-        }
-      }
-    }
-    return;
-  }
-  float* dstp = part + (int64_t)s * P * Q;
-#pragma unroll
-  for (int i = 0; i < NI; ++i) {
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int q = qcol(j);
-#pragma unroll
-      for (int e = 0; e < NE; ++e) {
-        const int p = prow(i, e);
-        if (p < P && q < Q) dstp[(int64_t)p * Q + q] = acc[i][j][e];
-      }
-    }
-  }
-}
-
 // dW[p, q] (+)= sum_s slab[s][p][q]   (8 columns per thread, fixed slice order)
 template <bool OF32>
 __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restrict__ part, int S, int64_t PQ,
@@ -546,18 +309,16 @@ namespace pllm {
 
 // Variant selection (wgrad_set_mfma): 0 = default -- the ping-pong kernel of wgrad_pp.hip where it
 // applies (fp32 gradient target), else this file's kernel per shape; 100 = this file's kernel per
-// shape; 16 / 32 = that MFMA shape with every wave loading, 116 / 132 = the asymmetric-DMA kernel.
+// shape; 116 / 132 (or 16 / 32) = this file's kernel with that MFMA shape.
 // Same-box A/B of this file's variants (profiles/r3_wgrad_asym_ab.md): the asymmetric DMA is +1-8 %
 // over the symmetric kernel; 16x16x32 wins everywhere except the LM-head shapes (P = vocabulary),
 // where 32x32x16 does (+0.5-4 %)
 static int g_wgrad_mfma = 0;
-static int g_wgrad_asym = 1;
 static bool g_wgrad_pp = true;
 void wgrad_set_mfma(int mf) {
   g_wgrad_pp = mf == 0;
   const int v = mf % 100;
   g_wgrad_mfma = v == 0 ? 0 : (v == 16 ? 16 : 32);
-  g_wgrad_asym = mf == 0 || mf >= 100;
 }
 
 // A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices
@@ -586,26 +347,6 @@ void wgrad_plan(int M, int P, int Q, int* S, int* slice) {
       best = s;
     }
   }
-  // XCD alignment: xcd_remap deals each XCD a contiguous 1/8 of the work items, and a slice's items
-  // share its dY / X panels through that XCD's L2.  With a one-round grid and S % 8 == 0 every XCD
-  // holds whole slices; otherwise slices straddle XCDs and their panels are fetched twice.  Measured
-  // (bench/wgrad_slices.py, profiles/r3s3_wgrad_slices.jsonl): GPT-2 QKV (27 tiles) S = 8 226 us vs
-  // the model's S = 9 260 us in isolation -- but the whole GPT-2 step ran 0.2 ms SLOWER with it
-  // (57.82-57.86 vs 58.02-58.08 ms, same box A/B/A/B), so it is off (PLLM_WGRAD_XCD_ALIGN=1 to build it).
-  {
-    int al = 0;
-    double al_t = 1e30;
-    for (int s = 8; s <= 64 && kst / s >= 8; s += 8) {
-      if (ntiles * s > 256) break;
-      const int st_per = (kst + s - 1) / s;
-      const double t = (double)st_per * 2.0e-6 + (double)P * Q * 4.0 * (2 * s + 1) / 4.0e12;
-      if (t < al_t) {
-        al_t = t;
-        al = s;
-      }
-    }
-    if (PLLM_WGRAD_XCD_ALIGN && al > 0 && al_t <= best_t * 1.15) best = al;
-  }
   if (g_wgrad_force_s > 0) best = std::min(g_wgrad_force_s, std::max(1, kst));
   int st_per = (kst + best - 1) / best;
   *slice = st_per * BKM;
@@ -623,7 +364,7 @@ int wgrad_bias_slices(int M, int P, int Q) {
 // 2048 5,190 vs 5,721 us, GPT-2 step +0.3 %, llama +0.2-0.3 % (profiles/r4_wgrad_hybrid.md).  On the
 // persistent grid only (whole rounds of one tile per CU); with a grid per tile the hardware deals the tiles
 // anyway.  (Full stream-K -- equal K-tile runs per workgroup -- lost 13-47 %: r4_wgrad_stream_k_negative.md)
-static int g_wgrad_hy = PLLM_WGRAD_HY_DEFAULT;
+static int g_wgrad_hy = 1;
 void wgrad_set_hy(int on) { g_wgrad_hy = on; }
 
 static bool wgrad_use_hy(int M, int P, int Q, bool out_f32, bool bias) {
@@ -666,21 +407,11 @@ bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   }
   const int mfma = g_wgrad_mfma != 0 ? g_wgrad_mfma : (P >= 16384 ? 32 : 16);
   // the bias gradient rides along only on the 16x16x32 kernel (see wgrad_kernel)
-  const bool fuse_b = bpart != nullptr && bout != nullptr && mfma == 16 && !kWgradLoaders;
+  const bool fuse_b = bpart != nullptr && bout != nullptr && mfma == 16;
   float* const bp = fuse_b ? bpart : nullptr;
-#define PLLM_WGRAD_LAUNCH(MFV, OF)                                                                              \
-  do {                                                                                                         \
-    if (kWgradLoaders)                                                                                         \
-      hipLaunchKernelGGL((wgrad_ld_kernel<MFV, OF>), dim3(ntiles * S), dim3(NTL), 0, st, (const uint16_t*)dy, \
-                         lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate);         \
-    else                                                                                                       \
-      if (g_wgrad_asym)                                                                                        \
-        hipLaunchKernelGGL((wgrad_kernel<MFV, OF, true>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
-                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp);     \
-      else                                                                                                     \
-        hipLaunchKernelGGL((wgrad_kernel<MFV, OF, false>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, \
-                           lda, (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp);     \
-  } while (0)
+#define PLLM_WGRAD_LAUNCH(MFV, OF)                                                                           \
+  hipLaunchKernelGGL((wgrad_kernel<MFV, OF>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda, \
+                     (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp)
   if (mfma == 16) {
     if (out_f32) PLLM_WGRAD_LAUNCH(16, true);
     else PLLM_WGRAD_LAUNCH(16, false);
@@ -689,18 +420,6 @@ bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
     else PLLM_WGRAD_LAUNCH(32, false);
   }
 #undef PLLM_WGRAD_LAUNCH
-#if PLLM_WGRAD_STAMPS
-  if (std::getenv("PLLM_WGRAD_STAMPS")) {
-    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipStreamSynchronize(st);
-    (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_wg_stamps), sizeof(h));
-    const double n = (double)h[4] > 0 ? (double)h[4] : 1.0;  // wave-stages (x8 waves per WG counted per wave)
-    fprintf(stderr, "[wgrad stamps] M %d P %d Q %d S %d | per wave-stage: vmcnt wait %.0f barrier %.0f dma issue %.0f compute %.0f\n",
-            M, P, Q, S, h[0] / n, h[1] / n, h[2] / n, h[3] / n);
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_wg_stamps), z, sizeof(z));
-  }
-#endif
   if (fuse_b) {  // bias gradient: the [S][P] partial rows summed in slice order into bout
     const dim3 bg((unsigned)((P / 8 + 255) / 256));
     if (bout_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);

@@ -124,22 +124,16 @@ struct GemmArgs {
   int group_m;  // set by gemm_tn
   float* delta;  // epilogue 6: [M / T, N / 64, T] row sums of C * aux per 64-column head
   int T;         // epilogue 6: rows per sequence
-  float* splitws;  // gemm_pp: per-workgroup 256x256 fp32 parking slots of the desynchronising split
-                   // (gemm_pp_split_ws_floats; nullptr = no split)
-  int stagger;     // gemm_pp: odd workgroups start this many x 8128 cycles late (gemm_pp_set_stagger)
 };
-void gemm_pp_set_stagger(int n);  // A/B: de-phase the workgroups' end-of-tile store bursts
 void gemm_tn(const GemmArgs& a, int epi, hipStream_t st);
 // phased: 0 single-phase, 2 asym DMA, 4 ping-pong kernel (gemm_pp.hip); reserve_cus >= 0: CUs left
 // free by the persistent grids (collectives in flight), -1 keeps the current setting
-void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, int split = -1, int persistent = -1);
+void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, int persistent = -1);
 // workgroup cap of the persistent GEMM grids (CUs minus reserve_cus; 2^30 when non-persistent)
 int gemm_grid_cap();
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
 int gemm_pp_colsum_groups(int M, int K);
 bool gemm_pp_quad_epilogue(int K, int epi);
-int64_t gemm_pp_split_ws_floats(int M, int N, int K, int epi, int ctas);  // 0: the call does not split
-int64_t gemm_split_ws_floats(int M, int N, int K, int epi, int T);  // gemm.hip: for the current config
 int gemm_colsum_groups(int M, int K);  // column-sum partial rows (epi 3 / 4) of the kernel serving K
 bool gemm_uses_pp(int K, int epi, int T);
 // gemm_wgrad.hip: dW[P,Q] (+)= dY[M,P]^T X[M,Q]; part: fp32 [S, P, Q] workspace (wgrad_plan)
@@ -209,6 +203,11 @@ void gemv(const GemvArgs& a, hipStream_t st);
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
+bool attn_bwd_uses_ks(int D);    // the key-stationary backward serves head dim D (q / k must be pre-rotated)
+// attn_bwd_ks.hip: keys per workgroup; one pass of the key-stationary main kernel (AttnBwdArgs as attn_bwd)
+int attn_bwd_ks_key_block();
+void attn_bwd_set_ks(int mask);  // A/B: bit 0 = D 64, bit 1 = D 128 on the key-stationary kernel
+void attn_bwd_ks_launch(const AttnBwdArgs& a, hipStream_t st);
 // attn_decode.hip: split-KV single-query attention over a KV cache
 bool attn_decode_supported(int D, int group);
 int attn_decode_splits(int B, int Hkv, int S_max);

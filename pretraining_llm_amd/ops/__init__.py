@@ -276,13 +276,11 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
 # MLP with the activation in the GEMM epilogues (csrc/gemm.hip)
 # ---------------------------------------------------------------------------
 def gemm_config(kernel: Optional[str] = None, reserve_cus: Optional[int] = None,
-                split: Optional[bool] = None, persistent: Optional[bool] = None) -> bool:
+                persistent: Optional[bool] = None) -> bool:
     """Configure the hand-written fused-epilogue TN GEMM (``torch.ops.pllm.gemm_tn``): ``kernel``
     'pp' (ping-pong main loop, csrc/gemm_pp.hip) or 'r3' (round-3 persistent kernel, csrc/gemm.hip);
     ``reserve_cus``: CUs its persistent grid leaves free (RCCL kernels run beside the backward at
-    world > 1); ``split``: the ping-pong kernel's desynchronising tile split (odd workgroups run
-    half of their last tile first, so their epilogue store bursts fall between the even ones';
-    opt-in, measured slower at the GPT-2 shapes: profiles/r4_gemm_pp.md); ``persistent`` False: the
+    world > 1); ``persistent`` False: the
     ping-pong GEMM and weight-gradient kernels launch one workgroup per tile / work item instead of one
     per CU, so a CU held by a concurrent RCCL kernel delays no tile list (the hardware deals the
     tiles to the free CUs).  None keeps the current setting; returns False without the extension (CPU)."""
@@ -292,7 +290,6 @@ def gemm_config(kernel: Optional[str] = None, reserve_cus: Optional[int] = None,
         raise ValueError(f"gemm kernel {kernel!r}: one of {sorted(_lib.GEMM_KERNELS)}")
     torch.ops.pllm.gemm_set_config(0, 0, _lib.GEMM_KERNELS[kernel] if kernel else -1,
                                    -1 if reserve_cus is None else int(reserve_cus),
-                                   -1 if split is None else int(bool(split)),
                                    -1 if persistent is None else int(bool(persistent)))
     return True
 
@@ -1094,53 +1091,6 @@ def _ce_chunk_rows(N: int, V: int = 50304, budget_bytes: Optional[int] = None) -
     return max(64, (math.ceil(N / n_chunks) + 63) // 64 * 64)
 
 
-# PLLM_CE_PIPE=K (> 1): the LM head + cross-entropy in K row chunks, each chunk's memory-bound CE pass on a
-# side HIP stream beside the compute-bound GEMMs of its neighbours (forward of chunk i + 1, data / weight
-# gradients of chunk i - 1) instead of between them
-CE_PIPE = int(_os.environ.get("PLLM_CE_PIPE", "0"))
-_CE_STREAMS = {}
-
-
-def _lm_head_ce_pipelined(h, weight, bias, targets, ignore_index, inv_n, ws, rows, dh, dw, db, wt):
-    N = h.shape[0]
-    R = (math.ceil(N / CE_PIPE) + 63) // 64 * 64
-    chunks = [(r0, min(N, r0 + R)) for r0 in range(0, N, R)]
-    main = torch.cuda.current_stream(h.device)
-    side = _CE_STREAMS.get(h.device.index)
-    if side is None:
-        side = _CE_STREAMS[h.device.index] = torch.cuda.Stream(h.device)
-    for t in (ws, rows, targets, inv_n):
-        t.record_stream(side)
-    done = []
-
-    def grads(i):
-        r0, r1 = chunks[i]
-        main.wait_event(done[i])
-        lg = ws[r0:r1]
-        if dh is not None:
-            torch.mm(lg, wt.t() if wt is not None else weight, out=dh[r0:r1])
-        if dw is not None:
-            _weight_grad(lg, h[r0:r1], dw, overwrite=i == 0)
-        if db is not None:
-            _ops().bias_grad(lg, db)
-
-    for i, (r0, r1) in enumerate(chunks):
-        lg = ws[r0:r1]
-        if bias is not None:
-            torch.addmm(bias, h[r0:r1], weight.t(), out=lg)
-        else:
-            torch.mm(h[r0:r1], weight.t(), out=lg)
-        fwd = main.record_event()
-        with torch.cuda.stream(side):
-            side.wait_event(fwd)
-            rows[r0:r1].copy_(_ops().cross_entropy(lg, targets[r0:r1], lg, ignore_index, inv_n))
-            done.append(side.record_event())
-        if i >= 1:
-            grads(i - 1)
-    grads(len(chunks) - 1)
-    main.wait_stream(side)
-
-
 class _LMHeadCEFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, weight, bias, targets, ignore_index):
@@ -1160,12 +1110,6 @@ class _LMHeadCEFn(torch.autograd.Function):
         rows = torch.empty(N, dtype=torch.float32, device=h.device)
         wt = getattr(weight, "_pllm_wT", None)
         wt = wt if wt is not None and getattr(weight, "_pllm_wT_ver", None) == weight._version else None
-        if CE_PIPE > 1 and R == N and h.is_cuda and N >= 64 * CE_PIPE:
-            _lm_head_ce_pipelined(h, weight, bias, targets, ignore_index, inv_n, ws, rows, dh, dw, db, wt)
-            ctx.save_for_backward(dh, dw, db)
-            ctx.w, ctx.b = weight, bias
-            ctx.wdtype = weight.dtype
-            return rows.sum() * inv_n[0]
         for r0 in range(0, N, R):
             r1 = min(N, r0 + R)
             hc, lg = h[r0:r1], ws[:r1 - r0]

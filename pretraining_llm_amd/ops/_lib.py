@@ -55,15 +55,12 @@ def load(raise_on_error: bool = False) -> bool:
                     torch.ops.pllm.wgrad_set_hy(int(os.environ["PLLM_WGRAD_HY"]))
                 # PLLM_GEMM_KERNEL=pp|r3: main loop of the fused-epilogue TN GEMM (ops.gemm_config);
                 # PLLM_GEMM_RESERVE_CUS=n: CUs its persistent grid leaves to concurrent RCCL kernels;
-                # PLLM_GEMM_SPLIT=0|1: the ping-pong kernel's desynchronising tile split
                 kern = os.environ.get("PLLM_GEMM_KERNEL")
                 res = os.environ.get("PLLM_GEMM_RESERVE_CUS")
-                spl = os.environ.get("PLLM_GEMM_SPLIT")
                 per = os.environ.get("PLLM_GEMM_PERSISTENT")  # 0|1: persistent GEMM grids
-                if kern or res or spl or per:
+                if kern or res or per:
                     torch.ops.pllm.gemm_set_config(0, 0, GEMM_KERNELS.get(kern, -1) if kern else -1,
-                                                   int(res) if res else -1, int(spl) if spl else -1,
-                                                   int(per) if per else -1)
+                                                   int(res) if res else -1, int(per) if per else -1)
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box

@@ -135,7 +135,7 @@ def _merge(o_acc, lse_acc, o, lse):
     (the HIP path: one fused kernel, csrc/elementwise.hip lse_merge_kernel)."""
     from .. import ops
     if (ops._hip(o) and o.dtype == torch.bfloat16 and o.shape[-1] % 8 == 0 and o.shape[-1] <= 128
-            and o.stride(-1) == 1 and o_acc.stride(-1) == 1):
+            and 64 % (o.shape[-1] // 8) == 0 and o.stride(-1) == 1 and o_acc.stride(-1) == 1):
         ops._ops().lse_merge_(o_acc, lse_acc, o, lse.float())
         return
     lse = lse.float()

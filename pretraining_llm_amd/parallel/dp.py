@@ -180,6 +180,11 @@ class DataParallelEngine:
         from .. import ops
         ops.sync_side_streams()  # side-stream weight gradients of this bucket must have landed
         bk = self.buckets[b]
+        # lazy zeroing: a weight of this bucket that no writer touched this step (unused on this rank)
+        # still holds last step's gradient -- zero it before it enters the all-reduce
+        clear = getattr(self.opt, "_clear_unwritten", None)
+        if clear is not None:
+            clear(bk["params"])
         view = self.opt.flat_grad[bk["start"]:bk["end"]]
         self.timer.launch(b)
         self._handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.pg, async_op=True))

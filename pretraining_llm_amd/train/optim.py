@@ -169,10 +169,14 @@ class FlatAdamW:
             for p in self._fresh_params:
                 p._pllm_grad_fresh = True
 
-    def _clear_unwritten(self):
-        """Fresh slots no writer touched this step (an unused weight) hold last step's gradient: zero them."""
+    def _clear_unwritten(self, idx=None):
+        """Fresh slots no writer touched this step (an unused weight) hold last step's gradient: zero them.
+        ``idx``: only these parameter indices (a DP bucket about to be all-reduced: a stale slot must be
+        zeroed BEFORE it enters the sum, or a weight unused on some ranks only would add last step's
+        gradient into every replica -- parallel/dp.py DataParallel._launch)."""
         if self.lazy_zero:
-            for p in self._fresh_params:
+            params = self._fresh_params if idx is None else [self.params[i] for i in idx]
+            for p in params:
                 if getattr(p, "_pllm_grad_fresh", False):
                     p._pllm_grad_fresh = False
                     p._pllm_gradbuf.zero_()

@@ -872,16 +872,14 @@ def test_graphed_steps_without_host_sync_match_eager():
     assert _rel(o1.master, o2.master) < 2e-2
 
 
-@pytest.mark.parametrize("chunk,pipe", [(128, 0), (8192, 0), (8192, 4)])
+@pytest.mark.parametrize("chunk", [128, 8192])
 @pytest.mark.parametrize("with_bias", [False, True])
-def test_lm_head_ce_chunked(chunk, pipe, with_bias, monkeypatch):
+def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
     """Chunked LM head + CE (logits workspace of `chunk` rows, backward GEMMs and head-bias
     column sums done per chunk in the forward, ragged last chunk) vs fp32 torch; into fp32 flat
-    gradient targets and as plain autograd gradients; no-grad evaluation path too.  pipe > 1: the
-    CE passes on a side stream beside the neighbouring chunks' GEMMs (ops.CE_PIPE)."""
+    gradient targets and as plain autograd gradients; no-grad evaluation path too."""
     from pretraining_llm_amd import ops
     monkeypatch.setattr(ops, "CE_CHUNK_ROWS", chunk)
-    monkeypatch.setattr(ops, "CE_PIPE", pipe)
     torch.manual_seed(28)
     N, C, V = 1000, 256, 50304
     h = (torch.randn(N, C, device=DEV) * 0.5).bfloat16().requires_grad_()
@@ -984,28 +982,57 @@ def _rope_case(D, Hkv):
 @pytest.mark.parametrize("M,P,Q", [(4096, 50304, 768), (2048, 50304, 2048), (1024, 11008, 2048), (8192, 65536, 256),
                                    (4096, 4104, 4104), (1024, 4352, 4096)])
 def test_wgrad_hybrid(M, P, Q):
-    """Hybrid weight gradients (wgrad_set_hy(1), csrc/wgrad_pp.hip: more tiles than workgroups -> whole tiles for
+    """Hybrid weight gradients (the default, csrc/wgrad_pp.hip: more tiles than workgroups -> whole tiles for
     the grid's whole rounds, the remaining tiles as slices of the last round, finished by the ordered fix-up;
-    edge tiles included): fp64 reference, accumulation into a non-zero gradient, run-to-run determinism, and
-    agreement with the slice kernel."""
+    edge tiles included): fp64 reference, accumulation into a non-zero gradient, OVERWRITE of a NaN-filled
+    target (every tile must be written: lazy zeroing and the LM head's first chunk rely on it), run-to-run
+    determinism, and agreement with the slice kernel."""
     torch.manual_seed(31)
     dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
     x = torch.randn(M, Q, device=DEV).bfloat16()
     w0 = torch.randn(P, Q, device=DEV)
-    ref = w0.double() + dy.double().t() @ x.double()
-    try:
-        torch.ops.pllm.wgrad_set_hy(1)
-        acc = w0.clone()
-        torch.ops.pllm.wgrad(dy, x, acc)
-        acc2 = w0.clone()
-        torch.ops.pllm.wgrad(dy, x, acc2)
-    finally:
-        torch.ops.pllm.wgrad_set_hy(0)
+    prod = dy.double().t() @ x.double()
+    ref = w0.double() + prod
+    acc = w0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc)
+    acc2 = w0.clone()
+    torch.ops.pllm.wgrad(dy, x, acc2)
     assert _rel(acc.double(), ref) < 1e-5, _rel(acc.double(), ref)
     assert torch.equal(acc, acc2)  # deterministic
-    acc3 = w0.clone()
-    torch.ops.pllm.wgrad(dy, x, acc3)  # slice kernel
+    ow = torch.full((P, Q), float("nan"), device=DEV)
+    torch.ops.pllm.wgrad(dy, x, ow, None, True)
+    assert not ow.isnan().any(), "tiles left unwritten by the overwrite path"
+    assert _rel(ow.double(), prod) < 1e-5, _rel(ow.double(), prod)
+    try:
+        torch.ops.pllm.wgrad_set_hy(0)  # the slice kernel as the reference
+        acc3 = w0.clone()
+        torch.ops.pllm.wgrad(dy, x, acc3)
+        ow3 = torch.full((P, Q), float("nan"), device=DEV)
+        torch.ops.pllm.wgrad(dy, x, ow3, None, True)
+    finally:
+        torch.ops.pllm.wgrad_set_hy(1)  # the shipped default
     assert _rel(acc.double(), acc3.double()) < 1e-6
+    assert _rel(ow.double(), ow3.double()) < 1e-6
+
+
+def test_lm_head_ce_overwrite_nan_buffer():
+    """GPT-2's LM head shape class (C = 768, V = 50304: 591 weight-gradient tiles, more than the CUs, so the
+    hybrid kernel runs) with the first chunk OVERWRITING a dw buffer that the caching allocator hands back
+    full of NaN: the weight gradient must still match fp32 torch everywhere."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(41)
+    N, C, V = 4096, 768, 50304
+    junk = torch.full((V, C), float("nan"), device=DEV)  # same-size block for the op's torch.empty
+    del junk
+    h = (torch.randn(N, C, device=DEV) * 0.5).bfloat16().requires_grad_()
+    W = (torch.randn(V, C, device=DEV) * 0.05).bfloat16().requires_grad_()
+    t = torch.randint(0, V, (N,), device=DEV)
+    loss = ops.lm_head_cross_entropy(h, W, None, t)
+    loss.backward()
+    Wf = W.detach().float().requires_grad_()
+    F.cross_entropy(h.detach().float() @ Wf.t(), t).backward()
+    assert not W.grad.isnan().any()
+    assert _rel(W.grad, Wf.grad) < 3e-2, _rel(W.grad, Wf.grad)
 
 
 @pytest.mark.parametrize("M,P,Q", [(4096, 4096, 8192), (8192, 2304, 768), (4096, 50304, 768), (2048, 200, 136)])
@@ -1063,3 +1090,46 @@ def test_lse_merge_kernel(D):
     assert torch.allclose(lse_acc, new, rtol=1e-5, atol=1e-5, equal_nan=True)
     assert torch.allclose(o_acc, ref_o, rtol=1e-5, atol=1e-5)
     assert torch.equal(full[:, :T], before)  # the rest of the buffer is untouched
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("T,S,H,Hkv,B,causal", [(2048, 2048, 4, 2, 1, True), (1000, 1000, 2, 2, 2, True),
+                                                 (512, 512, 2, 1, 2, False), (320, 384, 2, 2, 1, True),
+                                                 (300, 340, 2, 1, 1, True), (96, 700, 2, 2, 1, False)])
+def test_attention_bwd_key_stationary(D, T, S, H, Hkv, B, causal):
+    """The key-stationary backward (csrc/attn_bwd_ks.hip: 4 waves x 64 keys, dK / dV in the accumulator
+    file, one barrier per query slice) vs fp32 math and vs the previous kernels (fused-role D = 64,
+    role-split D = 128): causal and not, GQA, ragged T, queries aligned to the END of longer key rows
+    (S > T, offset 64 = 32-aligned and 40 = the per-element masked path), ragged key blocks (S = 340, 700),
+    and a forced one-key-block-per-pass run (bit-identical)."""
+    torch.manual_seed(T + S + D)
+    q = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16()
+    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16()
+    do = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    scale = 1 / math.sqrt(D)
+    o, lse = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    of, _ = _attn_ref(qf, kf, vf, causal, scale)
+    of.backward(do.float())
+    try:
+        torch.ops.pllm.attn_bwd_set_ks(3)
+        got = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *got, causal, scale)
+        for a, b, n in zip(got, (qf.grad, kf.grad, vf.grad), ("dq", "dk", "dv")):
+            assert not a.isnan().any(), n
+            assert _rel(a, b) < 2e-2, (n, _rel(a, b))
+        torch.ops.pllm.attn_bwd_set_workspace_mb(1e-3)  # one key block per pass
+        got2 = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *got2, causal, scale)
+        for a, b in zip(got2, got):
+            assert torch.equal(a, b)
+        torch.ops.pllm.attn_bwd_set_workspace_mb(4096)
+        torch.ops.pllm.attn_bwd_set_ks(0)
+        old = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *old, causal, scale)
+        for a, b, n in zip(got, old, ("dq", "dk", "dv")):
+            assert _rel(a, b) < 1e-2, (n, _rel(a, b))
+    finally:
+        torch.ops.pllm.attn_bwd_set_workspace_mb(4096)
+        torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
