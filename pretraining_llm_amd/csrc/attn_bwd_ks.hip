@@ -235,92 +235,152 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
       const int qj0 = q0 + 32 * j;
-      // body<L1, M0, M1>: key block 1 live (else its dS^T rows are zeros), per-element masks on the
-      // key blocks (compile-time per code path; lo: element i dead iff acc_row(i, 0) < lo)
-      // one key block (KH) of this wave: S = Q K^T, dP = dO V^T (key on the lane), P / dS, dV^T / dK^T
-      // updates, dS^T image rows.  ONE code path for every sub-block that has a live key: the
-      // causal / ragged-end mask is a wave-uniform branch around a VALU-only fix-up of P (element i
-      // dead iff acc_row(i, 0) < lo), and a fully masked key block simply adds zeros.  (Per-case code
-      // paths made hipcc copy the 256 dK / dV accumulator registers at every join.)  Key blocks run one
-      // after the other, each re-reading the Q / dO fragments: with both in flight it spilled.
+      // Software-pipelined sub-block: the wave's two key blocks (kb 0, 1) run staggered so that each
+      // MFMA chain has the other block's VALU work beside it -- with one wave per SIMD nothing else
+      // would fill the matrix pipe during the softmax:
+      //   A: S0 / dP0 chains (16 MFMAs)
+      //   B: S1 / dP1 chains          || P0 = exp2(S0 c2 - lse log2 e), dS0 = P0 (dP0 - delta), packs
+      //   C: dV0 / dK0 (16 MFMAs)     || P1, dS1, packs
+      //   D: dV1 / dK1 (16 MFMAs)     || dS^T image rows of both blocks
+      // Each step is a run of (LDS reads one step ahead, 2 MFMAs, a slice of the other block's VALU)
+      // groups fenced by sched_barrier, so hipcc neither clusters the MFMAs nor hoists the reads.
+      // Masking (causal diagonal, ragged key end, unaligned offset) is folded into the S chains'
+      // initial accumulators (0 or -inf per element: p = exp2(-inf) = 0), set up behind ONE wave-uniform
+      // branch before the straight-line steps; a sub-block whose keys all follow its queries is fully
+      // masked rather than skipped (one wave per SIMD: a skip saves no wall time, and a branch around
+      // the dK / dV updates made hipcc copy the 256 accumulators at the join).
       const bool mask_j = !aligned || (a.causal && kw0 + 63 > qj0 + off);  // wave-uniform
-      auto block = [&](auto kh_c) {
-        constexpr int KH = decltype(kh_c)::value;
-        f32x16 sc, dp;
+      f32x16 s0, s1, d0, d1;
+      if (mask_j) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 rd = *reinterpret_cast<const f32x4*>(&rl[BQ + 32 * j + 8 * g + 4 * hh]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) dp[4 * g + e] = rd[e];  // dP accumulated onto -delta
-        }
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          const int fo = fq ^ (ks << 4);
-          const bf16x8 qa = as_frag(ld16(Ql + 32 * j * D + fo));
-          const bf16x8 oa = as_frag(ld16(Ol + 32 * j * D + fo));
-          const bf16x8 kf = as_frag(ld16(Kl + (64 * w + 32 * KH) * D + fo));
-          if (ks == 0) mfma_v0(sc, qa, kf);
-          else mfma_v(sc, qa, kf);
-          mfma_v(dp, oa, vf[KH][ks]);
-        }
-        mfma_settle(sc, dp);
-        // P = exp2(S c2 - lse log2 e)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 rs = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) sc[4 * g + e] = fast_exp2(__builtin_fmaf(sc[4 * g + e], c2, rs[e]));
-        }
-        if (mask_j) {
-          const int key = kw0 + 32 * KH + r;
+        for (int kh = 0; kh < 2; ++kh) {
+          const int key = kw0 + 32 * kh + r;
           const int lo = key >= a.S ? 64 : (a.causal ? key - off - (qj0 + 4 * hh) : -64);
 #pragma unroll
-          for (int i = 0; i < 16; ++i) sc[i] = acc_row(i, 0) < lo ? 0.f : sc[i];
-        }
-        // dS = P (dP - delta)   (unscaled)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) dp[i] = sc[i] * dp[i];
-        const bf16x8 pf0 = pack_frag(sc, 0), pf1 = pack_frag(sc, 1);
-        const bf16x8 sf0 = pack_frag(dp, 0), sf1 = pack_frag(dp, 1);
-        // dV^T += dO^T P ; dK^T += Q^T dS   (A operands by transposed reads of the [q][d] images)
-#pragma unroll
-        for (int db = 0; db < NDB; ++db) {
-#pragma unroll
-          for (int st = 0; st < 2; ++st) {
-            const int rb = (32 * j + 16 * st) * D, o0 = rb + (ft0 ^ (db << 5)), o8 = rb + (ft8 ^ (db << 5));
-            const bf16x8 oA = cat_tr(ds_tr(Ol + o0), ds_tr(Ol + o8));
-            const bf16x8 qA = cat_tr(ds_tr(Ql + o0), ds_tr(Ql + o8));
-            mfma_a(dv[KH][db], oA, st == 0 ? pf0 : pf1);
-            mfma_a(dk[KH][db], qA, st == 0 ? sf0 : sf1);
+          for (int i = 0; i < 16; ++i) {
+            const float mv = acc_row(i, 0) < lo ? -INFINITY : 0.f;
+            if (kh == 0) s0[i] = mv;
+            else s1[i] = mv;
           }
         }
-        // dS^T image rows of these keys: group pairs of 4 queries swapped across the half-waves
-        // (v_permlane32_swap), one 16-B store of 8 consecutive queries per pair
-        const int row = 64 * w + 32 * KH + r;
-        u32x2 v[4];
+      } else {
+        s0 = zero16();
+        s1 = zero16();
+      }
+      float rs[16];  // -lse log2(e) of the lane's 16 query rows
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const u32x4 w4 = __builtin_bit_cast(u32x4, g < 2 ? sf0 : sf1);
-          v[g] = u32x2{w4[2 * (g & 1)], w4[2 * (g & 1) + 1]};
+      for (int g = 0; g < 4; ++g) {
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(&rl[BQ + 32 * j + 8 * g + 4 * hh]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          rs[4 * g + e] = x[e];
+          d0[4 * g + e] = y[e];  // dP accumulated onto -delta
         }
+      }
+      d1 = d0;
+      __builtin_amdgcn_sched_barrier(0);
+      // fragment reads of the S / dP chains: Q, dO rows of the sub-block and K rows of key block KH
+      auto rd_sd = [&](int KH, int ks, bf16x8& qa, bf16x8& oa, bf16x8& kf) {
+        const int fo = fq ^ (ks << 4);
+        qa = as_frag(ld16(Ql + 32 * j * D + fo));
+        oa = as_frag(ld16(Ol + 32 * j * D + fo));
+        kf = as_frag(ld16(Kl + (64 * w + 32 * KH) * D + fo));
+      };
+      // transposed A operands of the dV / dK updates, step t = (db, st)
+      auto rd_tr = [&](int t, bf16x8& oA, bf16x8& qA) {
+        const int db = t >> 1, st = t & 1;
+        const int rb = (32 * j + 16 * st) * D, o0 = rb + (ft0 ^ (db << 5)), o8 = rb + (ft8 ^ (db << 5));
+        oA = cat_tr(ds_tr(Ol + o0), ds_tr(Ol + o8));
+        qA = cat_tr(ds_tr(Ql + o0), ds_tr(Ql + o8));
+      };
+      // softmax slice of one key block: elements [i0, i0 + n) of P = exp2(S c2 + rs), dS = P dP
+      auto sm = [&](f32x16& sc, f32x16& dp, int i0, int n) {
 #pragma unroll
-        for (int k = 0; k < 4; k += 2) {
-#pragma unroll
-          for (int d = 0; d < 2; ++d) {
-            const auto sw = __builtin_amdgcn_permlane32_swap(v[k][d], v[k + 1][d], false, false);
-            v[k][d] = sw[0];
-            v[k + 1][d] = sw[1];
-          }
-          *reinterpret_cast<u32x4*>(Sd + IT::off(row, 32 * j + 8 * k + 8 * hh)) =
-              u32x4{v[k][0], v[k][1], v[k + 1][0], v[k + 1][1]};
+        for (int i = i0; i < i0 + n; ++i) {
+          const float pv = fast_exp2(__builtin_fmaf(sc[i], c2, rs[i]));
+          sc[i] = pv;
+          dp[i] = pv * dp[i];
         }
       };
-      // A sub-block whose keys all follow its queries (causal) is not skipped: its mask zeroes every
-      // P, so it adds nothing -- and with one wave per SIMD a skip saves no wall time (wave 0 is
-      // never dead and the slice ends at the barrier), while a branch around the dK / dV updates
-      // made hipcc copy the 256 accumulators at the join
-      block(std::integral_constant<int, 0>{});
-      block(std::integral_constant<int, 1>{});
+      constexpr int NT2 = 2 * NDB;  // (db, st) steps of a dV / dK update
+      constexpr int EPS = 16 / NKS;  // softmax elements per step of the S / dP chains
+      constexpr int EPT = 16 / NT2;  // ... per step of the dV / dK updates
+      bf16x8 qa[2], oa[2], kf[2];
+      // ---- A: S0 / dP0
+      rd_sd(0, 0, qa[0], oa[0], kf[0]);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int c = ks & 1;
+        if (ks + 1 < NKS) rd_sd(0, ks + 1, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);
+        else rd_sd(1, 0, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);  // step B's first reads
+        mfma_v(s0, qa[c], kf[c]);
+        mfma_v(d0, oa[c], vf[0][ks]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- B: S1 / dP1 || softmax of block 0
+      bf16x8 pf0[2], sf0[2];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        const int c = (ks + NKS) & 1;
+        if (ks + 1 < NKS) rd_sd(1, ks + 1, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);
+        mfma_v(s1, qa[c], kf[c]);
+        mfma_v(d1, oa[c], vf[1][ks]);
+        if (ks == 0) mfma_settle(s0, d0);  // block 0's chains done (behind this step's MFMAs)
+        sm(s0, d0, EPS * ks, EPS);
+        if ((EPS * (ks + 1)) % 8 == 0) {  // 8 elements done: one packed fragment pair
+          const int h8 = EPS * (ks + 1) / 8 - 1;
+          pf0[h8] = pack_frag(s0, h8);
+          sf0[h8] = pack_frag(d0, h8);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- C: dV0 / dK0 || softmax of block 1
+      bf16x8 pf1[2], sf1[2];
+      bf16x8 oA[2], qA[2];
+      rd_tr(0, oA[0], qA[0]);
+#pragma unroll
+      for (int t = 0; t < NT2; ++t) {
+        const int c = t & 1;
+        rd_tr(t + 1 < NT2 ? t + 1 : 0, oA[c ^ 1], qA[c ^ 1]);  // (step D re-reads from t = 0)
+        mfma_a(dv[0][t >> 1], oA[c], pf0[t & 1]);
+        mfma_a(dk[0][t >> 1], qA[c], sf0[t & 1]);
+        if (t == 0) mfma_settle(s1, d1);
+        sm(s1, d1, EPT * t, EPT);
+        if ((EPT * (t + 1)) % 8 == 0) {
+          const int h8 = EPT * (t + 1) / 8 - 1;
+          pf1[h8] = pack_frag(s1, h8);
+          sf1[h8] = pack_frag(d1, h8);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // ---- D: dV1 / dK1 || dS^T image rows of both key blocks (group pairs of 4 queries swapped
+      // across the half-waves by v_permlane32_swap: one 16-B store of 8 consecutive queries per pair)
+      auto ds_store = [&](int KH, const bf16x8 (&sf)[2], int k) {
+        u32x2 v0, v1;
+        {
+          const u32x4 w4 = __builtin_bit_cast(u32x4, sf[k >> 1]);
+          v0 = u32x2{w4[0], w4[1]};
+          v1 = u32x2{w4[2], w4[3]};
+        }
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          const auto sw = __builtin_amdgcn_permlane32_swap(v0[d], v1[d], false, false);
+          v0[d] = sw[0];
+          v1[d] = sw[1];
+        }
+        *reinterpret_cast<u32x4*>(Sd + IT::off(64 * w + 32 * KH + r, 32 * j + 8 * k + 8 * hh)) =
+            u32x4{v0[0], v0[1], v1[0], v1[1]};
+      };
+#pragma unroll
+      for (int t = 0; t < NT2; ++t) {
+        const int c = (t + NT2) & 1;
+        if (t + 1 < NT2) rd_tr(t + 1, oA[c ^ 1], qA[c ^ 1]);
+        mfma_a(dv[1][t >> 1], oA[c], pf1[t & 1]);
+        mfma_a(dk[1][t >> 1], qA[c], sf1[t & 1]);
+        if (t < 4) ds_store(t >> 1, t < 2 ? sf0 : sf1, 2 * (t & 1));
+        __builtin_amdgcn_sched_barrier(0);
+      }
     }
     // ---- hand-off: this slice's dS^T image and the next slice's Q / dO / row constants
     vm_wait_all();  // own DMA pieces of slice it + 1, its row constants, this wave's previous dQ stores
