@@ -306,24 +306,33 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       constexpr int NT2 = 2 * NDB;  // (db, st) steps of a dV / dK update
       constexpr int EPS = 16 / NKS;  // softmax elements per step of the S / dP chains
       constexpr int EPT = 16 / NT2;  // ... per step of the dV / dK updates
-      bf16x8 qa[2], oa[2], kf[2];
+      // LDS reads run TWO steps ahead of their MFMAs (3-deep register rings; one step = 2 MFMAs = 64
+      // cycles did not cover the read latency under load: WAIT_ANY 38 % of wave cycles)
+      constexpr int RA = 2;
+      bf16x8 qa[RA + 1], oa[RA + 1], kf[RA + 1];
+      auto rd_u = [&](int u) {  // S / dP step u of the A-then-B sequence: key block u / NKS, ks u % NKS
+        rd_sd(u / NKS, u % NKS, qa[u % (RA + 1)], oa[u % (RA + 1)], kf[u % (RA + 1)]);
+      };
+#pragma unroll
+      for (int u = 0; u < RA; ++u) rd_u(u);
       // ---- A: S0 / dP0
-      rd_sd(0, 0, qa[0], oa[0], kf[0]);
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const int c = ks & 1;
-        if (ks + 1 < NKS) rd_sd(0, ks + 1, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);
-        else rd_sd(1, 0, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);  // step B's first reads
+        rd_u(ks + RA);
+        const int c = ks % (RA + 1);
         mfma_v(s0, qa[c], kf[c]);
         mfma_v(d0, oa[c], vf[0][ks]);
         __builtin_amdgcn_sched_barrier(0);
       }
       // ---- B: S1 / dP1 || softmax of block 0
       bf16x8 pf0[2], sf0[2];
+      bf16x8 oA[RA + 1], qA[RA + 1];
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
-        const int c = (ks + NKS) & 1;
-        if (ks + 1 < NKS) rd_sd(1, ks + 1, qa[c ^ 1], oa[c ^ 1], kf[c ^ 1]);
+        const int u = NKS + ks;
+        if (u + RA < 2 * NKS) rd_u(u + RA);
+        else rd_tr((u + RA - 2 * NKS) % NT2, oA[(u + RA - 2 * NKS) % (RA + 1)], qA[(u + RA - 2 * NKS) % (RA + 1)]);
+        const int c = u % (RA + 1);
         mfma_v(s1, qa[c], kf[c]);
         mfma_v(d1, oa[c], vf[1][ks]);
         if (ks == 0) mfma_settle(s0, d0);  // block 0's chains done (behind this step's MFMAs)
@@ -335,14 +344,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
-      // ---- C: dV0 / dK0 || softmax of block 1
+      // ---- C: dV0 / dK0 || softmax of block 1   (transposed-read step v of the C-then-D sequence)
       bf16x8 pf1[2], sf1[2];
-      bf16x8 oA[2], qA[2];
-      rd_tr(0, oA[0], qA[0]);
 #pragma unroll
       for (int t = 0; t < NT2; ++t) {
-        const int c = t & 1;
-        rd_tr(t + 1 < NT2 ? t + 1 : 0, oA[c ^ 1], qA[c ^ 1]);  // (step D re-reads from t = 0)
+        const int v = t;
+        rd_tr((v + RA) % NT2, oA[(v + RA) % (RA + 1)], qA[(v + RA) % (RA + 1)]);
+        const int c = v % (RA + 1);
         mfma_a(dv[0][t >> 1], oA[c], pf0[t & 1]);
         mfma_a(dk[0][t >> 1], qA[c], sf0[t & 1]);
         if (t == 0) mfma_settle(s1, d1);
@@ -374,8 +382,9 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       };
 #pragma unroll
       for (int t = 0; t < NT2; ++t) {
-        const int c = (t + NT2) & 1;
-        if (t + 1 < NT2) rd_tr(t + 1, oA[c ^ 1], qA[c ^ 1]);
+        const int v = NT2 + t;
+        if (v + RA < 2 * NT2) rd_tr((v + RA) % NT2, oA[(v + RA) % (RA + 1)], qA[(v + RA) % (RA + 1)]);
+        const int c = v % (RA + 1);
         mfma_a(dv[1][t >> 1], oA[c], pf1[t & 1]);
         mfma_a(dk[1][t >> 1], qA[c], sf1[t & 1]);
         if (t < 4) ds_store(t >> 1, t < 2 ? sf0 : sf1, 2 * (t & 1));
@@ -394,13 +403,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     const int qt0 = q0 + 32 * tq_blk;
     if (qt0 < a.T) {
       f32x16 acc;
+      constexpr int QA = 3;  // transposed reads QA steps ahead of the MFMA chain
+      bf16x8 fa[QA + 1], fb[QA + 1];
+      auto rd_q = [&](int ks) {
+        fa[ks % (QA + 1)] = cat_tr(ds_tr(Sd + 16 * ks * BQ + sa0), ds_tr(Sd + 16 * ks * BQ + sa4));
+        fb[ks % (QA + 1)] = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
+      };
+#pragma unroll
+      for (int ks = 0; ks < QA; ++ks) rd_q(ks);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
-        const bf16x8 A = cat_tr(ds_tr(Sd + 16 * ks * BQ + sa0), ds_tr(Sd + 16 * ks * BQ + sa4));
-        const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
-        if (ks == 0) mfma_v0(acc, Bf, A);
-        else mfma_v(acc, Bf, A);
-        if (ks % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+        if (ks + QA < BK / 16) rd_q(ks + QA);
+        if (ks == 0) mfma_v0(acc, fb[0], fa[0]);
+        else mfma_v(acc, fb[ks % (QA + 1)], fa[ks % (QA + 1)]);
+        __builtin_amdgcn_sched_barrier(0);
       }
       mfma_settle(acc);
       float lo[8], hi[8];

@@ -76,6 +76,12 @@ for task in "$@"; do
       done
       python3 scripts/pmc_kernels.py "$name: $script ${sargs//+/ }" "${dirs[@]}" > "$O/$name.md" || exit 1
       grep -E "^## |MFMA busy|shares" "$O/$name.md" | head -30 ;;
+    ktrace)  # kernel trace + stats of a script: ktrace:<name>:<script>[:args]
+      IFS=':' read -r script sargs <<< "$rest"
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv -- \
+          python3 "$R/$script" ${sargs//+/ } > "$O/$name.log" 2>&1 ) || { tail -5 "$O/$name.log"; exit 1; }
+      python3 scripts/prof_summary.py "$O/$name/run_kernel_stats.csv" 1 "$name: $script ${sargs//+/ }" > "$O/$name.md" || exit 1
+      head -14 "$O/$name.md" ;;
     py)
       IFS=':' read -r script sargs <<< "$rest"
       timeout -k 10 600 python3 -u "$script" ${sargs//+/ } > "$O/$name.log" 2>&1 || { tail -5 "$O/$name.log"; exit 1; }
