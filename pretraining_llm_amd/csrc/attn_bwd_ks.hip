@@ -13,22 +13,32 @@
 // result as an operand so every consumer is ordered after it) precedes any non-MFMA reader.
 #include <type_traits>
 
+#ifndef PLLM_BWD_STAMPS
+#define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums (scripts/build_variant.py -DPLLM_BWD_STAMPS=1)
+#endif
+
 #include "attn_common.h"
 #include "common.h"
 #include "kernels.h"
 
 namespace {
 
-// v_mfma_f32_32x32x16_bf16 with the accumulator in arch VGPRs: acc (+)= A B
+// v_mfma_f32_32x32x16_bf16 with the accumulator in arch VGPRs: acc (+)= A B.  NOP: the statement opens
+// with s_nop 1 (2 wait states) -- needed when A / B / C was just written by a VALU instruction (a chain's
+// first MFMA after its VALU-initialised accumulator); A / B from LDS reads and C from the chain's
+// previous MFMA need none (s_nop 1 on all 80 MFMAs of a slice cost ~160 issue cycles per wave)
+template <bool NOP = false>
 PLLM_DEV void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
+  else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
-PLLM_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
+PLLM_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B (A, B from LDS)
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
 }
-// ... with the accumulator pinned to the accumulator file
+// ... with the accumulator pinned to the accumulator file.  B (the packed P / dS fragments) was written
+// by VALU at least one pipelined step (>= 2 MFMAs) earlier; the accumulators' zero init is far back
 PLLM_DEV void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
+  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // an MFMA result read by anything but the next MFMA of its chain: 16-pass XDL -> 18 wait states
 PLLM_DEV void mfma_settle(f32x16& x) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x)); }
@@ -220,6 +230,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   const int sa00 = IT::off(8 * hh + tq, qc), sa40 = IT::off(8 * hh + tq + 4, qc);
   const int ka00 = I::off(8 * hh + tq, dc), ka40 = I::off(8 * hh + tq + 4, dc);
 
+#if PLLM_BWD_STAMPS
+  // diagnostic build: per-wave s_memtime sums of the slice phases (host: PLLM_BWD_STAMPS=1 prints them)
+  uint64_t st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t st_start = __builtin_amdgcn_s_memtime();
+  uint64_t ts_prev = st_start;
+  auto stamp = [&](int i) {
+    const uint64_t now = __builtin_amdgcn_s_memtime();
+    st_acc[i] += now - ts_prev;
+    ts_prev = now;
+  };
+#define KS_STAMP(i) stamp(i)
+#else
+#define KS_STAMP(i)
+#endif
   int h = hk * G, qi = qs_start;  // (head, slice) of iteration it, advanced incrementally
   for (int it = 0; it < total; ++it, (++qi == nqs) ? (qi = qs_start, ++h) : 0) {
     const int sl = it & 1;
@@ -280,6 +304,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       }
       d1 = d0;
       __builtin_amdgcn_sched_barrier(0);
+      KS_STAMP(7);
       // fragment reads of the S / dP chains: Q, dO rows of the sub-block and K rows of key block KH
       auto rd_sd = [&](int KH, int ks, bf16x8& qa, bf16x8& oa, bf16x8& kf) {
         const int fo = fq ^ (ks << 4);
@@ -320,10 +345,16 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       for (int ks = 0; ks < NKS; ++ks) {
         rd_u(ks + RA);
         const int c = ks % (RA + 1);
-        mfma_v(s0, qa[c], kf[c]);
-        mfma_v(d0, oa[c], vf[0][ks]);
+        if (ks == 0) {
+          mfma_v<true>(s0, qa[c], kf[c]);  // s0 / d0: VALU-initialised (mask / -delta)
+          mfma_v<true>(d0, oa[c], vf[0][ks]);
+        } else {
+          mfma_v(s0, qa[c], kf[c]);
+          mfma_v(d0, oa[c], vf[0][ks]);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+      KS_STAMP(0);
       // ---- B: S1 / dP1 || softmax of block 0
       bf16x8 pf0[2], sf0[2];
       bf16x8 oA[RA + 1], qA[RA + 1];
@@ -333,8 +364,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         if (u + RA < 2 * NKS) rd_u(u + RA);
         else rd_tr((u + RA - 2 * NKS) % NT2, oA[(u + RA - 2 * NKS) % (RA + 1)], qA[(u + RA - 2 * NKS) % (RA + 1)]);
         const int c = u % (RA + 1);
-        mfma_v(s1, qa[c], kf[c]);
-        mfma_v(d1, oa[c], vf[1][ks]);
+        if (ks == 0) {
+          mfma_v<true>(s1, qa[c], kf[c]);
+          mfma_v<true>(d1, oa[c], vf[1][ks]);
+        } else {
+          mfma_v(s1, qa[c], kf[c]);
+          mfma_v(d1, oa[c], vf[1][ks]);
+        }
         if (ks == 0) mfma_settle(s0, d0);  // block 0's chains done (behind this step's MFMAs)
         sm(s0, d0, EPS * ks, EPS);
         if ((EPS * (ks + 1)) % 8 == 0) {  // 8 elements done: one packed fragment pair
@@ -344,6 +380,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      KS_STAMP(1);
       // ---- C: dV0 / dK0 || softmax of block 1   (transposed-read step v of the C-then-D sequence)
       bf16x8 pf1[2], sf1[2];
 #pragma unroll
@@ -362,6 +399,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      KS_STAMP(2);
       // ---- D: dV1 / dK1 || dS^T image rows of both key blocks (group pairs of 4 queries swapped
       // across the half-waves by v_permlane32_swap: one 16-B store of 8 consecutive queries per pair)
       auto ds_store = [&](int KH, const bf16x8 (&sf)[2], int k) {
@@ -391,6 +429,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    KS_STAMP(3);
     // ---- hand-off: this slice's dS^T image and the next slice's Q / dO / row constants
     vm_wait_all();  // own DMA pieces of slice it + 1, its row constants, this wave's previous dQ stores
     if (it + 1 < total) rstore(it + 1);
@@ -399,6 +438,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       qdma(it + 2, sl);  // every wave is past its reads of slot sl (slice it)
       rload(it + 2);
     }
+    KS_STAMP(4);
     // ---- dQ partial of this key block: dQ^T tile (32 dims x 32 queries) = K^T dS^T over 256 keys
     const int qt0 = q0 + 32 * tq_blk;
     if (qt0 < a.T) {
@@ -430,7 +470,20 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       st16(dqp, pack8(lo));
       st16(dqp + 8, pack8(hi));
     }
+    KS_STAMP(5);
+#if PLLM_BWD_STAMPS
+    st_acc[6] += 1;
+#endif
   }
+#if PLLM_BWD_STAMPS
+  if (a.stamps && lane == 0) {
+    unsigned long long* stp = a.stamps + ((int64_t)blockIdx.x * 4 + w) * 9;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stp[i] = st_acc[i];
+    stp[8] = __builtin_amdgcn_s_memtime() - st_start;
+  }
+#endif
+#undef KS_STAMP
   // ---- dK (scaled; RoPE: rotated back, R^T) and dV of this lane's keys: the accumulators settle
   // (18 wait states after the last MFMA), then every one is pinned behind that statement
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");

@@ -1021,7 +1021,7 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.delta_split = dsplit ? 2 : 1;
   static const bool bstamps = std::getenv("PLLM_BWD_STAMPS") != nullptr;
   Tensor bst;
-  if (bstamps && D <= 64) {  // diagnostic, with a PLLM_BWD_STAMPS=1 build of attention.hip
+  if (bstamps) {  // diagnostic, with a PLLM_BWD_STAMPS=1 build of attention.hip / attn_bwd_ks.hip
     bst = at::zeros({nkb * B * Hkv * 8 * 9}, q.options().dtype(at::kLong));
     a.stamps = (unsigned long long*)bst.data_ptr();
   }
@@ -1030,7 +1030,10 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
     auto hs = bst.view({-1, 9}).to(at::kCPU).to(at::kDouble);
     auto tot = hs.sum(0);
     const double its = tot[6].item<double>();
-    fprintf(stderr, "[bwd stamps] waves %lld iters %.0f | per iter: wait+barrier %.0f stage+barrier %.0f gload %.0f subblocks %.0f barrier %.0f dq %.0f loop-top %.0f | per wave %.0f\n",
+    // fused-role kernel: wait+barrier, stage+barrier, gload, subblocks, barrier, dq, -, loop-top;
+    // key-stationary kernel: A (S0/dP0), B (S1/dP1 | softmax 0), C (dV0/dK0 | softmax 1), D (dV1/dK1 | dS^T),
+    // wait + barrier + DMA issue, dQ task, -, init
+    fprintf(stderr, "[bwd stamps] waves %lld iters %.0f | per iter (cycles): p0 %.0f p1 %.0f p2 %.0f p3 %.0f p4 %.0f p5 %.0f p7 %.0f | per wave %.0f\n",
             (long long)hs.size(0), its, tot[0].item<double>() / its, tot[1].item<double>() / its,
             tot[2].item<double>() / its, tot[3].item<double>() / its, tot[4].item<double>() / its,
             tot[5].item<double>() / its, tot[7].item<double>() / its, tot[8].item<double>() / hs.size(0));
