@@ -185,18 +185,18 @@ def main(argv=None):
         opt.zero_grad()
         return loss
 
+    from pretraining_llm_amd.train import graph as _graph
     if args.cuda_graph == "auto":
-        from pretraining_llm_amd.train.graph import graph_step_policy
-        ok, _why = graph_step_policy(cuda=not cpu, world=world, dist_backend=di.backend if world > 1 else None,
-                                     zero=bool(args.zero), hip_ops=args.backend == "auto" and bool(getattr(opt, "use_hip", False)),
-                                     graph_collectives=args.graph_collectives)
+        ok, _why = _graph.graph_step_policy(cuda=not cpu, world=world, dist_backend=di.backend if world > 1 else None,
+                                            zero=bool(args.zero),
+                                            hip_ops=args.backend == "auto" and bool(getattr(opt, "use_hip", False)),
+                                            graph_collectives=args.graph_collectives)
         args.cuda_graph = "1" if ok else "0"
     args.cuda_graph = args.cuda_graph == "1"
     if args.cuda_graph:
-        from pretraining_llm_amd.train.graph import GraphedTrainStep
         engine.timer.enabled = False  # no event records inside a captured graph
         x0, y0 = loader.next()
-        gstep = GraphedTrainStep(model, opt, engine, B, T, dev, warmup=2).capture(x0, y0, 6e-4)
+        gstep = _graph.GraphedTrainStep(model, opt, engine, B, T, dev, warmup=2).capture(x0, y0, 6e-4)
 
         def step():  # noqa: F811
             x, y = loader.next()

@@ -158,12 +158,13 @@ class Trainer:
         self.gstep = None
         self.use_graph = False
         self.fwd = self.model
-        if self.compile and self.device.type == "cuda":
+        if self.compile:
             # the same policy bench.py applies (train/graph.py): at world > 1 the eager step with
-            # hook-launched RCCL buckets unless graph_collectives=True
-            from .graph import graph_step_policy
-            ok, why = graph_step_policy(
-                cuda=True, world=self.di.world_size, dist_backend=dist.get_backend() if dist.is_initialized() else None,
+            # hook-launched RCCL buckets unless graph_collectives=True; on the CPU torch.compile
+            from . import graph as _graph
+            ok, why = _graph.graph_step_policy(
+                cuda=self.device.type == "cuda", world=self.di.world_size,
+                dist_backend=dist.get_backend() if dist.is_initialized() else None,
                 zero=int(self.cfg.get("zero_stage", 0)) >= 1, model_parallel=self.pg.model_parallel,
                 loss_scaling=self.scaler.enabled, bf16=self.dtype == torch.bfloat16, hip_ops=self._hip_step_ok(),
                 graph_collectives=bool(self.cfg.get("graph_collectives", False)))
@@ -171,10 +172,10 @@ class Trainer:
                 self.use_graph = True
                 if self.di.is_master:
                     self.log(f"TORCH_COMPILE: whole training step captured as a hipGraph (grad_accum_steps={self.accum})")
+            elif self.device.type != "cuda":
+                self.fwd = torch.compile(self.model, backend=self.cfg.get("compile_backend", "inductor"))
             elif self.di.is_master:
                 self.log(f"TORCH_COMPILE: hipGraph step disabled for this configuration ({why}); running eagerly")
-        elif self.compile:
-            self.fwd = torch.compile(self.model, backend=self.cfg.get("compile_backend", "inductor"))
         self.step_mode = "graph" if self.use_graph else "eager"
         self.metrics = MetricsLogger(self.cfg.get("metrics_path"), enabled=self.di.is_master)
         self.train_loader = self._loader(self.cfg["train_path"], seed, 0)
@@ -211,7 +212,7 @@ class Trainer:
     def train_step(self) -> torch.Tensor:
         """One optimizer step (``grad_accum_steps`` micro-batches). Returns the mean loss (device tensor)."""
         lr = self.lr(self.step)
-        if self.use_graph and self.gstep is None and not self._hip_step_ok():
+        if self.use_graph and self.gstep is None and self.device.type == "cuda" and not self._hip_step_ok():
             self.use_graph = False  # the op backend was switched to torch after construction
         if self.use_graph:
             return self._graph_step(lr)
@@ -256,15 +257,15 @@ class Trainer:
         """hipGraph-replayed step.  The first call runs one real (eager, side-stream) step on its
         batch -- it also teaches the DP engine its bucket order -- then captures the step; every
         later call copies its micro-batches into the static inputs and replays."""
-        from .graph import GraphedTrainStep
+        from . import graph as _graph
         batches = [self.train_loader.next() for _ in range(self.accum)]
         x = torch.stack([b[0] for b in batches])
         y = torch.stack([b[1] for b in batches])
         self.step += 1
         if self.gstep is None:
             _, B, T = x.shape
-            self.gstep = GraphedTrainStep(self.model, self.opt, self.engine, B, T, self.device, warmup=1,
-                                          accum=self.accum)
+            self.gstep = _graph.GraphedTrainStep(self.model, self.opt, self.engine, B, T, self.device, warmup=1,
+                                                 accum=self.accum)
             self.gstep.capture(x, y, lr)
             return self.gstep.warmup_loss
         return self.gstep(x, y, lr).clone()

@@ -209,20 +209,42 @@ def test_byte_tokenizer_renders_non_byte_ids():
     assert t.decode(t.encode("plain")) == "plain"
 
 
-def test_trainer_and_bench_share_the_step_policy():
-    """the Trainer's world > 1 step and ``bench.py --gpus N`` must be the same path.
-    Both decide through ``train/graph.py: graph_step_policy``; at world > 1 on RCCL the default
-    is the eager step with hook-launched buckets (capture is the ``graph_collectives`` opt-in),
-    at world 1 the hipGraph step."""
-    import inspect
+@pytest.mark.parametrize("mode", ["default", "graph_collectives"])
+def test_trainer_and_bench_take_the_same_step_path(mode, tmp_path):
+    """the Trainer's world > 1 step and ``bench.py --gpus N`` take the same path,
+    checked by what they DO: 2 gloo ranks (torch.distributed.run) with the step policy stubbed to the
+    RCCL branch (GPU, nccl, HIP ops) and a recording eager stand-in for the hipGraph capture
+    (tests/_policy_probe.py).  Default: both run the eager hook-overlapped step (no capture object
+    built); graph_collectives=True: both build the capture and step through it."""
+    import json
+    import subprocess
     import sys
-    from pretraining_llm_amd.train import graph as g
-    from pretraining_llm_amd.train import trainer as tr
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path.insert(0, root)
-    import bench
-    assert "graph_step_policy(" in inspect.getsource(tr.Trainer.__init__)
-    assert "graph_step_policy(" in inspect.getsource(bench.main)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "2"
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nproc-per-node", "2", "--master-addr",
+                        "127.0.0.1", "--master-port", str(_free_port()), os.path.join(root, "tests", "_policy_probe.py"),
+                        mode, str(tmp_path)], capture_output=True, text=True, timeout=300, cwd="/tmp", env=env)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    recs = [json.loads(l.split("PROBE ", 1)[1]) for l in r.stdout.splitlines() if "PROBE " in l]
+    assert sorted(x["rank"] for x in recs) == [0, 1], r.stdout
+    want = "graph" if mode == "graph_collectives" else "eager"
+    for x in recs:
+        t, b = x["trainer"], x["bench"]
+        assert t["step_mode"] == want, x
+        assert b["rc"] in (None, 0), x
+        if x["rank"] == 0:
+            assert b["step_mode"] == want, x  # rank 0 prints the bench record
+        if want == "graph":
+            assert t["capture_objects"] == 1 and t["captured_steps"] == 2, x
+            assert b["capture_objects"] == 1 and b["captured_steps"] >= 3, x  # 2 warmup-less timed + capture
+        else:
+            assert t["capture_objects"] == 0 and b["capture_objects"] == 0, x
+
+
+def test_step_policy_decisions():
+    """graph_step_policy's table (the function both launch paths call, see the behavioural test above)."""
+    from pretraining_llm_amd.train import graph as g
     for world in (2, 4, 8):
         ok, why = g.graph_step_policy(cuda=True, world=world, dist_backend="nccl")
         assert not ok and "eager" in why
@@ -231,9 +253,7 @@ def test_trainer_and_bench_share_the_step_policy():
     assert g.graph_step_policy(cuda=True, world=1, dist_backend=None) == (True, None)
     assert not g.graph_step_policy(cuda=True, world=1, dist_backend=None, zero=True)[0]
     assert not g.graph_step_policy(cuda=False, world=1, dist_backend=None)[0]
-    # persistent GEMM grids: world 1 only by default, the same decision in both
-    assert "gemm_persistent_policy(" in inspect.getsource(tr.Trainer.__init__)
-    assert "gemm_persistent_policy(" in inspect.getsource(bench.main)
+    # persistent GEMM grids: world 1 only by default
     assert g.gemm_persistent_policy(1) and g.gemm_persistent_policy(1, "auto")
     for world in (2, 4, 8):
         assert not g.gemm_persistent_policy(world)
