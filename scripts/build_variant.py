@@ -24,10 +24,12 @@ def main():
     B._run([hipcc, *B.COMMON_FLAGS, *B.FILE_FLAGS.get(src_name, []), *flags, "-I", B.CSRC, "-c", src_path,
             "-o", vobj])
     import glob
-    names = [os.path.basename(p) + ".o" for p in sorted(glob.glob(os.path.join(B.CSRC, "*.hip")))] + ["bindings.o"]
+    names = [os.path.basename(p) + ".o" for p in sorted(glob.glob(os.path.join(B.CSRC, "*.hip")))]
+    # every torch-facing translation unit (bindings.cpp, blaslt.cpp, ...), as the normal build links them
+    names += [os.path.splitext(os.path.basename(p))[0] + ".o" for p in sorted(glob.glob(os.path.join(B.CSRC, "*.cpp")))]
     objs = [vobj if n == f"{src_name}.o" else os.path.join(B.BUILD, n) for n in names]
     B._run([hipcc, "-shared", f"--offload-arch={B.ARCH}", *objs, "-o", out, f"-L{lib}", "-lc10", "-lc10_hip", "-ltorch",
-            "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{lib}"])
+            "-ltorch_cpu", "-ltorch_hip", "-lhipblaslt", f"-Wl,-rpath,{lib}"])
     print(out)
 
 
