@@ -1511,8 +1511,8 @@ static void attn_bwd_rs_r(const AttnBwdArgs& a, hipStream_t st) {
   else attn_bwd_rs_t<D, 2>(a, st);
 }
 
-// key-stationary backward (attn_bwd_ks.hip): delta pre-pass, then per pass of key blocks the main kernel
-// and the ordered slab reduce
+// key-stationary backward (attn_bwd_ks.hip): per pass of key blocks the main kernel (delta formed
+// inside it) and the ordered slab reduce
 template <int D>
 static void attn_bwd_ks_t(AttnBwdArgs a, hipStream_t st) {
   const int64_t nrows = (int64_t)a.B * a.T * a.H;
@@ -1520,7 +1520,7 @@ static void attn_bwd_ks_t(AttnBwdArgs a, hipStream_t st) {
   const int BK = attn_bwd_ks_key_block();
   const int nkb = (a.S + BK - 1) / BK;
   const int red_grid = a.B * a.H * a.nqt;  // one workgroup per 32-query tile
-  if (!a.delta_ready) hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
+  (void)pre_grid;  // delta = rowsum(dO O) is formed inside the key-stationary kernel (no pre-pass)
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {
     a.kb0 = kb0;

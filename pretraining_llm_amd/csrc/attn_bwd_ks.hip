@@ -73,11 +73,13 @@ struct KsCfg {
   static constexpr int CPR = D / 8;          // 16-B chunks per row
   static constexpr int QRP = 512 / D;        // rows per 1-KiB DMA piece
   static constexpr int QNP = BQ / QRP;       // pieces per Q (or dO) tile
-  static constexpr int QPPW = 2 * QNP / NW;  // Q + dO pieces per wave and slice
+  static constexpr int PPI = QNP / NW;       // pieces per image and wave: wave w moves rows [w, w+1) BQ/4
+  static constexpr int QPPW = 3 * PPI;       // Q + dO + O pieces per wave and slice
+  static constexpr int RPW = BQ / NW;        // query rows whose delta = rowsum(dO O) wave w forms
   static constexpr int KPPW = BK / QRP / NW; // K image pieces per wave
   static constexpr int TILE = BQ * D;        // elements of one Q (dO) tile
   static constexpr int SIMG = BK * BQ;       // elements of one dS^T image [keys][BQ]
-  static constexpr int LDS_ELEMS = BK * D + 4 * TILE + 2 * SIMG;  // 128 KiB at D = 64 and 128
+  static constexpr int LDS_ELEMS = BK * D + 6 * TILE + 2 * SIMG;  // 144 KiB at D = 64 and 128
 };
 
 // dS^T image [256 keys][W = BQ queries] of the KS kernel: chunk ch (16 B) of row r at ch ^ f(r).
@@ -108,6 +110,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   uint16_t* const Kl = smem;
   uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
   uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
+  uint16_t* const Obuf = Sl + 2 * SIMG;  // slot s: O tile at Obuf + s TILE (delta rows)
 
   const int BH = a.B * a.Hkv;
   const int id = blockIdx.x;
@@ -141,14 +144,17 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       blds16(ks, (uint32_t)((row * a.k_st + 8 * ch) * 2), lds0 + 1024u * (unsigned)p);
     }
   }
-  // ---- Q / dO DMA of slice it into slot sl; per-lane source offsets: piece pc = w QPPW + k of the
-  // slice's 2 QNP pieces (first QNP: Q, then dO)
+  // ---- Q / dO / O DMA of slice it into slot sl.  Wave w moves the pieces of rows [w RPW, (w+1) RPW) of
+  // all three tiles (k = img PPI + m: image img = Q, dO, O, piece w PPI + m), so the rows whose delta =
+  // rowsum(dO O) it forms have landed in ITS view after its own vmcnt wait -- no barrier between the DMA
+  // and the delta, and no separate pre-pass kernel over dO and O (verdict r4 item 1b)
   uint32_t qvo[QPPW];
 #pragma unroll
   for (int k = 0; k < QPPW; ++k) {
-    const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;
+    const int img = k / C::PPI, blk = w * C::PPI + k % C::PPI;
     const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
-    qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
+    const int64_t st = img == 0 ? a.q_st : img == 1 ? a.do_st : a.o_st;
+    qvo[k] = (uint32_t)((row * st + 8 * ch) * 2);
   }
   auto slice_of = [&](int it, int& h, int& q0) {
     h = hk * G + it / per_head;
@@ -162,29 +168,50 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
                              (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
     const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
                              (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
+    const i32x4v ors = srd_of(a.o + b * a.o_sb + (int64_t)h * a.o_sh + (int64_t)q0 * a.o_st,
+                              (uint32_t)(((int64_t)(rows - 1) * a.o_st + D) * 2));
 #pragma unroll
     for (int k = 0; k < QPPW; ++k) {
-      const int pc = w * QPPW + k, img = pc / QNP, blk = pc % QNP;  // wave-uniform
-      blds16(img == 0 ? qs : os, qvo[k], lds0 + 2u * (unsigned)(BK * D + 2 * sl * TILE + img * TILE) + 1024u * blk);
+      const int img = k / C::PPI, blk = w * C::PPI + k % C::PPI;  // wave-uniform
+      const unsigned dst = img < 2 ? (unsigned)(BK * D + 2 * sl * TILE + img * TILE)
+                                   : (unsigned)(BK * D + 4 * TILE + 2 * SIMG + sl * TILE);
+      blds16(img == 0 ? qs : img == 1 ? os : ors, qvo[k], lds0 + 2u * dst + 1024u * blk);
     }
   };
-  // row constants of slice it (threads < 2 BQ: -lse log2 e for rows [0, BQ), -delta after)
+  // -delta of this wave's RPW rows of the slice in slot sl (its own DMA pieces, landed): D / 16 lanes per
+  // row, 16 products each, summed across those lanes; rows past T hold zeros (descriptor range)
+  auto delta_rows = [&](int sl) {
+    constexpr int LPR = D / 16;
+    const int row = C::RPW * w + lane / LPR, seg = lane % LPR;
+    const uint16_t* Ob = Obuf + sl * TILE;
+    const uint16_t* Db = QOl + 2 * sl * TILE + TILE;
+    float x[8], y[8], acc = 0.f;
+#pragma unroll
+    for (int hlf = 0; hlf < 2; ++hlf) {
+      const int off_e = I::off(row, 16 * seg + 8 * hlf);
+      unpack8(ld16(Db + off_e), x);
+      unpack8(ld16(Ob + off_e), y);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc = __builtin_fmaf(x[e], y[e], acc);
+    }
+#pragma unroll
+    for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
+    if (seg == 0) rowc[sl][BQ + row] = -acc;
+  };
+  // row constants of slice it: -lse log2 e for rows [0, BQ) by threads < BQ (-delta: delta_rows)
   float rc = 0.f;
   auto rload = [&](int it) {
-    if (tid < 2 * BQ) {
+    if (tid < BQ) {
       int h, q0;
       slice_of(it, h, q0);
-      const float* base = tid < BQ ? a.lse : a.delta;
-      const int q = min(q0 + (tid & (BQ - 1)), a.T - 1);
-      rc = base[((int64_t)b * a.H + h) * a.T + q];
+      rc = a.lse[((int64_t)b * a.H + h) * a.T + min(q0 + tid, a.T - 1)];
     }
   };
   auto rstore = [&](int it) {
-    if (tid < 2 * BQ) {
+    if (tid < BQ) {
       int h, q0;
       slice_of(it, h, q0);
-      const bool live = q0 + (tid & (BQ - 1)) < a.T;
-      rowc[it & 1][tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
+      rowc[it & 1][tid] = q0 + tid < a.T ? -rc * kLog2e : 0.f;
     }
   };
 
@@ -205,6 +232,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   vm_wait_all();
   if (total > 0) {
     rstore(0);
+    delta_rows(0);
     if (total > 1) rload(1);
   }
   __syncthreads();  // K image, slice 0 (and its row constants) landed for every wave
@@ -432,7 +460,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     KS_STAMP(3);
     // ---- hand-off: this slice's dS^T image and the next slice's Q / dO / row constants
     vm_wait_all();  // own DMA pieces of slice it + 1, its row constants, this wave's previous dQ stores
-    if (it + 1 < total) rstore(it + 1);
+    if (it + 1 < total) {
+      rstore(it + 1);
+      delta_rows(sl ^ 1);
+    }
     __syncthreads();
     if (it + 2 < total) {
       qdma(it + 2, sl);  // every wave is past its reads of slot sl (slice it)
