@@ -1082,7 +1082,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
 
   constexpr int QPAIR = (BQ * CPR2 + NT - 1) / NT;
   u32x4 qr[2 * QPAIR], dor[2 * QPAIR];
-  float rc = 0.f, rc2 = 0.f;
+  float rc = 0.f;
   auto gload = [&](int it) {
     const int h = hk * G + it / per_head;
     const int q0 = (qb_start + it % per_head) * BQ;
@@ -1105,11 +1105,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
       const bool isl = __builtin_amdgcn_readfirstlane(tid >> 6) < BQ / 64;
       const float* base = isl ? a.lse : a.delta;
       const int q = min(q0 + (tid & (BQ - 1)), a.T - 1);
-      // delta_split: the two 64-column halves of the head (gemm_tn epilogue 6 at D = 128), both
-      // loaded unconditionally and added at the LDS write (a use here would wait out the prefetch)
-      const int64_t i0 = a.delta_split == 2 && !isl ? ((int64_t)b * a.H + h) * 2 * a.T + q : ((int64_t)b * a.H + h) * a.T + q;
-      rc = base[i0];
-      rc2 = base[a.delta_split == 2 && !isl ? i0 + a.T : i0];
+      rc = base[((int64_t)b * a.H + h) * a.T + q];
     }
   };
 
@@ -1163,8 +1159,7 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_rs_kernel(AttnBwdArgs a) {
     }
     if (tid < 2 * BQ) {
       const bool live = q0 + (tid & (BQ - 1)) < a.T;
-      const float dsum = a.delta_split == 2 ? rc + rc2 : rc;
-      rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : dsum) : 0.f;  // -lse*log2(e), delta
+      rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : rc) : 0.f;  // -lse*log2(e), delta
     }
     flush_dq();
     __syncthreads();

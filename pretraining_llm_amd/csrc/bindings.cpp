@@ -945,12 +945,9 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   check_rope(rope_cos, rope_sin, S, D);
   auto f32 = q.options().dtype(at::kFloat);
   // delta_in: rowsum(dO * O) already computed (the output projection's gemm_tn epilogue 6)
-  // (at D = 128 also [B, 2H, T]: epilogue 6 sums per 64 columns, the kernel adds the two halves)
-  const bool dsplit = delta_in && D == 128 && delta_in->numel() == 2 * B * H * T;
   if (delta_in)
-    TORCH_CHECK(delta_in->scalar_type() == at::kFloat && delta_in->is_contiguous() &&
-                    (delta_in->numel() == B * H * T || dsplit),
-                "attn_bwd: delta [B, H, T] fp32 (D = 128: or [B, 2H, T] halves)");
+    TORCH_CHECK(delta_in->scalar_type() == at::kFloat && delta_in->is_contiguous() && delta_in->numel() == B * H * T,
+                "attn_bwd: delta [B, H, T] fp32");
   Tensor delta = delta_in ? *delta_in : at::empty({B, H, T}, f32);
   // per-key-block bf16 dQ partial slabs (attention.hip: plain stores + ordered fp32 reduce, no
   // atomics), run in passes of at most `per` key blocks: the workspace is bounded by
@@ -1018,7 +1015,6 @@ void attn_bwd(const Tensor& dout, const Tensor& q, const Tensor& k, const Tensor
   a.scale_log2 = (float)(scale * 1.4426950408889634);
   a.causal = causal ? 1 : 0;
   a.delta_ready = delta_in ? 1 : 0;
-  a.delta_split = dsplit ? 2 : 1;
   static const bool bstamps = std::getenv("PLLM_BWD_STAMPS") != nullptr;
   Tensor bst;
   if (bstamps) {  // diagnostic, with a PLLM_BWD_STAMPS=1 build of attention.hip / attn_bwd_ks.hip

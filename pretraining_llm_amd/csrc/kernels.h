@@ -51,7 +51,6 @@ struct AttnBwdArgs {
   int causal;
   unsigned long long* stamps;  // diagnostic builds only (PLLM_BWD_STAMPS): per-wave phase cycles
   int delta_ready;             // 1: delta already holds rowsum(dO * O) (gemm_tn epilogue 6): no pre-pass
-  int delta_split;             // 2: delta is [B, 2H, T], two 64-column partial sums per 128-wide head
 };
 
 namespace pllm {

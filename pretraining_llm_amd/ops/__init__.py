@@ -136,23 +136,14 @@ class _LinearFn(torch.autograd.Function):
         # the bias gradient rides along the weight-gradient GEMM when both go into flat targets
         btgt = None
         if (ctx.b is not None and ctx.needs_input_grad[2] and not ctx.bias_ext and ctx.needs_input_grad[1]
-                and not WGRAD_STREAM and FUSED_WGRAD_BIAS):
+                and FUSED_WGRAD_BIAS):
             btgt = _acc_target(ctx.b)
         if ctx.needs_input_grad[1]:
             x2 = x.reshape(-1, x.shape[-1])
             tgt, fresh = _set_target(ctx.w)
             if tgt is None:
                 btgt = None
-            if WGRAD_STREAM and tgt is not None and dy2.is_cuda:
-                main, side = torch.cuda.current_stream(), _side_stream(dy2.device)
-                side.wait_stream(main)
-                with torch.cuda.stream(side):
-                    _weight_grad(dy2, x2, tgt, overwrite=fresh)
-                dy2.record_stream(side)
-                x2.record_stream(side)
-                dw = None
-            else:
-                dw = _weight_grad(dy2, x2, tgt, btgt, overwrite=fresh)
+            dw = _weight_grad(dy2, x2, tgt, btgt, overwrite=fresh)
             if tgt is not None:
                 _notify(ctx.w)
         if btgt is not None:
@@ -181,36 +172,18 @@ WGRAD_ENGINE = _os.environ.get("PLLM_WGRAD", "hip")
 WGRAD_BLAS_SHAPES = {(16384, 6144, 2048), (16384, 2048, 5504), (16384, 50304, 2048)}
 
 
-# Weight gradients on a side HIP stream (opt-in: PLLM_WGRAD_STREAM=1): a layer's dW GEMM has
-# no consumer until the optimizer / gradient all-reduce, so it can run beside the next layer's
-# data-gradient work and fill the tails of its grids.  Every reader of the flat gradient
-# (bucket all-reduce, clipping, AdamW) and every other writer of a weight's gradient (the tied
-# embedding's scatter) first joins the side stream (``sync_side_streams``).  Measured on
-# MI355X: +1.5 % on one box, -0.8 % on another, and sporadic 2.5-3x slower runs on back-to-back
-# processes (never seen with it off), so it stays off by default.
-WGRAD_STREAM = _os.environ.get("PLLM_WGRAD_STREAM", "0") == "1"
+# (Weight gradients on a side HIP stream were measured and removed: +1.5 % on one box, -0.8 % on
+# another, sporadic 2.5-3x slower runs; profiles/r1_wgrad_side_stream_ab.txt.)
 # A linear layer's bias gradient computed inside its weight-gradient GEMM (csrc/gemm_wgrad.hip: MFMAs
 # against an all-ones operand by the first Q-tile's workgroups) instead of a separate column-sum pass
 # over dy (the GPT-2 QKV projection); PLLM_WGRAD_BIAS=0 for the separate pass
 FUSED_WGRAD_BIAS = _os.environ.get("PLLM_WGRAD_BIAS", "1") == "1"
-_SIDE_STREAMS = {}
-
-
-def _side_stream(dev):
-    s = _SIDE_STREAMS.get(dev.index)
-    if s is None:
-        s = torch.cuda.Stream(dev)
-        _SIDE_STREAMS[dev.index] = s
-    return s
 
 
 def sync_side_streams():
-    """Make the current stream wait for all weight-gradient work queued on side streams."""
-    if _SIDE_STREAMS:
-        cur = torch.cuda.current_stream()
-        for s in _SIDE_STREAMS.values():
-            if s.device == cur.device:
-                cur.wait_stream(s)
+    """No-op kept for the gradient readers that call it (every weight gradient now runs on the
+    current stream)."""
+    return None
 
 
 def _dgrad(dy, weight):
@@ -769,16 +742,14 @@ class _AttnProjFn(torch.autograd.Function):
 
 # PLLM_ATTN_PROJ_FUSED=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
 FUSED_ATTN_PROJ = os.environ.get("PLLM_ATTN_PROJ_FUSED", "1") == "1"
-# head dims served by it; PLLM_ATTN_PROJ_D128=1 adds D = 128 (llama: two 64-column delta halves per
-# head, added by the role-split backward).  Off by default: llama-1.3B 274.4 vs 273.0 ms per step
-# (profiles/r4_attn_experiments.md) -- the ping-pong projection dgrad is slower than hipBLASLt's by
-# about what the delta pre-pass costs
-ATTN_PROJ_HEAD_DIMS = (64, 128) if os.environ.get("PLLM_ATTN_PROJ_D128", "0") == "1" else (64,)
+# head dims served by it: 64.  (D = 128 -- two 64-column delta halves per head -- measured 0.5 % slower on
+# llama-1.3B, profiles/r4_attn_experiments.md, and was removed: the D = 128 backward, csrc/attn_bwd_ks.hip,
+# forms delta itself)
+ATTN_PROJ_HEAD_DIMS = (64,)
 
 
 def attn_proj_ok(qkv, n_head: int, n_kv_head: int, w, b) -> bool:
-    """The fused attention + output projection path (_AttnProjFn): HIP training path, head dim 64 or
-    128 (128: epilogue 6's per-64-column delta halves, added by the role-split backward)."""
+    """The fused attention + output projection path (_AttnProjFn): HIP training path, head dim 64."""
     if not FUSED_ATTN_PROJ or not torch.is_grad_enabled() or not (_hip_op("attn", qkv) and _hip_op("linear", qkv)):
         return False
     B, T, W = qkv.shape
