@@ -13,6 +13,10 @@
 // result as an operand so every consumer is ordered after it) precedes any non-MFMA reader.
 #include <type_traits>
 
+#ifndef PLLM_KS_DELTA
+#define PLLM_KS_DELTA 1  // 1: delta = rowsum(dO O) formed in the kernel; 0: attn_bwd_pre_kernel pass (A/B)
+#endif
+constexpr bool kKsDelta = PLLM_KS_DELTA != 0;
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums (scripts/build_variant.py -DPLLM_BWD_STAMPS=1)
 #endif
@@ -74,7 +78,7 @@ struct KsCfg {
   static constexpr int QRP = 512 / D;        // rows per 1-KiB DMA piece
   static constexpr int QNP = BQ / QRP;       // pieces per Q (or dO) tile
   static constexpr int PPI = QNP / NW;       // pieces per image and wave: wave w moves rows [w, w+1) BQ/4
-  static constexpr int QPPW = 3 * PPI;       // Q + dO + O pieces per wave and slice
+  static constexpr int QPPW = (kKsDelta ? 3 : 2) * PPI;  // Q + dO (+ O) pieces per wave and slice
   static constexpr int RPW = BQ / NW;        // query rows whose delta = rowsum(dO O) wave w forms
   static constexpr int KPPW = BK / QRP / NW; // K image pieces per wave
   static constexpr int TILE = BQ * D;        // elements of one Q (dO) tile
@@ -106,7 +110,10 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   constexpr int BK = C::BK, BQ = C::BQ, NQB = C::NQB, NKS = C::NKS, NDB = C::NDB, CPR = C::CPR;
   constexpr int TILE = C::TILE, SIMG = C::SIMG, QRP = C::QRP, QNP = C::QNP, QPPW = C::QPPW;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[C::LDS_ELEMS];
-  __shared__ __attribute__((aligned(16))) float rowc[2][2 * BQ];  // per slot: -lse log2(e), -delta
+  // row constants per slot: raw lse of the slice's rows (LDS-DMA'd, 64 lanes x 4 B: padded to 64) and
+  // delta (in-kernel: -delta written by delta_rows; pre-pass build: +delta DMA'd like lse)
+  __shared__ __attribute__((aligned(16))) float lsec[2][64];
+  __shared__ __attribute__((aligned(16))) float rowc[2][BQ < 64 ? 64 : BQ];
   uint16_t* const Kl = smem;
   uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
   uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
@@ -181,6 +188,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   // -delta of this wave's RPW rows of the slice in slot sl (its own DMA pieces, landed): D / 16 lanes per
   // row, 16 products each, summed across those lanes; rows past T hold zeros (descriptor range)
   auto delta_rows = [&](int sl) {
+    if constexpr (!kKsDelta) return;
     constexpr int LPR = D / 16;
     const int row = C::RPW * w + lane / LPR, seg = lane % LPR;
     const uint16_t* Ob = Obuf + sl * TILE;
@@ -196,22 +204,21 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     }
 #pragma unroll
     for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    if (seg == 0) rowc[sl][BQ + row] = -acc;
+    if (seg == 0) rowc[sl][row] = -acc;
   };
-  // row constants of slice it: -lse log2 e for rows [0, BQ) by threads < BQ (-delta: delta_rows)
-  float rc = 0.f;
+  // row constants of slice it by LDS DMA (buffer_load_dword ... lds, one wave each, lane l -> row q0 + l;
+  // rows past T read zeros): no register round trip, so no compiler-inserted vmcnt(0) in front of a
+  // register use (it waited out the previous slice's dQ stores too)
   auto rload = [&](int it) {
-    if (tid < BQ) {
-      int h, q0;
-      slice_of(it, h, q0);
-      rc = a.lse[((int64_t)b * a.H + h) * a.T + min(q0 + tid, a.T - 1)];
-    }
-  };
-  auto rstore = [&](int it) {
-    if (tid < BQ) {
-      int h, q0;
-      slice_of(it, h, q0);
-      rowc[it & 1][tid] = q0 + tid < a.T ? -rc * kLog2e : 0.f;
+    int h, q0;
+    slice_of(it, h, q0);
+    const int64_t row0 = ((int64_t)b * a.H + h) * a.T + q0;
+    if (w == 0) {
+      const i32x4v srd = srd_of(a.lse + row0, (uint32_t)(a.T - q0) * 4u);
+      blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&lsec[it & 1][0]);
+    } else if (!kKsDelta && w == 1) {
+      const i32x4v srd = srd_of(a.delta + row0, (uint32_t)(a.T - q0) * 4u);
+      blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&rowc[it & 1][0]);
     }
   };
 
@@ -226,15 +233,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   }
   if (total > 0) {
     qdma(0, 0);
-    if (total > 1) qdma(1, 1);
     rload(0);
+    if (total > 1) {
+      qdma(1, 1);
+      rload(1);  // before the wait below: the first hand-off's vmcnt(2) has no dQ stores to skip
+    }
   }
   vm_wait_all();
-  if (total > 0) {
-    rstore(0);
-    delta_rows(0);
-    if (total > 1) rload(1);
-  }
+  if (total > 0) delta_rows(0);
   __syncthreads();  // K image, slice 0 (and its row constants) landed for every wave
 
   f32x16 dk[2][NDB], dv[2][NDB];
@@ -283,6 +289,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     const uint16_t* Ql = QOl + 2 * sl * TILE;
     const uint16_t* Ol = Ql + TILE;
     const float* rl = rowc[sl];
+    const float* ll = lsec[sl];
     uint16_t* Sd = Sl + sl * SIMG;
 #pragma unroll
     for (int j = 0; j < NQB; ++j) {
@@ -322,12 +329,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       float rs[16];  // -lse log2(e) of the lane's 16 query rows
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(&rl[BQ + 32 * j + 8 * g + 4 * hh]);
+        const f32x4 x = *reinterpret_cast<const f32x4*>(&ll[32 * j + 8 * g + 4 * hh]);
+        const f32x4 y = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          rs[4 * g + e] = x[e];
-          d0[4 * g + e] = y[e];  // dP accumulated onto -delta
+          rs[4 * g + e] = -kLog2e * x[e];
+          d0[4 * g + e] = kKsDelta ? y[e] : -y[e];  // dP accumulated onto -delta
         }
       }
       d1 = d0;
@@ -459,11 +466,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     }
     KS_STAMP(3);
     // ---- hand-off: this slice's dS^T image and the next slice's Q / dO / row constants
-    vm_wait_all();  // own DMA pieces of slice it + 1, its row constants, this wave's previous dQ stores
-    if (it + 1 < total) {
-      rstore(it + 1);
-      delta_rows(sl ^ 1);
-    }
+    // own DMA pieces of slice it + 1 and its row constants, issued right after the previous barrier; the
+    // 2 dQ slab stores issued after them (the previous slice's dQ task) may stay in flight (counted wait:
+    // vmcnt(0) here waited out their write latency, p4 ~1.8k cycles of ~7k per slice)
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    if (it + 1 < total) delta_rows(sl ^ 1);
     __syncthreads();
     if (it + 2 < total) {
       qdma(it + 2, sl);  // every wave is past its reads of slot sl (slice it)
@@ -471,8 +478,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     }
     KS_STAMP(4);
     // ---- dQ partial of this key block: dQ^T tile (32 dims x 32 queries) = K^T dS^T over 256 keys
+    // (no branch on a ragged last slice: its tiles past T read zero dS^T columns, and their two stores
+    // go out of the descriptor's range -- dropped -- so every wave issues exactly 2 stores per slice,
+    // which the counted vmcnt(2) of the hand-off relies on)
     const int qt0 = q0 + 32 * tq_blk;
-    if (qt0 < a.T) {
+    {
       f32x16 acc;
       constexpr int QA = 3;  // transposed reads QA steps ahead of the MFMA chain
       bf16x8 fa[QA + 1], fb[QA + 1];
@@ -496,10 +506,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         lo[e] = acc[e];
         hi[e] = acc[8 + e];
       }
-      uint16_t* dqp = a.dq_acc + (kb - a.kb0) * a.slab +
-                      ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
-      st16(dqp, pack8(lo));
-      st16(dqp + 8, pack8(hi));
+      // this (key block, batch, head)'s slab tiles: nqt x NDB fragment blocks of 1024 bf16
+      const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.dq_acc + (kb - a.kb0) * a.slab + ((int64_t)b * a.H + h) * a.nqt * NDB * 1024), (short)0,
+          a.nqt * NDB * 2048, 0x00020000);
+      const uint32_t doff = qt0 < a.T ? (uint32_t)(((qt0 >> 5) * NDB + tdb) * 2048 + lane * 32) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(pack8(lo), drs, doff, 0, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(pack8(hi), drs, doff + 16u, 0, 0);
     }
     KS_STAMP(5);
 #if PLLM_BWD_STAMPS
@@ -551,6 +564,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
 namespace pllm {
 
 int attn_bwd_ks_key_block() { return KsCfg<128>::BK; }
+bool attn_bwd_ks_needs_delta() { return !kKsDelta; }
 
 // one pass of key blocks [a.kb0, a.kb0 + a.nkb_pass) (the caller runs the delta pre-pass before and the
 // slab reduce after)

@@ -214,6 +214,12 @@ PLLM_DEV void blds16(const i32x4v& srd, uint32_t voff, unsigned lds_byte) {
                "s"(__builtin_amdgcn_readfirstlane(lds_byte))
                : "memory", "m0");
 }
+// ... 4 B per lane into [m0 + 4 * lane] (buffer_load_dword ... lds), e.g. a row of 64 fp32 statistics
+PLLM_DEV void blds4(const i32x4v& srd, uint32_t voff, unsigned lds_byte) {
+  asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dword %0, %1, 0 offen lds" ::"v"(voff), "s"(srd),
+               "s"(__builtin_amdgcn_readfirstlane(lds_byte))
+               : "memory", "m0");
+}
 #define PLLM_CHECK_LAUNCH() (void)hipGetLastError()
 
 // Debug builds (python -m pretraining_llm_amd.build --debug): report a violated device-side
