@@ -111,9 +111,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   constexpr int TILE = C::TILE, SIMG = C::SIMG, QRP = C::QRP, QNP = C::QNP, QPPW = C::QPPW;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[C::LDS_ELEMS];
   // row constants per slot: raw lse of the slice's rows (LDS-DMA'd, 64 lanes x 4 B: padded to 64) and
-  // delta (in-kernel: -delta written by delta_rows; pre-pass build: +delta DMA'd like lse)
+  // delta (pre-pass build: +delta DMA'd like lse; in-kernel: pdel below)
   __shared__ __attribute__((aligned(16))) float lsec[2][64];
-  __shared__ __attribute__((aligned(16))) float rowc[2][BQ < 64 ? 64 : BQ];
+  __shared__ __attribute__((aligned(16))) float rowc[kKsDelta ? 1 : 2][64];
+  // in-kernel delta: each wave forms -delta of ALL the slice's rows itself into its own area (no
+  // cross-wave hand-off, so no barrier between the dO / O DMA and the dP init that needs it)
+  __shared__ __attribute__((aligned(16))) float pdel[kKsDelta ? 4 : 1][2][64];
   uint16_t* const Kl = smem;
   uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
   uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
@@ -185,27 +188,33 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       blds16(img == 0 ? qs : img == 1 ? os : ors, qvo[k], lds0 + 2u * dst + 1024u * blk);
     }
   };
-  // -delta of this wave's RPW rows of the slice in slot sl (its own DMA pieces, landed): D / 16 lanes per
-  // row, 16 products each, summed across those lanes; rows past T hold zeros (descriptor range)
-  auto delta_rows = [&](int sl) {
-    if constexpr (!kKsDelta) return;
-    constexpr int LPR = D / 16;
-    const int row = C::RPW * w + lane / LPR, seg = lane % LPR;
-    const uint16_t* Ob = Obuf + sl * TILE;
+  // -delta of every row of the slice in slot sl into this wave's pdel[w][sl]: 64 / BQ lanes per row, D BQ / 64
+  // = 64 products per lane as 32 v_dot2c_f32_bf16 on the packed bf16 pairs (no unpacking), split in
+  // a load half (dv / ov: 8 + 8 fragments) and a dot half so the loads can fly under the dQ MFMAs
+  constexpr int DLPR = 64 / BQ, DEPL = D / DLPR;  // lanes per row, elements per lane (64)
+  auto delta_load = [&](int sl, u32x4 (&dv)[8], u32x4 (&ov)[8]) {
+    const int row = lane / DLPR, d0 = (lane % DLPR) * DEPL;
     const uint16_t* Db = QOl + 2 * sl * TILE + TILE;
-    float x[8], y[8], acc = 0.f;
+    const uint16_t* Ob = Obuf + sl * TILE;
 #pragma unroll
-    for (int hlf = 0; hlf < 2; ++hlf) {
-      const int off_e = I::off(row, 16 * seg + 8 * hlf);
-      unpack8(ld16(Db + off_e), x);
-      unpack8(ld16(Ob + off_e), y);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc = __builtin_fmaf(x[e], y[e], acc);
+    for (int c = 0; c < 8; ++c) {
+      const int e = I::off(row, d0 + 8 * c);
+      dv[c] = ld16(Db + e);
+      ov[c] = ld16(Ob + e);
     }
-#pragma unroll
-    for (int o = 1; o < LPR; o <<= 1) acc += __shfl_xor(acc, o, 64);
-    if (seg == 0) rowc[sl][row] = -acc;
   };
+  auto delta_dot = [&](const u32x4& x, const u32x4& y, float acc) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, x[k]), __builtin_bit_cast(bf16x2, y[k]), acc,
+                                            false);
+    return acc;
+  };
+  auto delta_store = [&](int sl, float acc) {
+    if constexpr (DLPR == 2) acc += __shfl_xor(acc, 1, 64);
+    if (lane % DLPR == 0) pdel[w][sl][lane / DLPR] = -acc;
+  };
+
   // row constants of slice it by LDS DMA (buffer_load_dword ... lds, one wave each, lane l -> row q0 + l;
   // rows past T read zeros): no register round trip, so no compiler-inserted vmcnt(0) in front of a
   // register use (it waited out the previous slice's dQ stores too)
@@ -240,8 +249,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     }
   }
   vm_wait_all();
-  if (total > 0) delta_rows(0);
   __syncthreads();  // K image, slice 0 (and its row constants) landed for every wave
+  if (kKsDelta && total > 0) {
+    u32x4 dv[8], ov[8];
+    delta_load(0, dv, ov);
+    float acc = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc = delta_dot(dv[c], ov[c], acc);
+    delta_store(0, acc);
+  }
 
   f32x16 dk[2][NDB], dv[2][NDB];
 #pragma unroll
@@ -288,7 +304,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     asm volatile("" : "+v"(fq), "+v"(ft0), "+v"(ft8), "+v"(sa0), "+v"(sa4), "+v"(ka0), "+v"(ka4));
     const uint16_t* Ql = QOl + 2 * sl * TILE;
     const uint16_t* Ol = Ql + TILE;
-    const float* rl = rowc[sl];
+    const float* rl = kKsDelta ? pdel[w][sl] : rowc[sl];
     const float* ll = lsec[sl];
     uint16_t* Sd = Sl + sl * SIMG;
 #pragma unroll
@@ -470,7 +486,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     // 2 dQ slab stores issued after them (the previous slice's dQ task) may stay in flight (counted wait:
     // vmcnt(0) here waited out their write latency, p4 ~1.8k cycles of ~7k per slice)
     asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    if (it + 1 < total) delta_rows(sl ^ 1);
     __syncthreads();
     if (it + 2 < total) {
       qdma(it + 2, sl);  // every wave is past its reads of slot sl (slice it)
@@ -484,6 +499,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     const int qt0 = q0 + 32 * tq_blk;
     {
       f32x16 acc;
+      // the next slice's -delta (its dO / O landed before the barrier): loads first, dots beside the
+      // MFMAs (branch-free: after the last slice the stale slot is computed and never read)
+      u32x4 dlv[8], olv[8];
+      float dacc = 0.f;
+      if constexpr (kKsDelta) delta_load(sl ^ 1, dlv, olv);
       constexpr int QA = 3;  // transposed reads QA steps ahead of the MFMA chain
       bf16x8 fa[QA + 1], fb[QA + 1];
       auto rd_q = [&](int ks) {
@@ -497,8 +517,12 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         if (ks + QA < BK / 16) rd_q(ks + QA);
         if (ks == 0) mfma_v0(acc, fb[0], fa[0]);
         else mfma_v(acc, fb[ks % (QA + 1)], fa[ks % (QA + 1)]);
+        if constexpr (kKsDelta) {
+          if (ks >= 4 && ks < 12) dacc = delta_dot(dlv[ks - 4], olv[ks - 4], dacc);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+      if constexpr (kKsDelta) delta_store(sl ^ 1, dacc);
       mfma_settle(acc);
       float lo[8], hi[8];
 #pragma unroll

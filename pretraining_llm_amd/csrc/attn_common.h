@@ -7,6 +7,7 @@
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 PLLM_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
