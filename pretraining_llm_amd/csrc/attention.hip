@@ -1515,8 +1515,8 @@ static void attn_bwd_ks_t(AttnBwdArgs a, hipStream_t st) {
   const int BK = attn_bwd_ks_key_block();
   const int nkb = (a.S + BK - 1) / BK;
   const int red_grid = a.B * a.H * a.nqt;  // one workgroup per 32-query tile
-  // delta = rowsum(dO O) is formed inside the key-stationary kernel unless it was built without
-  if (attn_bwd_ks_needs_delta() && !a.delta_ready)
+  // delta = rowsum(dO O) pre-pass (skipped when the caller already holds it)
+  if (!a.delta_ready)
     hipLaunchKernelGGL(attn_bwd_pre_kernel<D>, dim3(pre_grid), dim3(256), 0, st, a);
   const int per = a.nkb_pass;
   for (int kb0 = 0; kb0 < nkb; kb0 += per) {

@@ -13,10 +13,6 @@
 // result as an operand so every consumer is ordered after it) precedes any non-MFMA reader.
 #include <type_traits>
 
-#ifndef PLLM_KS_DELTA
-#define PLLM_KS_DELTA 1  // 1: delta = rowsum(dO O) formed in the kernel; 0: attn_bwd_pre_kernel pass (A/B)
-#endif
-constexpr bool kKsDelta = PLLM_KS_DELTA != 0;
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums (scripts/build_variant.py -DPLLM_BWD_STAMPS=1)
 #endif
@@ -78,12 +74,11 @@ struct KsCfg {
   static constexpr int QRP = 512 / D;        // rows per 1-KiB DMA piece
   static constexpr int QNP = BQ / QRP;       // pieces per Q (or dO) tile
   static constexpr int PPI = QNP / NW;       // pieces per image and wave: wave w moves rows [w, w+1) BQ/4
-  static constexpr int QPPW = (kKsDelta ? 3 : 2) * PPI;  // Q + dO (+ O) pieces per wave and slice
-  static constexpr int RPW = BQ / NW;        // query rows whose delta = rowsum(dO O) wave w forms
+  static constexpr int QPPW = 2 * PPI;      // Q + dO pieces per wave and slice
   static constexpr int KPPW = BK / QRP / NW; // K image pieces per wave
   static constexpr int TILE = BQ * D;        // elements of one Q (dO) tile
   static constexpr int SIMG = BK * BQ;       // elements of one dS^T image [keys][BQ]
-  static constexpr int LDS_ELEMS = BK * D + 6 * TILE + 2 * SIMG;  // 144 KiB at D = 64 and 128
+  static constexpr int LDS_ELEMS = BK * D + 4 * TILE + 2 * SIMG;  // 136 KiB at D = 64 and 128
 };
 
 // dS^T image [256 keys][W = BQ queries] of the KS kernel: chunk ch (16 B) of row r at ch ^ f(r).
@@ -110,17 +105,15 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   constexpr int BK = C::BK, BQ = C::BQ, NQB = C::NQB, NKS = C::NKS, NDB = C::NDB, CPR = C::CPR;
   constexpr int TILE = C::TILE, SIMG = C::SIMG, QRP = C::QRP, QNP = C::QNP, QPPW = C::QPPW;
   __shared__ __attribute__((aligned(1024))) uint16_t smem[C::LDS_ELEMS];
-  // row constants per slot: raw lse of the slice's rows (LDS-DMA'd, 64 lanes x 4 B: padded to 64) and
-  // delta (pre-pass build: +delta DMA'd like lse; in-kernel: pdel below)
+  // row constants per slot, LDS-DMA'd (64 lanes x 4 B: padded to 64): raw lse and delta = rowsum(dO O)
+  // of the slice's rows.  delta comes from attn_bwd_pre_kernel: forming it in this kernel (dO / O rows
+  // DMA'd beside Q / dO, fp32 FMAs beside the dQ MFMAs) measured 1212 us vs 1106 us for pre-pass +
+  // kernel at 16x16x2048x128 (r5 A/B) -- the unpack + FMA VALU work lands on the MFMA-bound phases
   __shared__ __attribute__((aligned(16))) float lsec[2][64];
-  __shared__ __attribute__((aligned(16))) float rowc[kKsDelta ? 1 : 2][64];
-  // in-kernel delta: each wave forms -delta of ALL the slice's rows itself into its own area (no
-  // cross-wave hand-off, so no barrier between the dO / O DMA and the dP init that needs it)
-  __shared__ __attribute__((aligned(16))) float pdel[kKsDelta ? 4 : 1][2][64];
+  __shared__ __attribute__((aligned(16))) float rowc[2][64];
   uint16_t* const Kl = smem;
   uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
   uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
-  uint16_t* const Obuf = Sl + 2 * SIMG;  // slot s: O tile at Obuf + s TILE (delta rows)
 
   const int BH = a.B * a.Hkv;
   const int id = blockIdx.x;
@@ -154,16 +147,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       blds16(ks, (uint32_t)((row * a.k_st + 8 * ch) * 2), lds0 + 1024u * (unsigned)p);
     }
   }
-  // ---- Q / dO / O DMA of slice it into slot sl.  Wave w moves the pieces of rows [w RPW, (w+1) RPW) of
-  // all three tiles (k = img PPI + m: image img = Q, dO, O, piece w PPI + m), so the rows whose delta =
-  // rowsum(dO O) it forms have landed in ITS view after its own vmcnt wait -- no barrier between the DMA
-  // and the delta, and no separate pre-pass kernel over dO and O (verdict r4 item 1b)
+  // ---- Q / dO DMA of slice it into slot sl (k = img PPI + m: image img = Q, dO, piece w PPI + m)
   uint32_t qvo[QPPW];
 #pragma unroll
   for (int k = 0; k < QPPW; ++k) {
     const int img = k / C::PPI, blk = w * C::PPI + k % C::PPI;
     const int row = blk * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
-    const int64_t st = img == 0 ? a.q_st : img == 1 ? a.do_st : a.o_st;
+    const int64_t st = img == 0 ? a.q_st : a.do_st;
     qvo[k] = (uint32_t)((row * st + 8 * ch) * 2);
   }
   auto slice_of = [&](int it, int& h, int& q0) {
@@ -178,43 +168,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
                              (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
     const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
                              (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
-    const i32x4v ors = srd_of(a.o + b * a.o_sb + (int64_t)h * a.o_sh + (int64_t)q0 * a.o_st,
-                              (uint32_t)(((int64_t)(rows - 1) * a.o_st + D) * 2));
 #pragma unroll
     for (int k = 0; k < QPPW; ++k) {
       const int img = k / C::PPI, blk = w * C::PPI + k % C::PPI;  // wave-uniform
-      const unsigned dst = img < 2 ? (unsigned)(BK * D + 2 * sl * TILE + img * TILE)
-                                   : (unsigned)(BK * D + 4 * TILE + 2 * SIMG + sl * TILE);
-      blds16(img == 0 ? qs : img == 1 ? os : ors, qvo[k], lds0 + 2u * dst + 1024u * blk);
+      const unsigned dst = (unsigned)(BK * D + 2 * sl * TILE + img * TILE);
+      blds16(img == 0 ? qs : os, qvo[k], lds0 + 2u * dst + 1024u * blk);
     }
   };
-  // -delta of every row of the slice in slot sl into this wave's pdel[w][sl]: 64 / BQ lanes per row, D BQ / 64
-  // = 64 products per lane as 32 v_dot2c_f32_bf16 on the packed bf16 pairs (no unpacking), split in
-  // a load half (dv / ov: 8 + 8 fragments) and a dot half so the loads can fly under the dQ MFMAs
-  constexpr int DLPR = 64 / BQ, DEPL = D / DLPR;  // lanes per row, elements per lane (64)
-  auto delta_load = [&](int sl, u32x4 (&dv)[8], u32x4 (&ov)[8]) {
-    const int row = lane / DLPR, d0 = (lane % DLPR) * DEPL;
-    const uint16_t* Db = QOl + 2 * sl * TILE + TILE;
-    const uint16_t* Ob = Obuf + sl * TILE;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      const int e = I::off(row, d0 + 8 * c);
-      dv[c] = ld16(Db + e);
-      ov[c] = ld16(Ob + e);
-    }
-  };
-  auto delta_dot = [&](const u32x4& x, const u32x4& y, float acc) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      acc = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2, x[k]), __builtin_bit_cast(bf16x2, y[k]), acc,
-                                            false);
-    return acc;
-  };
-  auto delta_store = [&](int sl, float acc) {
-    if constexpr (DLPR == 2) acc += __shfl_xor(acc, 1, 64);
-    if (lane % DLPR == 0) pdel[w][sl][lane / DLPR] = -acc;
-  };
-
   // row constants of slice it by LDS DMA (buffer_load_dword ... lds, one wave each, lane l -> row q0 + l;
   // rows past T read zeros): no register round trip, so no compiler-inserted vmcnt(0) in front of a
   // register use (it waited out the previous slice's dQ stores too)
@@ -225,7 +185,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     if (w == 0) {
       const i32x4v srd = srd_of(a.lse + row0, (uint32_t)(a.T - q0) * 4u);
       blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&lsec[it & 1][0]);
-    } else if (!kKsDelta && w == 1) {
+    } else if (w == 1) {
       const i32x4v srd = srd_of(a.delta + row0, (uint32_t)(a.T - q0) * 4u);
       blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&rowc[it & 1][0]);
     }
@@ -250,14 +210,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   }
   vm_wait_all();
   __syncthreads();  // K image, slice 0 (and its row constants) landed for every wave
-  if (kKsDelta && total > 0) {
-    u32x4 dv[8], ov[8];
-    delta_load(0, dv, ov);
-    float acc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) acc = delta_dot(dv[c], ov[c], acc);
-    delta_store(0, acc);
-  }
 
   f32x16 dk[2][NDB], dv[2][NDB];
 #pragma unroll
@@ -304,7 +256,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     asm volatile("" : "+v"(fq), "+v"(ft0), "+v"(ft8), "+v"(sa0), "+v"(sa4), "+v"(ka0), "+v"(ka4));
     const uint16_t* Ql = QOl + 2 * sl * TILE;
     const uint16_t* Ol = Ql + TILE;
-    const float* rl = kKsDelta ? pdel[w][sl] : rowc[sl];
+    const float* rl = rowc[sl];
     const float* ll = lsec[sl];
     uint16_t* Sd = Sl + sl * SIMG;
 #pragma unroll
@@ -350,7 +302,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           rs[4 * g + e] = -kLog2e * x[e];
-          d0[4 * g + e] = kKsDelta ? y[e] : -y[e];  // dP accumulated onto -delta
+          d0[4 * g + e] = -y[e];  // dP accumulated onto -delta
         }
       }
       d1 = d0;
@@ -499,11 +451,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
     const int qt0 = q0 + 32 * tq_blk;
     {
       f32x16 acc;
-      // the next slice's -delta (its dO / O landed before the barrier): loads first, dots beside the
-      // MFMAs (branch-free: after the last slice the stale slot is computed and never read)
-      u32x4 dlv[8], olv[8];
-      float dacc = 0.f;
-      if constexpr (kKsDelta) delta_load(sl ^ 1, dlv, olv);
       constexpr int QA = 3;  // transposed reads QA steps ahead of the MFMA chain
       bf16x8 fa[QA + 1], fb[QA + 1];
       auto rd_q = [&](int ks) {
@@ -517,12 +464,8 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
         if (ks + QA < BK / 16) rd_q(ks + QA);
         if (ks == 0) mfma_v0(acc, fb[0], fa[0]);
         else mfma_v(acc, fb[ks % (QA + 1)], fa[ks % (QA + 1)]);
-        if constexpr (kKsDelta) {
-          if (ks >= 4 && ks < 12) dacc = delta_dot(dlv[ks - 4], olv[ks - 4], dacc);
-        }
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (kKsDelta) delta_store(sl ^ 1, dacc);
       mfma_settle(acc);
       float lo[8], hi[8];
 #pragma unroll
@@ -588,7 +531,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
 namespace pllm {
 
 int attn_bwd_ks_key_block() { return KsCfg<128>::BK; }
-bool attn_bwd_ks_needs_delta() { return !kKsDelta; }
 
 // one pass of key blocks [a.kb0, a.kb0 + a.nkb_pass) (the caller runs the delta pre-pass before and the
 // slab reduce after)

@@ -205,7 +205,7 @@ int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab cou
 bool attn_bwd_uses_ks(int D);    // the key-stationary backward serves head dim D (q / k must be pre-rotated)
 // attn_bwd_ks.hip: keys per workgroup; one pass of the key-stationary main kernel (AttnBwdArgs as attn_bwd)
 int attn_bwd_ks_key_block();
-bool attn_bwd_ks_needs_delta();  // the key-stationary build reads delta from the pre-pass (PLLM_KS_DELTA=0)
+
 void attn_bwd_set_ks(int mask);  // A/B: bit 0 = D 64, bit 1 = D 128 on the key-stationary kernel
 void attn_bwd_ks_launch(const AttnBwdArgs& a, hipStream_t st);
 // attn_decode.hip: split-KV single-query attention over a KV cache
