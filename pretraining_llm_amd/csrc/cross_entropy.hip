@@ -15,12 +15,8 @@
 namespace {
 
 constexpr int CE_THREADS = 512;
-#ifndef PLLM_CE_ONLINE
-// 1: each lane's (max, exp-sum) pair merged in ONE block reduction (2 barriers per row instead of 5):
-// 2,524 vs 2,551 us at 65536 x 50304 (bench/ce_bench.py, scripts/gpu/r4_ce1.sh, same box, 3 rounds)
-#define PLLM_CE_ONLINE 1
-#endif
-constexpr bool kCeOnline = PLLM_CE_ONLINE != 0;
+// each lane's (max, exp-sum) pair merged in ONE block reduction (2 barriers per row instead of 5 for
+// separate max / sum reductions): 2,524 vs 2,551 us at 65536 x 50304 (bench/ce_bench.py, round 4)
 
 // one row per block: stores of the gradient with the non-temporal hint when NTS (A/B)
 template <int CH, bool WRITE_GRAD, int CE_THREADS = 512, bool NTS = false>
@@ -62,7 +58,7 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
   const int64_t t = targets[row];
   const bool valid = t != (int64_t)ignore_index && t >= 0 && t < V;
   float mc, s;
-  if constexpr (kCeOnline) {
+  {
     // the lane's own max, its exp-sum against it, then ONE block reduction of (max, sum) pairs
     // (2 barriers instead of 4; the target logit is read before any lane can overwrite it)
     const float xt = (threadIdx.x == 0 && valid) ? bf2f(x[t]) : 0.f;
@@ -112,28 +108,6 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
     if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - xt) : 0.f;
     if (!WRITE_GRAD) return;
     __syncthreads();  // lane 0's target-logit read (consumed by the loss above) precedes every store
-  } else {
-  m = block_max<CE_WAVES>(m, scratch);
-  mc = m * LOG2E;
-  // opaque to the optimiser: keeps only the packed row live across the passes
-#pragma unroll
-  for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
-  s = 0.f;
-#pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    float f[8];
-    unpack8(v[k], f);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s += fast_exp2(__builtin_fmaf(f[j], LOG2E, -mc));
-  }
-  if (tj < V) s += fast_exp2(__builtin_fmaf(tv, LOG2E, -mc));
-  s = block_sum<CE_WAVES>(s, scratch);
-#pragma unroll
-  for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
-  if (threadIdx.x == 0) PLLM_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
-  if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - bf2f(x[t])) : 0.f;
-  if (!WRITE_GRAD) return;
-  __syncthreads();  // every lane has read its logits before in-place overwrite (x may alias dlogits)
   }
   const float in = *inv_n;
   const float scale = valid ? in / s : 0.f;

@@ -38,11 +38,6 @@
 #include "common.h"
 #include "kernels.h"
 
-#ifndef PLLM_GEMM_STAGGER
-#define PLLM_GEMM_STAGGER 0  // n > 0: waves 4-7 issue the next stage's DMA before k-step n
-#endif
-constexpr int kGemmStagger = PLLM_GEMM_STAGGER;
-
 namespace {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));

@@ -45,12 +45,6 @@ constexpr int WNT = 512;         // 8 waves
 constexpr int WIMG = WBK * 32;   // elements of one [64][32] image (4 KiB)
 constexpr int WSLOT = 16 * WIMG; // 8 dY images then 8 X images: 64 KiB
 constexpr uint32_t kWOff = 0x80000000u;  // a byte offset past every descriptor built here
-#ifndef PLLM_WP_DMA_MFMA
-#define PLLM_WP_DMA_MFMA 0
-#endif
-// the K-tile DMA pieces issued between the phase's own MFMAs (after MFMAs 4 and 12) instead of in
-// its LOAD segment (as gemm_pp.hip's kPPDmaMfma)
-constexpr bool kWPDmaMfma = PLLM_WP_DMA_MFMA != 0;
 
 PLLM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -170,7 +164,7 @@ PLLM_DEV void wp_issue(const WPCtx& c, const WPSrd& srd, int sl) {
 // (a lower bound of what it issued after its last DMA)
 template <bool F, int PH>
 constexpr int wp_dma_wait() {
-  return (kWPDmaMfma ? 2 : 4) + ((F && PH < 2) ? 32 : 0);  // (kWPDmaMfma: this phase's 2 come after)
+  return 4 + ((F && PH < 2) ? 32 : 0);
 }
 
 // One phase: fragment reads of quadrant PH (rows half jh, column pair p; snake order (0,0) (0,1)
@@ -200,10 +194,8 @@ PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   i32x4v gr;
   unsigned glds;
   wp_group<PH>(c, srd, nsl, gr, glds);
-  if constexpr (!kWPDmaMfma) {
-    wp_piece<PH>(c, gr, glds, 0);
-    wp_piece<PH>(c, gr, glds, 1);
-  }
+  wp_piece<PH>(c, gr, glds, 0);
+  wp_piece<PH>(c, gr, glds, 1);
   wp_vmwait<wp_dma_wait<FIRST, PH>()>();
   wp_barrier();
   __builtin_amdgcn_s_setprio(1);
@@ -216,14 +208,6 @@ PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
         f32x4& a = acc[2 * p + ii][4 * jh + jj];
         if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
         else a = mfma16(fb[k][ii], fa[k][jj], a);
-        if constexpr (kWPDmaMfma) {
-          const int idx = 8 * k + 2 * jj + ii;
-          if (idx == 3 || idx == 11) {
-            __builtin_amdgcn_sched_barrier(0);
-            wp_piece<PH>(c, gr, glds, idx == 3 ? 0 : 1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
       }
   if constexpr (BIAS && (PH == 0 || PH == 2)) {
     if (dob) {
