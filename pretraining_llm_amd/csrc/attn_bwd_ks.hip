@@ -23,29 +23,6 @@
 
 namespace {
 
-// v_mfma_f32_32x32x16_bf16 with the accumulator in arch VGPRs: acc (+)= A B.  NOP: the statement opens
-// with s_nop 1 (2 wait states) -- needed when A / B / C was just written by a VALU instruction (a chain's
-// first MFMA after its VALU-initialised accumulator); A / B from LDS reads and C from the chain's
-// previous MFMA need none (s_nop 1 on all 80 MFMAs of a slice cost ~160 issue cycles per wave)
-template <bool NOP = false>
-PLLM_DEV void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-  else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
-}
-PLLM_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B (A, B from LDS)
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
-}
-// ... with the accumulator pinned to the accumulator file.  B (the packed P / dS fragments) was written
-// by VALU at least one pipelined step (>= 2 MFMAs) earlier; the accumulators' zero init is far back
-PLLM_DEV void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// an MFMA result read by anything but the next MFMA of its chain: 16-pass XDL -> 18 wait states
-PLLM_DEV void mfma_settle(f32x16& x) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x)); }
-PLLM_DEV void mfma_settle(f32x16& x, f32x16& y) {
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x), "+v"(y));
-}
-
 // ---------------------------------------------------------------------------
 // Key-stationary backward ("KS", round 5; D = 64 / 128): one workgroup = 4 waves, ONE per SIMD
 // (512 registers each) = 256 keys of one (batch, kv-head).  Wave w owns keys k0 + 64 w + [0, 64) as

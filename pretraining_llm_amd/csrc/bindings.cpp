@@ -1069,6 +1069,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_set_hy(int on) -> ()", [](int64_t on) { pllm::wgrad_set_hy((int)on); });
   m.def("attn_bwd_set_ks(int mask) -> ()", [](int64_t m) { pllm::attn_bwd_set_ks((int)m); });
+  m.def("attn_fwd_set_pw(int mask) -> ()", [](int64_t m) { pllm::attn_fwd_set_pw((int)m); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");

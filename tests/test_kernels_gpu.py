@@ -317,6 +317,32 @@ def test_attention_fwd(D, T, causal):
     assert (lse - lref).abs().max().item() < 2e-2
 
 
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("T,S,H,Hkv,B,causal", [(2048, 2048, 4, 2, 1, True), (1000, 1000, 2, 2, 2, True),
+                                                (300, 300, 2, 1, 2, False), (200, 456, 2, 2, 1, True),
+                                                (37, 300, 2, 1, 1, True), (96, 700, 2, 2, 1, False)])
+def test_attention_fwd_one_wave_per_simd(D, T, S, H, Hkv, B, causal):
+    """attn_fwd_pw_kernel (one wave per SIMD, block pairs staggered across the tile seam) vs fp32 and vs
+    the two-waves-per-SIMD kernel: ragged T / S, T < S (decode alignment), GQA, blocks that end early
+    (causal) or lie past T."""
+    torch.manual_seed(13)
+    q = torch.randn(B, T, H, D, device=DEV, dtype=torch.bfloat16)
+    k = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    v = torch.randn(B, S, Hkv, D, device=DEV, dtype=torch.bfloat16)
+    scale = 1 / math.sqrt(D)
+    try:
+        torch.ops.pllm.attn_fwd_set_pw(3)
+        o, lse = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
+        torch.ops.pllm.attn_fwd_set_pw(0)
+        o2, lse2 = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
+    finally:
+        torch.ops.pllm.attn_fwd_set_pw(2)
+    oref, lref = _attn_ref(q, k, v, causal, scale)
+    assert _rel(o, oref) < 1e-2, _rel(o, oref)
+    assert (lse - lref).abs().max().item() < 2e-2
+    assert _rel(o, o2) < 1e-2 and (lse - lse2).abs().max().item() < 2e-2
+
+
 @pytest.mark.parametrize("D", [32, 64, 128])
 @pytest.mark.parametrize("causal", [True, False])
 def test_attention_fwd_lazy_max_rescale_branch(D, causal):
