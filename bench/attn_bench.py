@@ -39,9 +39,6 @@ def main():
     ap.add_argument("--ks-ab", action="store_true",
                     help="backward only: key-stationary kernel (attn_bwd_set_ks(3)) vs the previous kernels "
                          "(set_ks(0)), interleaved rounds")
-    ap.add_argument("--pw-ab", action="store_true",
-                    help="forward only: one-wave-per-SIMD kernel (attn_fwd_set_pw(3)) vs the two-wave kernel "
-                         "(set_pw(0)), interleaved rounds")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
@@ -80,19 +77,6 @@ def main():
             res["prepass_us"] = min(1e6 * timeit(pre) for _ in range(args.rounds))
             res["prepass_fwd_us"] = min(1e6 * timeit(f_) for _ in range(args.rounds))
             res["prepass_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
-            print(json.dumps(res), flush=True)
-            continue
-        if args.pw_ab:
-            flops_f = 2 * 2 * B * H * T * T * D / 2
-            res = {"cfg": cfg, "pw_fwd_us": [], "old_fwd_us": []}
-            for _ in range(args.rounds):
-                torch.ops.pllm.attn_fwd_set_pw(3)
-                res["pw_fwd_us"].append(1e6 * timeit(ours_f))
-                torch.ops.pllm.attn_fwd_set_pw(0)
-                res["old_fwd_us"].append(1e6 * timeit(ours_f))
-            torch.ops.pllm.attn_fwd_set_pw(2)
-            for k_ in ("pw", "old"):
-                res[k_ + "_tflops"] = flops_f / (min(res[k_ + "_fwd_us"]) * 1e-6) / 1e12
             print(json.dumps(res), flush=True)
             continue
         if args.ks_ab:

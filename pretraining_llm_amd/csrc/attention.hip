@@ -1475,24 +1475,7 @@ static void attn_bwd_r(const AttnBwdArgs& a, hipStream_t st) {
   else attn_bwd_t<D, 2>(a, st);
 }
 
-// one-wave-per-SIMD forward (attn_fwd_pw.hip) per head dim, a bit mask as the KS backward's: initial
-// value from PLLM_ATTN_FWD_PW (comma list of head dims, default "128"), runtime A/B via attn_fwd_set_pw
-static int g_attn_pw = -1;
-static bool attn_fwd_pw_on(int D) {
-  if (g_attn_pw < 0) {
-    const char* e = std::getenv("PLLM_ATTN_FWD_PW");
-    const char* v = e ? e : "128";
-    g_attn_pw = (std::strstr(v, "64") ? 1 : 0) | (std::strstr(v, "128") ? 2 : 0);
-  }
-  return (D == 64 && (g_attn_pw & 1)) || (D == 128 && (g_attn_pw & 2));
-}
-void attn_fwd_set_pw(int mask) { g_attn_pw = mask & 3; }
-
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
-  if (attn_fwd_pw_on(a.D) && attn_fwd_pw_supported(a)) {
-    attn_fwd_pw(a, st);
-    return;
-  }
   if (a.D == 32) attn_fwd_t<32>(a, st);
   else if (a.D == 64) attn_fwd_t<64>(a, st);
   else attn_fwd_t<128>(a, st);

@@ -140,7 +140,7 @@ struct ImgS {
 constexpr float kLog2e = 1.4426950408889634f;
 
 // ---------------------------------------------------------------------------
-// Inline-asm MFMAs with an explicit register class (attn_bwd_ks.hip, attn_fwd_pw.hip): hipcc left to
+// Inline-asm MFMAs with an explicit register class (attn_bwd_ks.hip): hipcc left to
 // itself put the long-lived accumulators in whichever file it liked and copied them at branch joins.
 // Hazards the compiler does not pad for asm (cdna_hip_programming.md §5.7) are the caller's: NOP
 // variants open with s_nop 1 (a VALU-written operand), mfma_settle() precedes a non-MFMA reader.

@@ -871,8 +871,8 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
   // the forward's tile loop, summed and printed to stderr after the launch
   static const bool stamps = std::getenv("PLLM_FWD_STAMPS") != nullptr;
   Tensor st;
-  if (stamps && D <= 64) {
-    const int64_t nqb = (T + 255) / 256;
+  if (stamps) {
+    const int64_t nqb = (T + 127) / 128;  // >= the workgroups of every forward kernel
     st = at::zeros({nqb * B * H * 4 * 9}, q.options().dtype(at::kLong));
     a.stamps = (unsigned long long*)st.data_ptr();
   }
@@ -881,7 +881,7 @@ std::vector<Tensor> attn_fwd(const Tensor& q, const Tensor& k, const Tensor& v, 
     auto h = st.view({-1, 9}).to(at::kCPU).to(at::kDouble);
     auto tot = h.sum(0);
     const double tiles = tot[6].item<double>();
-    fprintf(stderr, "[fwd stamps] waves %lld tiles %.0f | per tile: gload %.0f qk %.0f softmax %.0f pv %.0f swrite %.0f barrier %.0f | per wave total %.0f (mask sum %.0f)\n",
+    fprintf(stderr, "[fwd stamps] waves %lld tiles %.0f | per tile: p0 %.0f p1 %.0f p2 %.0f p3 %.0f p4 %.0f p5 %.0f | per wave total %.0f (p7 sum %.0f)\n",
             (long long)h.size(0), tiles, tot[0].item<double>() / tiles, tot[1].item<double>() / tiles,
             tot[2].item<double>() / tiles, tot[3].item<double>() / tiles, tot[4].item<double>() / tiles,
             tot[5].item<double>() / tiles, tot[8].item<double>() / h.size(0), tot[7].item<double>());
@@ -1069,7 +1069,6 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_set_hy(int on) -> ()", [](int64_t on) { pllm::wgrad_set_hy((int)on); });
   m.def("attn_bwd_set_ks(int mask) -> ()", [](int64_t m) { pllm::attn_bwd_set_ks((int)m); });
-  m.def("attn_fwd_set_pw(int mask) -> ()", [](int64_t m) { pllm::attn_fwd_set_pw((int)m); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");

@@ -208,11 +208,7 @@ void gemv(const GemvArgs& a, hipStream_t st);
 // attention.hip
 bool attn_supported_head_dim(int D);
 int attn_bwd_key_block(int D);  // keys per backward workgroup = dq_acc slab count divisor
-bool attn_bwd_uses_ks(int D);
-// one-wave-per-SIMD forward (attn_fwd_pw.hip): D = 64 / 128 without fused RoPE
-bool attn_fwd_pw_supported(const AttnFwdArgs& a);
-void attn_fwd_pw(const AttnFwdArgs& a, hipStream_t st);
-void attn_fwd_set_pw(int mask);    // the key-stationary backward serves head dim D (q / k must be pre-rotated)
+bool attn_bwd_uses_ks(int D);    // the key-stationary backward serves head dim D (q / k must be pre-rotated)
 // attn_bwd_ks.hip: keys per workgroup; one pass of the key-stationary main kernel (AttnBwdArgs as attn_bwd)
 int attn_bwd_ks_key_block();
 
