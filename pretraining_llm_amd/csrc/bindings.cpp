@@ -614,9 +614,7 @@ Tensor cross_entropy(const Tensor& logits, const Tensor& targets, const std::opt
 // ---------------------------------------------------------------- optimizer
 void adamw_(Tensor& param, Tensor& master, Tensor& m, Tensor& v, const Tensor& grad, double lr, double b1, double b2,
             double eps, double wd, int64_t step, double grad_scale, const std::optional<Tensor>& scale,
-            const std::optional<Tensor>& wd_mask, const std::optional<Tensor>& hyper,
-            const std::optional<Tensor>& tp_desc, int64_t tp_tiles, const std::optional<Tensor>& runs,
-            int64_t flat_blocks) {
+            const std::optional<Tensor>& wd_mask, const std::optional<Tensor>& hyper) {
   const int64_t n = master.numel();
   TORCH_CHECK(master.scalar_type() == at::kFloat && m.scalar_type() == at::kFloat && v.scalar_type() == at::kFloat,
               "adamw: master/m/v must be fp32");
@@ -648,20 +646,6 @@ void adamw_(Tensor& param, Tensor& master, Tensor& m, Tensor& v, const Tensor& g
   if (hyper) {  // device-side [lr, 1/bc1, 1/sqrt(bc2)] (graph-capturable step)
     TORCH_CHECK(hyper->scalar_type() == at::kFloat && hyper->is_cuda() && hyper->numel() >= 3, "adamw: hyper");
     hp = hyper->data_ptr<float>();
-  }
-  if (tp_desc) {
-    // fused shadow refresh: the table must describe matrices inside `param` (FlatAdamW builds both)
-    TORCH_CHECK(pp && runs && tp_desc->is_cuda() && tp_desc->scalar_type() == at::kLong && tp_desc->dim() == 2 &&
-                    tp_desc->size(1) == 6 && tp_desc->is_contiguous(), "adamw_: tp_desc from transpose_plan");
-    TORCH_CHECK(runs->is_cuda() && runs->scalar_type() == at::kLong && runs->dim() == 2 && runs->size(1) == 3 &&
-                    runs->size(0) >= 1 && runs->is_contiguous(), "adamw_: runs [n, 3] int64");
-    TORCH_CHECK(tp_tiles >= 0 && flat_blocks >= 0 && tp_tiles + flat_blocks < (1ll << 31), "adamw_: grid");
-    if (n)
-      pllm::adamw_shadow(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), gf32,
-                         (float)lr, (float)b1, (float)b2, (float)eps, (float)wd, (int)step, (float)grad_scale, sp, wm,
-                         hp, tp_desc->data_ptr<int64_t>(), (int)tp_desc->size(0), (int)tp_tiles,
-                         runs->data_ptr<int64_t>(), (int)runs->size(0), (int)flat_blocks, cur_stream());
-    return;
   }
   if (n)
     pllm::adamw_flat(pp, master.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), grad.data_ptr(), gf32, n,
@@ -1083,7 +1067,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("lse_merge_(Tensor(a!) o_acc, Tensor(b!) lse_acc, Tensor o, Tensor lse) -> ()");
   m.def("zero_ranges_(Tensor(a!) buf, Tensor ranges, int total_len) -> ()");
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
-  m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None, Tensor? tp_desc=None, int tp_tiles=0, Tensor? runs=None, int flat_blocks=0) -> ()");
+  m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe) -> (Tensor, Tensor)");

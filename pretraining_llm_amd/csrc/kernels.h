@@ -98,12 +98,6 @@ int cross_entropy_max_vocab();
 void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, size_t n,
                 float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,
                 const float* scale_ptr, const uint8_t* wd_blocks, const float* hyper, hipStream_t st);
-// AdamW + the W^T shadow refresh in one launch: desc = transpose_plan's table (matrices inside param),
-// runs = [start vector, end vector, first block] of the elements outside them
-void adamw_shadow(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, float lr,
-                  float b1, float b2, float eps, float wd, int step, float grad_scale, const float* scale_ptr,
-                  const uint8_t* wd_blocks, const float* hyper, const int64_t* desc, int ndesc, int tiles,
-                  const int64_t* runs, int nruns, int flat_blocks, hipStream_t st);
 int sumsq_blocks(size_t n);
 void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
 

@@ -145,11 +145,6 @@ class FlatAdamW:
             self._tp_desc = _lib.require().transpose_plan([p.data for p in self.shadowed],
                                                           [p._pllm_wT for p in self.shadowed])
             self._tp_tiles = sum(((p.shape[0] + 63) // 64) * ((p.shape[1] + 63) // 64) for p in self.shadowed)
-            idx_of = {id(p): i for i, p in enumerate(self.params)}
-            # AdamW writes the shadows itself (csrc/adamw.hip adamw_shadow_kernel): its tile blocks cover the
-            # shadowed matrices, its flat blocks these runs of 8-element vectors outside them
-            self._adam_runs, self._adam_flat_blocks = shadow_complement_runs(
-                [(self.offsets[idx_of[id(p)]], p.numel()) for p in self.shadowed], total, dev)
         self.refresh_shadows()
         # Lazy zeroing (HIP path): zero_grad clears only the slots that accumulating writers fill (norms,
         # biases, embedding tables) in one launch, and marks the weight-GEMM slots "fresh": their first
@@ -313,17 +308,10 @@ class FlatAdamW:
             clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).to(torch.float32).reshape(1)
         b1, b2 = self.betas
         if self.use_hip and _ops_mod.get_backend() == "auto":
-            fused = self._tp_desc is not None
             _lib.require().adamw_(self.flat_param, self.master, self.exp_avg, self.exp_avg_sq, self.flat_grad,
                                   self.lr, b1, b2, self.eps, self.weight_decay, self.step_count, grad_scale, clip,
-                                  self.wd_mask, self.hyper if graph else None,
-                                  self._tp_desc if fused else None, self._tp_tiles,
-                                  self._adam_runs if fused else None, self._adam_flat_blocks if fused else 0)
-            if fused:
-                for p in self.shadowed:
-                    p._pllm_wT_ver = p._version
-            else:
-                self.refresh_shadows()
+                                  self.wd_mask, self.hyper if graph else None)
+            self.refresh_shadows()
             return
         if graph:
             raise RuntimeError("graph-captured optimizer steps need the HIP AdamW kernel (bf16 params on GPU)")
@@ -395,22 +383,6 @@ class FlatAdamW:
         """Call after loading model weights directly into the params."""
         self.master.copy_(self.flat_param.float())
         self.refresh_shadows()
-
-
-def shadow_complement_runs(segments, total: int, device, block: int = 256):
-    """[start vector, end vector, first block] rows (int64 tensor on ``device``) of the 8-element vectors of a
-    flat buffer of ``total`` elements NOT inside the (offset, numel) ``segments`` (every bound a multiple of
-    8), plus the number of ``block``-vector blocks they need: the flat half of the fused AdamW launch."""
-    rows, pos, fb = [], 0, 0
-    for o, n in sorted(segments) + [(total, 0)]:
-        if o > pos:
-            a, b = pos // 8, o // 8
-            rows.append([a, b, fb])
-            fb += (b - a + block - 1) // block
-        pos = max(pos, o + n)
-    if not rows:
-        rows = [[0, 0, 0]]
-    return torch.tensor(rows, dtype=torch.int64, device=device), fb
 
 
 def accumulate_only_runs(params, offsets, total: int, fresh_ids) -> list:

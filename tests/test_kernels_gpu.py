@@ -235,50 +235,6 @@ def test_adamw_flat_matches_torch():
     assert _rel(pb, ref_p.detach()) < 1e-2
 
 
-@pytest.mark.parametrize("decay_all", [True, False])
-def test_adamw_fused_shadow_refresh(decay_all):
-    """AdamW with the W^T shadow refresh fused in (adamw_shadow_kernel) vs the flat AdamW + the separate
-    batched transpose: params, fp32 state and shadows bit-identical; shadows == W^T.  Matrices with edge
-    tiles (dims multiples of 8, not of 64), 1-D params between them, weight decay per parameter."""
-    from pretraining_llm_amd.train.optim import FlatAdamW, no_decay_1d
-
-    class M(torch.nn.Module):
-        def __init__(self):
-            super().__init__()
-            self.a = torch.nn.Parameter(torch.randn(72, 200))
-            self.n1 = torch.nn.Parameter(torch.randn(200))
-            self.b = torch.nn.Parameter(torch.randn(256, 64))
-            self.c = torch.nn.Parameter(torch.randn(40, 8))
-            self.n2 = torch.nn.Parameter(torch.randn(37))
-            self.d = torch.nn.Parameter(torch.randn(1000, 136))
-
-    torch.manual_seed(7)
-    base = M().to(DEV).bfloat16()
-    opts = []
-    for _ in range(2):
-        m = M().to(DEV).bfloat16()
-        m.load_state_dict(base.state_dict())
-        opts.append((m, FlatAdamW(m, lr=1e-2, weight_decay=0.1, max_grad_norm=1.0,
-                                  decay_filter=None if decay_all else no_decay_1d)))
-    fused, plain = opts[0][1], opts[1][1]
-    assert fused._tp_desc is not None and len(fused.shadowed) == 4
-    plain._tp_desc_saved, plain._tp_desc = plain._tp_desc, None  # flat AdamW, then per-matrix refresh...
-    for step in range(3):
-        g = torch.randn(fused.total, device=DEV)
-        for opt in (fused, plain):
-            opt.zero_grad()
-            opt.flat_grad.copy_(g)
-            for p in opt._fresh_params:
-                p._pllm_grad_fresh = False
-            opt.step()
-    torch.cuda.synchronize()
-    for a, b in ((fused.flat_param, plain.flat_param), (fused.master, plain.master),
-                 (fused.exp_avg, plain.exp_avg), (fused.exp_avg_sq, plain.exp_avg_sq)):
-        assert torch.equal(a, b)
-    for p in fused.shadowed:
-        assert torch.equal(p._pllm_wT, p.t())
-
-
 def test_sumsq():
     x = torch.randn(1 << 20, device=DEV).bfloat16()
     s = torch.ops.pllm.sumsq(x)
