@@ -6,8 +6,9 @@
 #   tests                 GPU test suite (pytest -m gpu)
 #   tests:<expr>          GPU tests selected by pytest -k <expr>
 #   smoke                 __graft_entry__.smoke()
-#   bench:<name>[:args]   python bench.py <args>  ('+' separates args, e.g. bench:llama:--model+llama-1.3b)
-#   prof:<name>[:args]    rocprofv3 kernel trace + stats of bench.py <args>, summarised to <name>.md
+#   bench:<name>[:args]   python bench.py <args>; no args: the named config (CFG below), else '+'-separated
+#                         literal args, e.g. bench:llama or bench:l8:--model+llama-1.3b+--batch+8
+#   prof:<name>[:args]    rocprofv3 kernel trace + stats of bench.py <args> (same rule), summarised to <name>.md
 #   pmc:<name>:<counterset>:<script>[:args]
 #                         one rocprofv3 --pmc pass per counter set group (see SETS below) over
 #                         python3 <script> <args>, summarised by scripts/pmc_kernels.py to <name>.md
@@ -55,11 +56,11 @@ for task in "$@"; do
         || { tail -5 "$O/smoke.log"; exit 1; }
       tail -1 "$O/smoke.log" ;;
     bench)
-      timeout -k 10 500 python bench.py $(args_of "$rest") > "$O/bench_$name.log" 2>&1 \
+      timeout -k 10 500 python bench.py $(args_of "${rest:-$name}") > "$O/bench_$name.log" 2>&1 \
         || { tail -3 "$O/bench_$name.log"; exit 1; }
       tail -1 "$O/bench_$name.log" | cut -c1-260 ;;
     prof)
-      a=$(args_of "$rest")
+      a=$(args_of "${rest:-$name}")
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv -- \
           python3 "$R/bench.py" $a > "$O/$name.log" 2>&1 ) || { tail -3 "$O/$name.log"; exit 1; }
       steps=$(python3 -c "import sys,json; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['steps']+d['warmup'])" "$O/$name.log") || exit 1
