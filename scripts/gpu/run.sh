@@ -63,7 +63,7 @@ for task in "$@"; do
       a=$(args_of "${rest:-$name}")
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$O/$name" -o run --output-format csv -- \
           python3 "$R/bench.py" $a > "$O/$name.log" 2>&1 ) || { tail -3 "$O/$name.log"; exit 1; }
-      steps=$(python3 -c "import sys,json; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]); print(d['steps']+d['warmup']+(2 if d.get('step_mode')=='graph' else 0))" "$O/$name.log") || exit 1
+      steps=$(python3 -c "import sys,json; d=json.loads([l for l in open(sys.argv[1]) if l.startswith('{\"metric')][-1]); print(d['steps']+d['warmup']+(2 if d.get('config', {}).get('step_mode')=='graph' else 0))" "$O/$name.log") || exit 1
       # (graph mode: GraphedTrainStep runs 2 eager warm-up steps before its capture, bench.py:199)
       python3 scripts/prof_summary.py "$O/$name/run_kernel_stats.csv" "$steps" "$name: bench.py $a" > "$O/$name.md" || exit 1
       head -14 "$O/$name.md" ;;
