@@ -291,7 +291,25 @@ __global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* __restri
 #pragma unroll
     for (int j = 0; j < 8; ++j) f[j] = 0.f;
   }
-  for (int s = 0; s < S; ++s) {
+  // four slices' loads in flight before their adds (slice order kept: deterministic)
+  int s = 0;
+  for (; s + 4 <= S; s += 4) {
+    f32x4 v[4][2];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4* p = reinterpret_cast<const f32x4*>(part + (s + u) * PQ + i);
+      v[u][0] = p[0];
+      v[u][1] = p[1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        f[j] += v[u][0][j];
+        f[4 + j] += v[u][1][j];
+      }
+  }
+  for (; s < S; ++s) {
     const f32x4* p = reinterpret_cast<const f32x4*>(part + s * PQ + i);
     const f32x4 a = p[0], b = p[1];
 #pragma unroll
