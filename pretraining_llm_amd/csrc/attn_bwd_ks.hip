@@ -11,7 +11,6 @@
 // with s_nop 1 (a VALU-written A / B / C operand; free while the previous MFMA occupies the pipe), an
 // accumulate chain into the same C needs nothing, and mfma_settle() (18 wait states, taking the
 // result as an operand so every consumer is ordered after it) precedes any non-MFMA reader.
-#include <cstdlib>
 #include <type_traits>
 
 #ifndef PLLM_BWD_STAMPS
@@ -504,295 +503,6 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
 }
 
 
-// ---------------------------------------------------------------------------
-// Key-stationary backward at D = 64 with TWO waves per SIMD ("KS8", round 5): one workgroup = 8 waves
-// = 256 keys of one (batch, kv-head), wave w owning ONE 32-key block (dK^T / dV^T: 64 AGPRs) across the
-// whole sweep; 64-query slices (2 sub-blocks of 32).  At D = 64 a slice carries twice the softmax
-// elements per MFMA of D = 128, which one wave per SIMD cannot hide behind its own MFMAs (the 4-wave KS
-// kernel ran 612-885 us vs 548-717 for attn_bwd_kernel<64>); here the SIMD partner's MFMAs cover each
-// wave's softmax, and what the 8-wave kernel of attention.hip pays per 128-query iteration -- two
-// barriers and the Q / dO DMA waited at the top of the next iteration -- goes: ONE barrier per slice
-// with double-buffered Q / dO / dS^T images and row constants (the DMA of slice it + 2 issued right
-// after the barrier of slice it).  The slice's dQ (4 tasks of 32 queries x 32 dims over all 256 keys,
-// 16 MFMAs each, the KS slab format) runs on waves 0-3 while waves 4-7 start the next slice.
-template <int ROPE>
-__global__ __launch_bounds__(512, 1) void attn_bwd_ks8_kernel(AttnBwdArgs a) {
-  static_assert(ROPE != 1, "KS backward: q / k pre-rotated (ROPE 0 or 2)");
-  constexpr int D = 64;
-  using I = Img<D>;
-  using IT = ImgT<64>;
-  constexpr int NW = 8, BK = 256, BQ = 64, NQB = 2, NKS = D / 16, NDB = D / 32, CPR = D / 8;
-  constexpr int QRP = 512 / D, KPPW = BK / QRP / NW;  // 8 rows per 1-KiB piece; 4 K pieces per wave
-  constexpr int TILE = BQ * D, SIMG = BK * BQ;
-  static_assert(BQ / QRP == NW, "one Q and one dO piece per wave and slice");
-  __shared__ __attribute__((aligned(1024))) uint16_t smem[BK * D + 4 * TILE + 2 * SIMG];  // 128 KiB
-  __shared__ __attribute__((aligned(16))) float lsec[2][64];
-  __shared__ __attribute__((aligned(16))) float rowc[2][64];
-  uint16_t* const Kl = smem;
-  uint16_t* const QOl = smem + BK * D;  // slot s: Q tile at QOl + 2 s TILE, dO tile right after
-  uint16_t* const Sl = QOl + 4 * TILE;  // slot s: dS^T image at Sl + s SIMG
-
-  const int BH = a.B * a.Hkv;
-  const int id = blockIdx.x;
-  const int kb = a.kb0 + id / BH;
-  const int bh = id % BH;
-  const int b = bh / a.Hkv, hk = bh % a.Hkv;
-  const int G = a.H / a.Hkv;
-  const int tid = threadIdx.x, lane = tid & 63, r = lane & 31, hh = lane >> 5;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k0 = kb * BK, kw0 = k0 + 32 * w;
-  const int off = a.S - a.T;
-  const unsigned lds0 = (unsigned)(uintptr_t)smem;
-  const uint16_t* kp = a.k + b * a.k_sb + (int64_t)hk * a.k_sh;
-  const uint16_t* vp = a.v + b * a.v_sb + (int64_t)hk * a.v_sh;
-
-  const int nqs = (a.T + BQ - 1) / BQ;
-  const int qs_start = a.causal ? max(0, k0 - off) / BQ : 0;
-  const int per_head = max(0, nqs - qs_start);
-  const int total = per_head * G;
-
-  {  // K image by LDS DMA (swizzle applied to the source; keys past S read zeros)
-    const int rows = min(BK, a.S - k0);
-    const i32x4v ks = srd_of(kp + (int64_t)k0 * a.k_st, (uint32_t)(((int64_t)(rows - 1) * a.k_st + D) * 2));
-#pragma unroll
-    for (int k = 0; k < KPPW; ++k) {
-      const int p = w * KPPW + k, row = p * QRP + lane / CPR, ch = (lane % CPR) ^ I::f(row);
-      blds16(ks, (uint32_t)((row * a.k_st + 8 * ch) * 2), lds0 + 1024u * (unsigned)p);
-    }
-  }
-  // Q / dO DMA of slice it into slot sl: wave w moves piece w (rows 8 w + [0, 8)) of both tiles
-  const int qrow = w * QRP + lane / CPR, qch = (lane % CPR) ^ I::f(qrow);
-  const uint32_t qvo = (uint32_t)((qrow * a.q_st + 8 * qch) * 2), ovo = (uint32_t)((qrow * a.do_st + 8 * qch) * 2);
-  auto slice_of = [&](int it, int& h, int& q0) {
-    h = hk * G + it / per_head;
-    q0 = (qs_start + it % per_head) * BQ;
-  };
-  auto qdma = [&](int it, int sl) {
-    int h, q0;
-    slice_of(it, h, q0);
-    const int rows = a.T - q0;
-    const i32x4v qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
-                             (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
-    const i32x4v os = srd_of(a.dO + b * a.do_sb + (int64_t)h * a.do_sh + (int64_t)q0 * a.do_st,
-                             (uint32_t)(((int64_t)(rows - 1) * a.do_st + D) * 2));
-    blds16(qs, qvo, lds0 + 2u * (unsigned)(BK * D + 2 * sl * TILE) + 1024u * (unsigned)w);
-    blds16(os, ovo, lds0 + 2u * (unsigned)(BK * D + 2 * sl * TILE + TILE) + 1024u * (unsigned)w);
-  };
-  auto rload = [&](int it) {  // row constants (raw lse, delta) by LDS DMA, waves 0 / 1
-    int h, q0;
-    slice_of(it, h, q0);
-    const int64_t row0 = ((int64_t)b * a.H + h) * a.T + q0;
-    if (w == 0) {
-      const i32x4v srd = srd_of(a.lse + row0, (uint32_t)(a.T - q0) * 4u);
-      blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&lsec[it & 1][0]);
-    } else if (w == 1) {
-      const i32x4v srd = srd_of(a.delta + row0, (uint32_t)(a.T - q0) * 4u);
-      blds4(srd, (uint32_t)lane * 4u, (unsigned)(uintptr_t)&rowc[it & 1][0]);
-    }
-  };
-  bf16x8 vf[NKS];  // V rows of this wave's keys as B fragments, zero past S
-  {
-    const int key = kw0 + r;
-#pragma unroll
-    for (int ks = 0; ks < NKS; ++ks)
-      vf[ks] = key < a.S ? as_frag(ld16(vp + (int64_t)key * a.v_st + 16 * ks + 8 * hh)) : zero_frag();
-  }
-  if (total > 0) {
-    qdma(0, 0);
-    rload(0);
-    if (total > 1) {
-      qdma(1, 1);
-      rload(1);
-    }
-  }
-  vm_wait_all();
-  __syncthreads();
-
-  f32x16 dk[NDB], dv[NDB];
-#pragma unroll
-  for (int db = 0; db < NDB; ++db) {
-    dk[db] = zero16();
-    dv[db] = zero16();
-  }
-  const float c2 = a.scale_log2;
-  const int g1 = (lane >> 4) & 1, i16 = lane & 15, tq = i16 >> 2, tp = i16 & 3;
-  const int fq0 = I::off(r, 8 * hh);
-  const int ft00 = I::off(4 * hh + tq, 16 * g1 + 4 * tp), ft80 = I::off(4 * hh + tq + 8, 16 * g1 + 4 * tp);
-  const bool aligned = (off & 31) == 0 && kw0 + 32 <= a.S;
-  const bool dq_wave = w < 4;  // waves 0-3: one dQ task each (query sub-block w / 2, dim block w % 2)
-  const int tq_blk = (w >> 1) & 1, tdb = w & 1;
-  const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = 32 * tdb + 16 * g1 + 4 * tp;
-  const int sa00 = IT::off(8 * hh + tq, qc), sa40 = IT::off(8 * hh + tq + 4, qc);
-  const int ka00 = I::off(8 * hh + tq, dc), ka40 = I::off(8 * hh + tq + 4, dc);
-
-  int h = hk * G, qi = qs_start;
-  for (int it = 0; it < total; ++it, (++qi == nqs) ? (qi = qs_start, ++h) : 0) {
-    const int sl = it & 1;
-    const int q0 = qi * BQ;
-    int fq = fq0, ft0 = ft00, ft8 = ft80;
-    asm volatile("" : "+v"(fq), "+v"(ft0), "+v"(ft8));
-    const uint16_t* Ql = QOl + 2 * sl * TILE;
-    const uint16_t* Ol = Ql + TILE;
-    const float* rl = rowc[sl];
-    const float* ll = lsec[sl];
-    uint16_t* Sd = Sl + sl * SIMG;
-#pragma unroll
-    for (int j = 0; j < NQB; ++j) {
-      const int qj0 = q0 + 32 * j;
-      // masks folded into the S chain's initial accumulator (0 or -inf), behind one wave-uniform branch
-      const bool mask_j = !aligned || (a.causal && kw0 + 31 > qj0 + off);
-      f32x16 s, d;
-      if (mask_j) {
-        const int key = kw0 + r;
-        const int lo = key >= a.S ? 64 : (a.causal ? key - off - (qj0 + 4 * hh) : -64);
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s[i] = acc_row(i, 0) < lo ? -INFINITY : 0.f;
-      } else {
-        s = zero16();
-      }
-      float rs[16];
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const f32x4 x = *reinterpret_cast<const f32x4*>(&ll[32 * j + 8 * g + 4 * hh]);
-        const f32x4 y = *reinterpret_cast<const f32x4*>(&rl[32 * j + 8 * g + 4 * hh]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          rs[4 * g + e] = -kLog2e * x[e];
-          d[4 * g + e] = -y[e];  // dP accumulated onto -delta
-        }
-      }
-      // S = Q K^T, dP = dO V^T (key on the lane)
-#pragma unroll
-      for (int ks = 0; ks < NKS; ++ks) {
-        const int fo = fq ^ (ks << 4);
-        const bf16x8 qa = as_frag(ld16(Ql + 32 * j * D + fo));
-        const bf16x8 oa = as_frag(ld16(Ol + 32 * j * D + fo));
-        const bf16x8 kf = as_frag(ld16(Kl + 32 * w * D + fo));
-        if (ks == 0) {
-          mfma_v<true>(s, qa, kf);
-          mfma_v<true>(d, oa, vf[ks]);
-        } else {
-          mfma_v(s, qa, kf);
-          mfma_v(d, oa, vf[ks]);
-        }
-      }
-      mfma_settle(s, d);
-      // P = exp2(S c2 - lse log2 e), dS = P dP
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const float pv = fast_exp2(__builtin_fmaf(s[i], c2, rs[i]));
-        s[i] = pv;
-        d[i] = pv * d[i];
-      }
-      bf16x8 pf[2], sf[2];
-#pragma unroll
-      for (int x = 0; x < 2; ++x) {
-        pf[x] = pack_frag(s, x);
-        sf[x] = pack_frag(d, x);
-      }
-      // dV^T += dO^T P, dK^T += Q^T dS (transposed A operands)
-#pragma unroll
-      for (int t = 0; t < 2 * NDB; ++t) {
-        const int db = t >> 1, st = t & 1;
-        const int rb = (32 * j + 16 * st) * D, o0 = rb + (ft0 ^ (db << 5)), o8 = rb + (ft8 ^ (db << 5));
-        const bf16x8 oA = cat_tr(ds_tr(Ol + o0), ds_tr(Ol + o8));
-        const bf16x8 qA = cat_tr(ds_tr(Ql + o0), ds_tr(Ql + o8));
-        if (t == 0) {
-          mfma_a<true>(dv[db], oA, pf[st]);
-          mfma_a<true>(dk[db], qA, sf[st]);
-        } else {
-          mfma_a(dv[db], oA, pf[st]);
-          mfma_a(dk[db], qA, sf[st]);
-        }
-      }
-      // dS^T image rows of this wave's keys (group pairs swapped across the half-waves: 16-B stores)
-#pragma unroll
-      for (int k = 0; k < 4; k += 2) {
-        u32x2 v0, v1;
-        {
-          const u32x4 w4 = __builtin_bit_cast(u32x4, sf[k >> 1]);
-          v0 = u32x2{w4[0], w4[1]};
-          v1 = u32x2{w4[2], w4[3]};
-        }
-#pragma unroll
-        for (int dd = 0; dd < 2; ++dd) {
-          const auto sw = __builtin_amdgcn_permlane32_swap(v0[dd], v1[dd], false, false);
-          v0[dd] = sw[0];
-          v1[dd] = sw[1];
-        }
-        *reinterpret_cast<u32x4*>(Sd + IT::off(32 * w + r, 32 * j + 8 * k + 8 * hh)) = u32x4{v0[0], v0[1], v1[0], v1[1]};
-      }
-    }
-    // ---- hand-off: slice it + 1's Q / dO / row constants (DMA'd after the previous barrier) landed --
-    // counted: waves 0-3 may leave their 2 dQ slab stores of slice it - 1 in flight
-    if (dq_wave) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (it + 2 < total) {
-      qdma(it + 2, sl);
-      rload(it + 2);
-    }
-    // ---- dQ partial of this key block (waves 0-3; branch-free stores: past T the offset drops them)
-    if (dq_wave) {
-      int sa0 = sa00, sa4 = sa40, ka0 = ka00, ka4 = ka40;
-      asm volatile("" : "+v"(sa0), "+v"(sa4), "+v"(ka0), "+v"(ka4));
-      const int qt0 = q0 + 32 * tq_blk;
-      f32x16 acc;
-      constexpr int QA = 3;
-      bf16x8 fa[QA + 1], fb[QA + 1];
-      auto rd_q = [&](int ks) {
-        fa[ks % (QA + 1)] = cat_tr(ds_tr(Sd + 16 * ks * BQ + sa0), ds_tr(Sd + 16 * ks * BQ + sa4));
-        fb[ks % (QA + 1)] = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
-      };
-#pragma unroll
-      for (int ks = 0; ks < QA; ++ks) rd_q(ks);
-#pragma unroll
-      for (int ks = 0; ks < BK / 16; ++ks) {
-        if (ks + QA < BK / 16) rd_q(ks + QA);
-        if (ks == 0) mfma_v0(acc, fb[0], fa[0]);
-        else mfma_v(acc, fb[ks % (QA + 1)], fa[ks % (QA + 1)]);
-      }
-      mfma_settle(acc);
-      float lo[8], hi[8];
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        lo[e] = acc[e];
-        hi[e] = acc[8 + e];
-      }
-      const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc(
-          (void*)(a.dq_acc + (kb - a.kb0) * a.slab + ((int64_t)b * a.H + h) * a.nqt * NDB * 1024), (short)0,
-          a.nqt * NDB * 2048, 0x00020000);
-      const uint32_t doff = qt0 < a.T ? (uint32_t)(((qt0 >> 5) * NDB + tdb) * 2048 + lane * 32) : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(pack8(lo), drs, doff, 0, 0);
-      __builtin_amdgcn_raw_buffer_store_b128(pack8(hi), drs, doff + 16u, 0, 0);
-    }
-  }
-  // ---- dK (scaled; RoPE: rotated back) and dV of this lane's key
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
-#pragma unroll
-  for (int db = 0; db < NDB; ++db) asm volatile("" : "+a"(dk[db]), "+a"(dv[db]));
-  const int key = kw0 + r;
-  if (key < a.S) {
-    if (ROPE != 0) {
-      const float* cr = a.rope_cos + (int64_t)key * (D / 2);
-      const float* sr = a.rope_sin + (int64_t)key * (D / 2);
-#pragma unroll
-      for (int db = 0; db < NDB / 2; ++db)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int dd = db * 32 + 8 * (i >> 2) + 4 * hh + (i & 3);
-          const float c = cr[dd], sn = sr[dd];
-          const float x = dk[db][i], y = dk[db + NDB / 2][i];
-          dk[db][i] = x * c + y * sn;
-          dk[db + NDB / 2][i] = y * c - x * sn;
-        }
-    }
-    store_row_bf16<NDB>(a.dk + b * a.dk_sb + (int64_t)key * a.dk_st + (int64_t)hk * a.dk_sh, dk, a.scale, hh);
-    store_row_bf16<NDB>(a.dv + b * a.dv_sb + (int64_t)key * a.dv_st + (int64_t)hk * a.dv_sh, dv, 1.f, hh);
-  }
-}
-
-
 }  // namespace
 
 namespace pllm {
@@ -804,12 +514,7 @@ int attn_bwd_ks_key_block() { return KsCfg<128>::BK; }
 void attn_bwd_ks_launch(const AttnBwdArgs& a, hipStream_t st) {
   const dim3 grid(a.nkb_pass * a.B * a.Hkv), blk(256);
   if (a.D == 64) {
-    // two waves per SIMD at D = 64 (attn_bwd_ks8_kernel); the 4-wave kernel under PLLM_KS64_4W=1 (A/B)
-    static const bool four = std::getenv("PLLM_KS64_4W") != nullptr;
-    if (!four) {
-      if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks8_kernel<2>), grid, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((attn_bwd_ks8_kernel<0>), grid, dim3(512), 0, st, a);
-    } else if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks_kernel<64, 2>), grid, blk, 0, st, a);
+    if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks_kernel<64, 2>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((attn_bwd_ks_kernel<64, 0>), grid, blk, 0, st, a);
   } else {
     if (a.rope_cos) hipLaunchKernelGGL((attn_bwd_ks_kernel<128, 2>), grid, blk, 0, st, a);
