@@ -391,7 +391,9 @@ static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
 // MFMA groups (hipBLASLt's geometry; 4-18 % slower, its fused epilogues up to 40 % slower)
 // 4 (default): the ping-pong kernel of gemm_pp.hip (two wave groups one barrier apart, counted
 // waits): 4-6 % faster than this file's kernel on every fused epilogue measured (GELU' / SwiGLU' /
-// attention delta; gpurun_out/r4pp7_bench.jsonl, r4ab1_swiglu.jsonl), whole GPT-2 step +0.5 %
+// attention delta; gpurun_out/r4pp7_bench.jsonl, r4ab1_swiglu.jsonl), whole GPT-2 step +0.5 %.
+// This file's kernel remains the FALLBACK for what the ping-pong loop does not take (a single K-tile,
+// K < 128; the delta epilogue with T % 16 != 0); 0 / 2 select it for every shape (tests only)
 static int g_gemm_phased = 4;
 // CUs the persistent grids leave free, for RCCL kernels overlapping the backward (world > 1)
 static int g_gemm_reserve = 0;

@@ -248,21 +248,17 @@ def linear(x, weight, bias=None, bias_grad_external: bool = False):
 # ---------------------------------------------------------------------------
 # MLP with the activation in the GEMM epilogues (csrc/gemm.hip)
 # ---------------------------------------------------------------------------
-def gemm_config(kernel: Optional[str] = None, reserve_cus: Optional[int] = None,
-                persistent: Optional[bool] = None) -> bool:
-    """Configure the hand-written fused-epilogue TN GEMM (``torch.ops.pllm.gemm_tn``): ``kernel``
-    'pp' (ping-pong main loop, csrc/gemm_pp.hip) or 'r3' (round-3 persistent kernel, csrc/gemm.hip);
-    ``reserve_cus``: CUs its persistent grid leaves free (RCCL kernels run beside the backward at
-    world > 1); ``persistent`` False: the
-    ping-pong GEMM and weight-gradient kernels launch one workgroup per tile / work item instead of one
-    per CU, so a CU held by a concurrent RCCL kernel delays no tile list (the hardware deals the
-    tiles to the free CUs).  None keeps the current setting; returns False without the extension (CPU)."""
+def gemm_config(reserve_cus: Optional[int] = None, persistent: Optional[bool] = None) -> bool:
+    """Configure the hand-written fused-epilogue TN GEMM (``torch.ops.pllm.gemm_tn``: the ping-pong main loop of
+    csrc/gemm_pp.hip; shapes it does not take -- K < 128, the delta epilogue with T % 16 != 0 -- fall back to the
+    round-3 persistent loop of csrc/gemm.hip): ``reserve_cus``: CUs its persistent grid leaves free (RCCL
+    kernels run beside the backward at world > 1); ``persistent`` False: the ping-pong GEMM and weight-gradient
+    kernels launch one workgroup per tile / work item instead of one per CU, so a CU held by a concurrent RCCL
+    kernel delays no tile list (the hardware deals the tiles to the free CUs).  None keeps the current
+    setting; returns False without the extension (CPU)."""
     if not _lib.available():
         return False
-    if kernel is not None and kernel not in _lib.GEMM_KERNELS:
-        raise ValueError(f"gemm kernel {kernel!r}: one of {sorted(_lib.GEMM_KERNELS)}")
-    torch.ops.pllm.gemm_set_config(0, 0, _lib.GEMM_KERNELS[kernel] if kernel else -1,
-                                   -1 if reserve_cus is None else int(reserve_cus),
+    torch.ops.pllm.gemm_set_config(0, 0, -1, -1 if reserve_cus is None else int(reserve_cus),
                                    -1 if persistent is None else int(bool(persistent)))
     return True
 

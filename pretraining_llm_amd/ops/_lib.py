@@ -25,9 +25,6 @@ _HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SO_PATH = os.environ.get("PLLM_SO") or os.path.join(_HERE, "_C.so")  # PLLM_SO: A/B builds
 
 _lock = threading.Lock()
-# fused-epilogue TN GEMM main loops (gemm_set_config's `phased`): csrc/gemm_pp.hip's ping-pong
-# kernel, csrc/gemm.hip's round-3 persistent kernel
-GEMM_KERNELS = {"pp": 4, "r3": 0}
 _loaded = False
 _err: str | None = None
 
@@ -53,14 +50,11 @@ def load(raise_on_error: bool = False) -> bool:
                 # round (csrc/wgrad_pp.hip hybrid) instead of uniform split-K slices
                 if os.environ.get("PLLM_WGRAD_HY") and hasattr(torch.ops.pllm, "wgrad_set_hy"):
                     torch.ops.pllm.wgrad_set_hy(int(os.environ["PLLM_WGRAD_HY"]))
-                # PLLM_GEMM_KERNEL=pp|r3: main loop of the fused-epilogue TN GEMM (ops.gemm_config);
-                # PLLM_GEMM_RESERVE_CUS=n: CUs its persistent grid leaves to concurrent RCCL kernels;
-                kern = os.environ.get("PLLM_GEMM_KERNEL")
+                # PLLM_GEMM_RESERVE_CUS=n: CUs the persistent GEMM grids leave to concurrent RCCL kernels
                 res = os.environ.get("PLLM_GEMM_RESERVE_CUS")
                 per = os.environ.get("PLLM_GEMM_PERSISTENT")  # 0|1: persistent GEMM grids
-                if kern or res or per:
-                    torch.ops.pllm.gemm_set_config(0, 0, GEMM_KERNELS.get(kern, -1) if kern else -1,
-                                                   int(res) if res else -1, int(per) if per else -1)
+                if res or per:
+                    torch.ops.pllm.gemm_set_config(0, 0, -1, int(res) if res else -1, int(per) if per else -1)
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box
