@@ -171,7 +171,7 @@ constexpr int wp_dma_wait() {
 // (1,1) (1,0)), the next K-tile's piece group PH, the counted wait, a barrier, 16 MFMAs (+ the
 // bias MFMAs), a barrier.
 template <int PH, bool FIRST, bool BIAS>
-PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
                        f32x4 (&bacc)[2], bool dob, const char* slotp, const WPSrd& srd, int nsl) {
   constexpr int jh = PH >> 1;
   constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
@@ -183,8 +183,10 @@ PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
       for (int jj = 0; jj < 4; ++jj)
         fa[k][jj] = frag_tr(slotp + c.rd[jj & 1] + (unsigned)((4 * c.wr + 2 * jh + (jj >> 1)) * WIMG * 2 + 2048 * k));
   }
-  if constexpr (PH != 2) {
-    // X column tiles 2 p + ii: image 8 + 2 wc + p, columns 16 ii
+  // X column tiles 2 p + ii: image 8 + 2 wc + p, columns 16 ii -- both pairs kept (phase 3 reuses pair 0
+  // from phase 0 instead of reading it again: 48 instead of 56 transposed reads per K-tile and wave)
+  bf16x8 (&fb)[2][2] = fbp[p];
+  if constexpr (PH == 0 || PH == 1) {
 #pragma unroll
     for (int k = 0; k < 2; ++k)
 #pragma unroll
@@ -229,7 +231,7 @@ PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
 }
 
 template <bool FIRST, bool BIAS>
-PLLM_DEV void wp_ktile(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+PLLM_DEV void wp_ktile(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
                        f32x4 (&bacc)[2], bool dob, const uint16_t* smem, int s, const WPSrd& srd) {
   const char* slotp = reinterpret_cast<const char*>(smem + (s & 1) * WSLOT);
   const int nsl = (s + 1) & 1;
@@ -380,7 +382,7 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
 
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
-  bf16x8 fb[2][2];
+  bf16x8 fb[2][2][2];
   int s = 0;
   for (int i = 0; i < R; ++i) {
     const bool dob = BIAS && sg.tq == 0;
