@@ -180,12 +180,6 @@ WGRAD_BLAS_SHAPES = {(16384, 6144, 2048), (16384, 2048, 5504), (16384, 50304, 20
 FUSED_WGRAD_BIAS = _os.environ.get("PLLM_WGRAD_BIAS", "1") == "1"
 
 
-def sync_side_streams():
-    """No-op kept for the gradient readers that call it (every weight gradient now runs on the
-    current stream)."""
-    return None
-
-
 def _dgrad(dy, weight):
     """dx = dy @ weight.  When the optimizer keeps a transposed shadow of the weight
     (FlatAdamW ``transposed_shadow``), the product runs as dy @ (W^T)^T: hipBLASLt's
@@ -994,7 +988,6 @@ class _EmbeddingFn(torch.autograd.Function):
         tt = _acc_target(ctx.wte)
         tp = _acc_target(ctx.wpe) if has_pos else None
         if tt is not None and (not has_pos or tp is not None):
-            sync_side_streams()  # a tied LM head's dW may still be accumulating into wte's gradient
             _ops().embedding_bwd_acc(dx.contiguous(), idx, ctx.V, ctx.n_pos, has_pos, tt, tp)
             _notify(ctx.wte)
             if has_pos:

@@ -177,8 +177,6 @@ class DataParallelEngine:
         return hook
 
     def _launch(self, b):
-        from .. import ops
-        ops.sync_side_streams()  # side-stream weight gradients of this bucket must have landed
         bk = self.buckets[b]
         # lazy zeroing: a weight of this bucket that no writer touched this step (unused on this rank)
         # still holds last step's gradient -- zero it before it enters the all-reduce
@@ -207,8 +205,6 @@ class DataParallelEngine:
     def finish_grad_sync(self):
         """Launch any bucket not yet launched (unused params, no-overlap mode) and wait for all.
         Returns the gradient scale the optimizer must apply (1/world)."""
-        from .. import ops
-        ops.sync_side_streams()
         self.timer.backward_end()
         if self.world > 1:
             while self._next_launch < len(self.buckets):

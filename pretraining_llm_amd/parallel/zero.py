@@ -355,8 +355,6 @@ class ZeroDataParallelEngine:
         return hook
 
     def _launch(self, b):
-        from .. import ops
-        ops.sync_side_streams()
         opt = self.opt
         bs, be = opt.buckets[b]
         fs, fe, o = opt.own[b]
@@ -380,8 +378,6 @@ class ZeroDataParallelEngine:
             self.enabled = old
 
     def finish_grad_sync(self):
-        from .. import ops
-        ops.sync_side_streams()
         self.timer.backward_end()
         opt = self.opt
         if self.world > 1:
