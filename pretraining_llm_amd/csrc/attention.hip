@@ -568,9 +568,9 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     qvo[k] = (uint32_t)((row * (img == 0 ? a.q_st : a.do_st) + 8 * ch) * 2);
   }
   const unsigned lds_q = (unsigned)(uintptr_t)Ql, lds_o = (unsigned)(uintptr_t)Ol;
-  auto qdma_srd = [&](int it, i32x4v& qs, i32x4v& os) {
-    const int h = hk * G + it / per_head;
-    const int q0 = (qb_start + it % per_head) * BQ;
+  // (head h, first query row q0) of an iteration come from the loop's incremental counters: an
+  // it / per_head here was a run-time integer division (a long scalar chain) twice per iteration
+  auto qdma_srd = [&](int h, int q0, i32x4v& qs, i32x4v& os) {
     const int rows = a.T - q0;
     qs = srd_of(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st,
                 (uint32_t)(((int64_t)(rows - 1) * a.q_st + D) * 2));
@@ -582,16 +582,14 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     const int pc = wu * QPPW + k, img = pc / QNP, blk = pc % QNP;
     blds16(img == 0 ? qs : os, qvo[k], (img == 0 ? lds_q : lds_o) + 1024u * blk);
   };
-  auto qdma = [&](int it) {
+  auto qdma = [&](int h, int q0) {
     i32x4v qs, os;
-    qdma_srd(it, qs, os);
+    qdma_srd(h, q0, qs, os);
 #pragma unroll
     for (int k = 0; k < QPPW; ++k) qdma_piece(qs, os, k);
   };
   float rc = 0.f;
-  auto gload = [&](int it) {
-    const int h = hk * G + it / per_head;
-    const int q0 = (qb_start + it % per_head) * BQ;
+  auto gload = [&](int h, int q0) {
     // Q / dO rows of head h by buffer loads through a per-tile descriptor (scalar base = row
     // q0): rows past T read as zeros (range check), per-lane offsets loop-invariant
     const auto qrs = rows_rsrc(a.q + b * a.q_sb + (int64_t)h * a.q_sh + (int64_t)q0 * a.q_st, a.T - q0, a.q_st, D);
@@ -666,15 +664,15 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   if constexpr (QDMA) {
     if (total > 0) {
       // row constants of iteration 0 (their load retired by this write), then its Q / dO DMA
-      gload(0);
+      gload(hk * G, qb_start * BQ);
       if (tid < 2 * BQ) {
         const bool live = qb_start * BQ + (tid & (BQ - 1)) < a.T;
         rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;  // -lse*log2(e), -delta
       }
-      qdma(0);
+      qdma(hk * G, qb_start * BQ);
     }
   } else if (total > 0) {
-    gload(0);
+    gload(hk * G, qb_start * BQ);
   }
   // (head, query block) of iteration it, advanced incrementally (no integer division per step)
   int h = hk * G, qbi = qb_start;
@@ -693,6 +691,9 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
 #endif
   for (int it = 0; it < total; ++it, (++qbi == nqb) ? (qbi = qb_start, ++h) : 0) {
     const int q0 = qbi * BQ;
+    // the next iteration's (head, first query row)
+    const bool wrap = qbi + 1 == nqb;
+    const int hn = wrap ? h + 1 : h, qn0 = (wrap ? qb_start : qbi + 1) * BQ;
     PLLM_BSTAMP(7);
     // opaque per iteration: the (j, g) store offsets derived from it are formed next to their
     // stores instead of being hoisted out of the loop as 16 live registers
@@ -706,7 +707,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     PLLM_BSTAMP(0);
     if constexpr (QDMA) {
       flush_dq();
-      if (it + 1 < total) gload(it + 1);  // the next iteration's row constants
+      if (it + 1 < total) gload(hn, qn0);  // the next iteration's row constants
     }
 #pragma unroll
     for (int i = 0; i < (QDMA ? 0 : 2 * QPAIR); i += 2) {
@@ -728,7 +729,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       flush_dq();
       __syncthreads();
       PLLM_BSTAMP(1);
-      if (it + 1 < total) gload(it + 1);
+      if (it + 1 < total) gload(hn, qn0);
     }
     PLLM_BSTAMP(2);
 
@@ -883,11 +884,10 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         // every wave is past its Q / dO / row-constant reads: the next tile's row constants (their
         // load retired by this write, before the DMA below is in flight), then its Q / dO DMA
         if (tid < 2 * BQ) {
-          const int qn = (qbi + 1 == nqb ? qb_start : qbi + 1) * BQ;
-          const bool live = qn + (tid & (BQ - 1)) < a.T;
+          const bool live = qn0 + (tid & (BQ - 1)) < a.T;
           rowc[tid] = live ? (tid < BQ ? -rc * kLog2e : -rc) : 0.f;
         }
-        qdma(it + 1);
+        qdma(hn, qn0);
       }
     }
     PLLM_BSTAMP(4);
