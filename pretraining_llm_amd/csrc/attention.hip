@@ -54,6 +54,9 @@ constexpr float kLazyThr = 8.f;
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the forward loop
 #endif
+#ifndef PLLM_BWD_DQ_KREG
+#define PLLM_BWD_DQ_KREG 8  // D <= 64 backward: dQ-task K^T fragments held in registers (key steps 0..7 of 16)
+#endif
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
 #endif
@@ -630,6 +633,19 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // prefetched Q/dO) wait out their latency as well (same-box A/B: neutral at the GPT-2 / llama
   // shapes, where that latency was already covered).
   constexpr int NTPW = (NTASK + C::NW - 1) / C::NW;
+  // the dQ task's K^T fragments (A operand, key steps 0..KREG-1) in registers: the K block is fixed for
+  // the workgroup and, with one task per wave (NTPW == 1), so is the wave's d-block -- the same reads
+  // every iteration otherwise
+  constexpr int KREG = NTPW == 1 ? PLLM_BWD_DQ_KREG : 0;
+  bf16x8 kdq[KREG > 0 ? KREG : 1];
+  if constexpr (KREG > 0) {
+    const int tdb0 = __builtin_amdgcn_readfirstlane(w) % NDB;
+    const int dc0 = tdb0 * 32 + 16 * g1 + 4 * tp;
+    const int k0a = I::off(8 * hh + tq, dc0), k4a = I::off(8 * hh + tq + 4, dc0);
+#pragma unroll
+    for (int ks = 0; ks < KREG; ++ks)
+      kdq[ks] = cat_tr(ds_tr(Kl + 16 * ks * D + k0a), ds_tr(Kl + 16 * ks * D + k4a));
+  }
   u32x4 dqv[NTPW][2];
   uint16_t* dqp[NTPW];
 #pragma unroll
@@ -915,7 +931,8 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         const bf16x8 A = cat_tr(ds_tr(Sl + 16 * ks * BQ + sa0), ds_tr(Sl + 16 * ks * BQ + sa4));
-        const bf16x8 Bf = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
+        const bf16x8 Bf = ks < KREG ? kdq[ks < KREG ? ks : 0]
+                                    : cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
         acc = mfma32(Bf, A, acc);
       }
       float lo[8], hi[8];
