@@ -169,8 +169,8 @@ class Block(_gpt.Block):
 
     def forward(self, x, residual=None, rope=None):
         m, res = super().forward(x, residual, rope)
-        if residual is None:
-            return m + res          # reference semantics: a single tensor out
+        if residual is None:        # reference semantics: a single tensor out
+            return m if res is None else m + res  # (None: the projections added the stream already)
         return m, res
 
     def forward_embedding(self, x, residual=None, rope=None):

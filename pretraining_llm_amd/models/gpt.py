@@ -71,17 +71,24 @@ class Attention(nn.Module):
         self.proj = nn.Linear(C, C, bias=cfg.bias) if cfg.attn_out_proj else None
 
     def forward(self, x, rope=None, fuse_out_bias: bool = False):
+        return self.forward_res(x, rope, fuse_out_bias)[0]
+
+    def forward_res(self, x, rope=None, fuse_out_bias: bool = False, residual=None):
+        """(y + residual, True) when the fused projection adds the block's residual stream in its GEMM
+        (ops.resid_gemm_ok), else (y, False) and the caller's norm adds it."""
         qkv = ops.linear(x, self.qkv.weight, self.qkv.bias)
         cos, sin = rope if rope is not None else (None, None)
         if self.proj is not None and ops.attn_proj_ok(qkv, self.n_head, self.n_kv_head, self.proj.weight,
                                                       self.proj.bias):
             # the projection's data gradient also emits the attention backward's row constants
+            r = residual if ops.resid_gemm_ok(residual, self.proj.weight) else None
             return ops.attention_proj(qkv, self.n_head, self.n_kv_head, self.proj.weight, self.proj.bias,
-                                      rope_cos=cos, rope_sin=sin, bias_grad_external=fuse_out_bias)
+                                      rope_cos=cos, rope_sin=sin, bias_grad_external=fuse_out_bias,
+                                      residual=r), r is not None
         y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is not None:
             y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
-        return y
+        return y, False
 
     # --- KV-cache decode -------------------------------------------------
     def forward_cached(self, x, cache, layer_idx, pos, rope=None, qkv=None):
@@ -162,10 +169,19 @@ class MLP(nn.Module):
 
     def forward(self, x, fuse_out_bias: bool = False):
         """``fuse_out_bias``: the down-projection's bias gradient is emitted by the next norm."""
+        return self.forward_res(x, fuse_out_bias)[0]
+
+    def forward_res(self, x, fuse_out_bias: bool = False, residual=None):
+        """(y + residual, True) when the fused MLP's down projection adds the residual stream in its GEMM
+        (ops.resid_gemm_ok), else (y, False)."""
         if ops.fused_mlp_ok(x, self.hidden.weight, self.hidden.bias, self.proj.weight, self.kind):
             # activation in the GEMM epilogues (csrc/gemm.hip)
+            r = residual if ops.resid_gemm_ok(residual, self.proj.weight) else None
             return ops.fused_mlp(x, self.hidden.weight, self.hidden.bias, self.proj.weight, self.proj.bias,
-                                 self.kind, out_bias_ext=fuse_out_bias)
+                                 self.kind, out_bias_ext=fuse_out_bias, residual=r), r is not None
+        return self._forward_unfused(x, fuse_out_bias), False
+
+    def _forward_unfused(self, x, fuse_out_bias: bool):
         if self.kind == "swiglu" and ops.fused_swiglu_ok(x, self.hidden.weight, self.hidden.bias,
                                                           self.proj.weight, self.proj.bias):
             # SwiGLU backward in the down-projection's data-gradient epilogue (csrc/gemm.hip)
@@ -200,9 +216,18 @@ class Block(nn.Module):
         fuse = ops._hip(x) and torch.is_grad_enabled() and self.attn.proj is not None \
             and self.attn.proj.bias is not None and getattr(self.attn, "fused_bias_ok", True)
         h, res = self.ln1(x, residual, x_bias=x_bias)
-        a = self.attn(h, rope, fuse_out_bias=fuse)
-        h2, res2 = self.ln2(a, res, x_bias=self.attn.proj.bias if fuse else None)
-        return self.mlp(h2, fuse_out_bias=fuse and fuse_mlp_out_bias), res2
+        # the output projections may add the residual stream in their GEMMs (ops.resid_gemm_ok): then the
+        # next norm gets the stream itself (residual None) and the block returns (stream, None)
+        if hasattr(self.attn, "forward_res"):
+            a, a_res = self.attn.forward_res(h, rope, fuse, res)
+        else:
+            a, a_res = self.attn(h, rope, fuse_out_bias=fuse), False
+        h2, res2 = self.ln2(a, None if a_res else res, x_bias=self.attn.proj.bias if fuse else None)
+        if hasattr(self.mlp, "forward_res"):
+            m, m_res = self.mlp.forward_res(h2, fuse and fuse_mlp_out_bias, res2)
+        else:
+            m, m_res = self.mlp(h2, fuse_out_bias=fuse and fuse_mlp_out_bias), False
+        return m, (None if m_res else res2)
 
     def fused_out_bias(self, x):
         """The bias the next norm must take as ``x_bias`` when fuse_mlp_out_bias=True (or None)."""

@@ -299,7 +299,7 @@ class _FusedMLPFn(torch.autograd.Function):
     Reference: the MLP of /root/reference/src/models/mlp.py:24-26,39-41."""
 
     @staticmethod
-    def forward(ctx, x, w1, b1, w2, b2, gelu, out_bias_ext):
+    def forward(ctx, x, w1, b1, w2, b2, gelu, out_bias_ext, res=None):
         C = x.shape[-1]
         x2 = x.reshape(-1, C)
         if not FUSED_MLP_FWD and not gelu and LT_RELU_FWD:
@@ -324,6 +324,10 @@ class _FusedMLPFn(torch.autograd.Function):
         ctx.gelu, ctx.ext = gelu, out_bias_ext
         ctx.params = (w1, b1, w2, b2)
         ctx.xshape = x.shape
+        ctx.has_res = res is not None
+        if res is not None:  # the block's residual stream added in the GEMM (one rounding, see resid_gemm_ok)
+            return _ops().gemm_lt(a, w2, b2, 0, not torch.are_deterministic_algorithms_enabled(),
+                                  res.reshape(-1, C))[0].view(*x.shape[:-1], C)
         return F.linear(a, w2, b2).view(*x.shape[:-1], C)
 
     @staticmethod
@@ -368,12 +372,29 @@ class _FusedMLPFn(torch.autograd.Function):
             _notify(w1)
         if dx is not None:
             dx = dx.view(ctx.xshape)
-        return dx, dw1, db1, dw2, db2, None, None
+        return dx, dw1, db1, dw2, db2, None, None, (dy if ctx.has_res else None)
 
 
-def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False):
+def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False, residual=None):
+    """``residual``: y + residual is returned (added by the down projection's GEMM, resid_gemm_ok)."""
     ext = bool(out_bias_ext and b2 is not None and not (_TORCH_OPS & {"norm", "act"}))
-    return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext)
+    return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext, residual)
+
+
+# PLLM_RESID_GEMM=1|0: a block's residual add done by its output projection's GEMM (hipBLASLt beta = 1,
+# s = residual + x W^T + b in one rounding, csrc/blaslt.cpp gemm_lt) instead of by the next norm, which
+# then reads one stream instead of two and writes one instead of two.  Round-4 measurement
+# (profiles/r4_residual_in_gemm_negative.md): -3.9 / -15.9 us per GPT-2 layer (attention out / MLP down),
+# but +105 us at llama's down projection (C 2048, K 5504: no fast beta = 1 solution), so output widths
+# <= RESID_GEMM_MAX_C only (GPT-2 small / medium).
+RESID_GEMM = _os.environ.get("PLLM_RESID_GEMM", "1") == "1"
+RESID_GEMM_MAX_C = 1024
+
+
+def resid_gemm_ok(res, w) -> bool:
+    return (RESID_GEMM and res is not None and torch.is_grad_enabled() and _hip(res) and not _TORCH_OPS
+            and res.dtype == torch.bfloat16 and res.is_contiguous() and w.shape[0] <= RESID_GEMM_MAX_C
+            and res.shape[-1] == w.shape[0])
 
 
 def fused_swiglu_ok(x, w1, b1, w2, b2) -> bool:
@@ -668,7 +689,7 @@ class _AttnProjFn(torch.autograd.Function):
     dim 64 (a wave's 64 output columns are one head).  Same math as _FlashAttnPacked + _LinearFn."""
 
     @staticmethod
-    def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin, w, b, bias_ext):
+    def forward(ctx, qkv, H, Hkv, causal, scale, cos, sin, w, b, bias_ext, res=None):
         B, T, W = qkv.shape
         D = W // (H + 2 * Hkv)
         q, k, v = _split_qkv(qkv, H, Hkv, D)
@@ -683,6 +704,11 @@ class _AttnProjFn(torch.autograd.Function):
         ctx.save_for_backward(qkv, qk, o, lse, cos, sin)
         ctx.cfg = (H, Hkv, D, causal, scale)
         ctx.w, ctx.b, ctx.bias_ext = w, b, bias_ext
+        ctx.has_res = res is not None
+        if res is not None:  # the block's residual stream added in the GEMM (resid_gemm_ok)
+            C = w.shape[0]
+            return _ops().gemm_lt(o.view(B * T, H * D), w, b, 0, not torch.are_deterministic_algorithms_enabled(),
+                                  res.reshape(-1, C))[0].view(B, T, C)
         return F.linear(o.view(B, T, H * D), w, b)
 
     @staticmethod
@@ -727,7 +753,7 @@ class _AttnProjFn(torch.autograd.Function):
         _attn_ws(qkv.device)
         _ops().attn_bwd(do2.view(B, T, H, D), q, k, v, o, lse, dq, dk, dv, causal, scale, cos, sin, qk is None,
                         delta)
-        return dqkv, None, None, None, None, None, None, dw, db, None
+        return dqkv, None, None, None, None, None, None, dw, db, None, (dy if ctx.has_res else None)
 
 
 # PLLM_ATTN_PROJ_FUSED=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
@@ -750,12 +776,13 @@ def attn_proj_ok(qkv, n_head: int, n_kv_head: int, w, b) -> bool:
 
 
 def attention_proj(qkv, n_head: int, n_kv_head: int, w, b, causal: bool = True, scale: Optional[float] = None,
-                   rope_cos=None, rope_sin=None, bias_grad_external: bool = False):
-    """``linear(attention_packed(qkv, ...), w, b)`` with the fused backward (see _AttnProjFn)."""
+                   rope_cos=None, rope_sin=None, bias_grad_external: bool = False, residual=None):
+    """``linear(attention_packed(qkv, ...), w, b)`` (+ ``residual``, added by the GEMM) with the fused
+    backward (see _AttnProjFn)."""
     D = qkv.shape[-1] // (n_head + 2 * n_kv_head)
     scale = scale if scale is not None else 1.0 / math.sqrt(D)
     ext = bool(bias_grad_external and b is not None and not (_TORCH_OPS & {"norm", "act"}))
-    return _AttnProjFn.apply(qkv, n_head, n_kv_head, causal, scale, rope_cos, rope_sin, w, b, ext)
+    return _AttnProjFn.apply(qkv, n_head, n_kv_head, causal, scale, rope_cos, rope_sin, w, b, ext, residual)
 
 
 _ATTN_WS_MB = [None]
