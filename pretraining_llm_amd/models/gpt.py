@@ -87,7 +87,9 @@ class Attention(nn.Module):
                                       residual=r), r is not None
         y = ops.attention_packed(qkv, self.n_head, self.n_kv_head, causal=True, rope_cos=cos, rope_sin=sin)
         if self.proj is not None:
-            y = ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias)
+            r = residual if ops.resid_gemm_ok(residual, self.proj.weight) else None
+            return ops.linear(y, self.proj.weight, self.proj.bias, bias_grad_external=fuse_out_bias,
+                              residual=r), r is not None
         return y, False
 
     # --- KV-cache decode -------------------------------------------------

@@ -120,10 +120,16 @@ class _LinearFn(torch.autograd.Function):
     alone instead of re-reading dy."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias, bias_grad_external):
+    def forward(ctx, x, weight, bias, bias_grad_external, res=None):
         ctx.save_for_backward(x, weight)
         ctx.w, ctx.b = weight, bias
         ctx.bias_ext = bias_grad_external
+        ctx.has_res = res is not None
+        if res is not None:  # + the residual stream, added by the GEMM (resid_gemm_ok)
+            N = weight.shape[0]
+            return _ops().gemm_lt(x.reshape(-1, x.shape[-1]), weight, bias, 0,
+                                  not torch.are_deterministic_algorithms_enabled(),
+                                  res.reshape(-1, N))[0].view(*x.shape[:-1], N)
         return F.linear(x, weight, bias)
 
     @staticmethod
@@ -156,7 +162,7 @@ class _LinearFn(torch.autograd.Function):
             else:
                 db = _ops().bias_grad(dy2.contiguous())
         ctx.w = ctx.b = None
-        return dx, dw, db, None
+        return dx, dw, db, None, (dy if ctx.has_res else None)
 
 
 import os as _os
@@ -222,12 +228,15 @@ def _weight_grad(dy2, x2, tgt, btgt=None, overwrite: bool = False):
     return dy2.t() @ x2
 
 
-def linear(x, weight, bias=None, bias_grad_external: bool = False):
+def linear(x, weight, bias=None, bias_grad_external: bool = False, residual=None):
+    """``residual`` (only when resid_gemm_ok holds -- the caller checks): x W^T + b + residual."""
     if _hip_op("linear", x) and torch.is_grad_enabled() and weight.requires_grad:
         # a bias gradient is left to the consumer's kernel only while that consumer (norm / act)
         # runs on the HIP kernels
         ext = bias_grad_external and bias is not None and not (_TORCH_OPS & {"norm", "act"})
-        return _LinearFn.apply(x, weight, bias, ext)
+        return _LinearFn.apply(x, weight, bias, ext, residual)
+    if residual is not None:
+        return F.linear(x, weight, bias) + residual
     if _hip(x) and not (torch.is_grad_enabled() and x.requires_grad):
         # decode-sized inference projections (<= 8 token rows): weight-streaming skinny GEMM
         # (csrc/gemv.hip) instead of the training-sized library tiles
@@ -385,16 +394,17 @@ def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False, residual=
 # s = residual + x W^T + b in one rounding, csrc/blaslt.cpp gemm_lt) instead of by the next norm, which
 # then reads one stream instead of two and writes one instead of two.  Round-4 measurement
 # (profiles/r4_residual_in_gemm_negative.md): -3.9 / -15.9 us per GPT-2 layer (attention out / MLP down),
-# but +105 us at llama's down projection (C 2048, K 5504: no fast beta = 1 solution), so output widths
-# <= RESID_GEMM_MAX_C only (GPT-2 small / medium).
+# -14.5 us at llama's attention output projection, but +105 us at its down projection (2048 x 5504: no fast
+# beta = 1 solution among hipBLASLt's candidates), so weights of at most RESID_GEMM_MAX_W elements only
+# (every measured-good shape: GPT-2 small / medium projections, llama's W_o; not llama / ref-3b MLP downs).
 RESID_GEMM = _os.environ.get("PLLM_RESID_GEMM", "1") == "1"
-RESID_GEMM_MAX_C = 1024
+RESID_GEMM_MAX_W = 2048 * 3072
 
 
 def resid_gemm_ok(res, w) -> bool:
     return (RESID_GEMM and res is not None and torch.is_grad_enabled() and _hip(res) and not _TORCH_OPS
-            and res.dtype == torch.bfloat16 and res.is_contiguous() and w.shape[0] <= RESID_GEMM_MAX_C
-            and res.shape[-1] == w.shape[0])
+            and res.dtype == torch.bfloat16 and res.is_contiguous() and w.numel() <= RESID_GEMM_MAX_W
+            and res.shape[-1] == w.shape[0] and w.shape[1] % 8 == 0)
 
 
 def fused_swiglu_ok(x, w1, b1, w2, b2) -> bool:

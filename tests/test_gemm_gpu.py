@@ -281,32 +281,39 @@ def test_attn_proj_fused_matches_unfused(bias, ext, D, Hkv):
         assert _rel(a, c) < 1e-2, (n, _rel(a, c))
 
 
-def test_resid_gemm_block_matches_norm_side_add(monkeypatch):
+@pytest.mark.parametrize("preset", ["gpt2-small", "llama-1.3b"])
+def test_resid_gemm_block_matches_norm_side_add(preset, monkeypatch):
     """A block's residual add done by the output projections' GEMMs (ops.resid_gemm_ok: hipBLASLt
-    beta = 1 inside attention_proj / fused_mlp) vs by the next norm: the block hands the stream on with
-    residual None, and a two-block GPT-2-shaped model's loss and every parameter gradient match the
-    norm-side form (one bf16 rounding of the stream instead of two)."""
+    beta = 1 in attention_proj / fused_mlp / linear) vs by the next norm.  GPT-2: both projections take
+    it and the block hands the stream on with residual None; llama: its attention output projection takes
+    it (the SwiGLU MLP does not), so the block still returns a residual.  A two-block model's loss and every
+    parameter gradient match the norm-side form (one bf16 rounding of the stream instead of two)."""
     from pretraining_llm_amd import ops
     from pretraining_llm_amd.models import GPT, get_preset
     torch.manual_seed(31)
-    cfg = get_preset("gpt2-small").replace(n_blocks=2)
+    cfg = get_preset(preset).replace(n_blocks=2)
     model = GPT(cfg).to(device=DEV, dtype=torch.bfloat16)
-    idx = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
-    tgt = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    T = 256
+    idx = torch.randint(0, cfg.vocab_size, (2, T), device=DEV)
+    tgt = torch.randint(0, cfg.vocab_size, (2, T), device=DEV)
     blk = model.attn_blocks[0]
-    x0 = torch.randn(2, 256, cfg.n_embed, device=DEV).bfloat16()
-    r0 = torch.randn(2, 256, cfg.n_embed, device=DEV).bfloat16()
+    rope = model.rope_tables(DEV, T)
+    x0 = torch.randn(2, T, cfg.n_embed, device=DEV).bfloat16()
+    r0 = torch.randn(2, T, cfg.n_embed, device=DEV).bfloat16()
+    gpt2 = preset.startswith("gpt2")
 
     def run(on):
         monkeypatch.setattr(ops, "RESID_GEMM", on)
+        assert ops.resid_gemm_ok(r0, blk.attn.proj.weight) == on
         model.zero_grad(set_to_none=True)
         with torch.enable_grad():
-            m, r = blk(x0.clone().requires_grad_(), r0.clone(), None, None, True)
-            assert (r is None) == on, "the residual-in-GEMM path did not run" if on else "unexpected fusion"
-            s = m if r is None else m.float() + r.float()
+            m, r = blk(x0.clone().requires_grad_(), r0.clone(), rope, None, True)
+            if gpt2:
+                assert (r is None) == on, "the residual-in-GEMM path did not run" if on else "unexpected fusion"
+            s = m.float() if r is None else m.float() + r.float()
             _, loss = model(idx, tgt)
             loss.backward()
-        return s.detach().float(), loss.detach().float(), [p.grad.detach().float().clone() for p in model.parameters()]
+        return s.detach(), loss.detach().float(), [p.grad.detach().float().clone() for p in model.parameters()]
 
     s1, l1, g1 = run(True)
     s0, l0, g0 = run(False)
