@@ -323,6 +323,31 @@ def test_resid_gemm_block_matches_norm_side_add(preset, monkeypatch):
         assert _rel(a, b) < 3e-2, (i, _rel(a, b))
 
 
+def test_resid_gemm_under_activation_checkpointing():
+    """The residual-in-GEMM blocks recomputed under activation checkpointing (every block checkpointed) give
+    the loss and gradients of the stored-activation run (same kernels, same cached GEMM plans)."""
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.models import GPT, get_preset
+    assert ops.RESID_GEMM
+    torch.manual_seed(37)
+    cfg = get_preset("gpt2-small").replace(n_blocks=2)
+    m1 = GPT(cfg).to(device=DEV, dtype=torch.bfloat16)
+    m2 = GPT(cfg.replace(activation_checkpointing=True)).to(device=DEV, dtype=torch.bfloat16)
+    m2.load_state_dict(m1.state_dict())
+    idx = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    tgt = torch.randint(0, cfg.vocab_size, (2, 256), device=DEV)
+    assert m2.checkpointed_blocks(idx) == 2 and m1.checkpointed_blocks(idx) == 0
+    losses = []
+    with torch.enable_grad():
+        for m in (m1, m2):
+            _, loss = m(idx, tgt)
+            loss.backward()
+            losses.append(loss.item())
+    assert abs(losses[0] - losses[1]) < 1e-3 * abs(losses[0])
+    for (n, p1), p2 in zip(m1.named_parameters(), m2.parameters()):
+        assert _rel(p2.grad.float(), p1.grad.float()) < 1e-2, (n, _rel(p2.grad.float(), p1.grad.float()))
+
+
 @pytest.mark.parametrize("phased", [0, 4])
 @pytest.mark.parametrize("reserve", [0, 32, 240])
 def test_gemm_tn_reserved_cus(phased, reserve):
