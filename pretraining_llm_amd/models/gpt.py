@@ -218,7 +218,8 @@ class Block(nn.Module):
         fuse = ops._hip(x) and torch.is_grad_enabled() and self.attn.proj is not None \
             and self.attn.proj.bias is not None and getattr(self.attn, "fused_bias_ok", True)
         h, res = self.ln1(x, residual, x_bias=x_bias)
-        # the output projections may add the residual stream in their GEMMs (ops.resid_gemm_ok): then the
+        # the output projections may add the residual stream in their GEMMs (ops.resid_gemm_ok; the reference's
+        # x + attn(ln1(x)) / x + mlp(ln2(x)), /root/reference/src/models/transformer_block.py:44,46): then the
         # next norm gets the stream itself (residual None) and the block returns (stream, None)
         if hasattr(self.attn, "forward_res"):
             a, a_res = self.attn.forward_res(h, rope, fuse, res)

@@ -390,7 +390,8 @@ def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False, residual=
     return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext, residual)
 
 
-# PLLM_RESID_GEMM=1|0: a block's residual add done by its output projection's GEMM (hipBLASLt beta = 1,
+# PLLM_RESID_GEMM=1|0: a block's residual add (reference: x = x + attn(ln1(x)); x = x + mlp(ln2(x)),
+# /root/reference/src/models/transformer_block.py:44,46) done by its output projection's GEMM (hipBLASLt beta = 1,
 # s = residual + x W^T + b in one rounding, csrc/blaslt.cpp gemm_lt) instead of by the next norm, which
 # then reads one stream instead of two and writes one instead of two.  Round-4 measurement
 # (profiles/r4_residual_in_gemm_negative.md): -3.9 / -15.9 us per GPT-2 layer (attention out / MLP down),
