@@ -54,8 +54,8 @@ constexpr float kLazyThr = 8.f;
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the forward loop
 #endif
-#ifndef PLLM_BWD_DQ_KREG
-#define PLLM_BWD_DQ_KREG 8  // D <= 64 backward: dQ-task K^T fragments held in registers (key steps 0..7 of 16)
+#ifndef PL_BWD_DQ_KREG
+#define PL_BWD_DQ_KREG 8  // D <= 64 backward: dQ-task K^T fragments held in registers (key steps 0..7 of 16)
 #endif
 #ifndef PLLM_BWD_STAMPS
 #define PLLM_BWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the D <= 64 backward loop
@@ -243,16 +243,16 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
       st_acc[i] += now - ts_prev;
       ts_prev = now;
     };
-#define PLLM_STAMP(i) stamp(i)
+#define PL_STAMP(i) stamp(i)
 #else
-#define PLLM_STAMP(i)
+#define PL_STAMP(i)
 #endif
     const int buf = t & 1;
     if (t + 1 < ntiles) {
       if constexpr (DMA) gdma(t + 1, buf ^ 1);
       else gload(t + 1);
     }
-    PLLM_STAMP(0);
+    PL_STAMP(0);
     const int kv0 = t * BN;
     // which of this wave's blocks see keys of this tile: a compile-time mask per code
     // path, so no MFMA is predicated (an if-converted MFMA keeps both results live)
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 2);
       }
-      PLLM_STAMP(1);
+      PL_STAMP(1);
       bf16x8 pf[QB][4];
 #pragma unroll
       for (int j = 0; j < QB; ++j) {
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
           pf[j][2 * kb + 1] = pack_frag(s[j][kb], 1);
         }
       }
-      PLLM_STAMP(2);
+      PL_STAMP(2);
 #pragma unroll
       for (int kst = 0; kst < 4; ++kst) {
 #pragma unroll
@@ -369,18 +369,18 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
     if (mask == 3) tile(std::integral_constant<int, 3>{});
     else if (mask == 1) tile(std::integral_constant<int, 1>{});
     else if (QB > 1 && mask == 2) tile(std::integral_constant<int, 2>{});
-    PLLM_STAMP(3);
+    PL_STAMP(3);
     if constexpr (DMA) vm_wait_all();
     else if (t + 1 < ntiles) swrite(buf ^ 1, t + 1, buf ^ 1);
-    PLLM_STAMP(4);
+    PL_STAMP(4);
     __syncthreads();
-    PLLM_STAMP(5);
+    PL_STAMP(5);
 #if PLLM_FWD_STAMPS
     st_acc[6] += 1;
     st_acc[7] += (uint64_t)mask;
 #endif
   }
-#undef PLLM_STAMP
+#undef PL_STAMP
 
 #if PLLM_FWD_STAMPS
   if (a.stamps && lane == 0) {
@@ -636,7 +636,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
   // the dQ task's K^T fragments (A operand, key steps 0..KREG-1) in registers: the K block is fixed for
   // the workgroup and, with one task per wave (NTPW == 1), so is the wave's d-block -- the same reads
   // every iteration otherwise
-  constexpr int KREG = NTPW == 1 ? PLLM_BWD_DQ_KREG : 0;
+  constexpr int KREG = NTPW == 1 ? PL_BWD_DQ_KREG : 0;
   bf16x8 kdq[KREG > 0 ? KREG : 1];
   if constexpr (KREG > 0) {
     const int tdb0 = __builtin_amdgcn_readfirstlane(w) % NDB;
@@ -701,16 +701,16 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     st_acc[i] += now - ts_prev;
     ts_prev = now;
   };
-#define PLLM_BSTAMP(i) stamp(i)
+#define PL_BSTAMP(i) stamp(i)
 #else
-#define PLLM_BSTAMP(i)
+#define PL_BSTAMP(i)
 #endif
   for (int it = 0; it < total; ++it, (++qbi == nqb) ? (qbi = qb_start, ++h) : 0) {
     const int q0 = qbi * BQ;
     // the next iteration's (head, first query row)
     const bool wrap = qbi + 1 == nqb;
     const int hn = wrap ? h + 1 : h, qn0 = (wrap ? qb_start : qbi + 1) * BQ;
-    PLLM_BSTAMP(7);
+    PL_BSTAMP(7);
     // opaque per iteration: the (j, g) store offsets derived from it are formed next to their
     // stores instead of being hoisted out of the loop as 16 live registers
     int fs = fs0;
@@ -720,7 +720,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
     // join and wait vmcnt(0) again before the next prefetch -- on the fresh dQ stores
     vm_wait_all();
     __syncthreads();  // previous iteration's readers of Q/dO/dS are done (QDMA: this one's tiles landed)
-    PLLM_BSTAMP(0);
+    PL_BSTAMP(0);
     if constexpr (QDMA) {
       flush_dq();
       if (it + 1 < total) gload(hn, qn0);  // the next iteration's row constants
@@ -744,10 +744,10 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       }
       flush_dq();
       __syncthreads();
-      PLLM_BSTAMP(1);
+      PL_BSTAMP(1);
       if (it + 1 < total) gload(hn, qn0);
     }
-    PLLM_BSTAMP(2);
+    PL_BSTAMP(2);
 
     // rows past T need no mask: their Q / dO rows are zero-filled, their row constants 0
     const bool need_mask = (k0 + BK > a.S) || (a.causal && k0 + BK - 1 > q0 + off);
@@ -893,7 +893,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         body(std::integral_constant<int, 1>{}, TT{});
       }
     }
-    PLLM_BSTAMP(3);
+    PL_BSTAMP(3);
     __syncthreads();
     if constexpr (QDMA) {
       if (it + 1 < total) {
@@ -906,7 +906,7 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
         qdma(hn, qn0);
       }
     }
-    PLLM_BSTAMP(4);
+    PL_BSTAMP(4);
     // dQ partial of this key block: dQ_kb[q, d] = dS[q, keys] K[keys, d], one (q sub-block,
     // d-block) task per wave (NTASK / NW of them), summed over all BK keys on chip, stored into
     // this pass's fp32 slab of the key block.
@@ -946,12 +946,12 @@ __global__ __launch_bounds__((BwdCfg<D>::NT), (BwdCfg<D>::MIN_WAVES)) void attn_
       dqp[ti] = a.dq_acc + (kb - a.kb0) * a.slab +
                 ((((int64_t)b * a.H + h) * a.nqt + (qt0 >> 5)) * NDB + tdb) * 1024 + lane * 16;
     }
-    PLLM_BSTAMP(5);
+    PL_BSTAMP(5);
 #if PLLM_BWD_STAMPS
     st_acc[6] += 1;
 #endif
   }
-#undef PLLM_BSTAMP
+#undef PL_BSTAMP
 #if PLLM_BWD_STAMPS
   if (a.stamps && lane == 0) {
     unsigned long long* stp = a.stamps + ((int64_t)blockIdx.x * C::NW + w) * 9;

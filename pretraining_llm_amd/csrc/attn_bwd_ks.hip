@@ -21,8 +21,8 @@
 #include "common.h"
 #include "kernels.h"
 
-#ifndef PLLM_KS_DQ_KREG
-#define PLLM_KS_DQ_KREG 4  // dQ-task K^T fragments held in registers (key steps 0..PLLM_KS_DQ_KREG-1 of 16)
+#ifndef PL_KS_DQ_KREG
+#define PL_KS_DQ_KREG 4  // dQ-task K^T fragments held in registers (key steps 0..PL_KS_DQ_KREG-1 of 16)
 #endif
 
 namespace {
@@ -70,11 +70,11 @@ struct KsCfg {
 // plain additions.
 template <int W>
 struct ImgT {
-  static PLLM_DEV int f(int r) {
+  static PL_DEV int f(int r) {
     if constexpr (W == 32) return (r >> 1) & 3;
     else return (((r >> 1) & 1) << 2) | ((r & 1) << 1) | ((r >> 2) & 1);
   }
-  static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+  static PL_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
 };
 
 template <int D, int ROPE>
@@ -212,11 +212,11 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
   const int qc = 32 * tq_blk + 16 * g1 + 4 * tp, dc = 32 * tdb + 16 * g1 + 4 * tp;
   const int sa00 = IT::off(8 * hh + tq, qc), sa40 = IT::off(8 * hh + tq + 4, qc);
   const int ka00 = I::off(8 * hh + tq, dc), ka40 = I::off(8 * hh + tq + 4, dc);
-  // the dQ task's K^T fragments of key steps 0..PLLM_KS_DQ_KREG-1 in registers: the K block and the wave's d-block
+  // the dQ task's K^T fragments of key steps 0..PL_KS_DQ_KREG-1 in registers: the K block and the wave's d-block
   // are fixed, so these reads would repeat every slice (the dQ phase runs at the LDS read roof)
-  bf16x8 kdq[PLLM_KS_DQ_KREG > 0 ? PLLM_KS_DQ_KREG : 1];
+  bf16x8 kdq[PL_KS_DQ_KREG > 0 ? PL_KS_DQ_KREG : 1];
 #pragma unroll
-  for (int ks = 0; ks < PLLM_KS_DQ_KREG; ++ks) kdq[ks] = cat_tr(ds_tr(Kl + 16 * ks * D + ka00), ds_tr(Kl + 16 * ks * D + ka40));
+  for (int ks = 0; ks < PL_KS_DQ_KREG; ++ks) kdq[ks] = cat_tr(ds_tr(Kl + 16 * ks * D + ka00), ds_tr(Kl + 16 * ks * D + ka40));
 
 #if PLLM_BWD_STAMPS
   // diagnostic build: per-wave s_memtime sums of the slice phases (host: PLLM_BWD_STAMPS=1 prints them)
@@ -441,14 +441,14 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_ks_kernel(AttnBwdArgs a) {
       bf16x8 fa[QA + 1], fb[QA + 1];
       auto rd_q = [&](int ks) {
         fa[ks % (QA + 1)] = cat_tr(ds_tr(Sd + 16 * ks * BQ + sa0), ds_tr(Sd + 16 * ks * BQ + sa4));
-        if (ks >= PLLM_KS_DQ_KREG) fb[ks % (QA + 1)] = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
+        if (ks >= PL_KS_DQ_KREG) fb[ks % (QA + 1)] = cat_tr(ds_tr(Kl + 16 * ks * D + ka0), ds_tr(Kl + 16 * ks * D + ka4));
       };
 #pragma unroll
       for (int ks = 0; ks < QA; ++ks) rd_q(ks);
 #pragma unroll
       for (int ks = 0; ks < BK / 16; ++ks) {
         if (ks + QA < BK / 16) rd_q(ks + QA);
-        const bf16x8& kb_ = ks < PLLM_KS_DQ_KREG ? kdq[ks < PLLM_KS_DQ_KREG ? ks : 0] : fb[ks % (QA + 1)];
+        const bf16x8& kb_ = ks < PL_KS_DQ_KREG ? kdq[ks < PL_KS_DQ_KREG ? ks : 0] : fb[ks % (QA + 1)];
         if (ks == 0) mfma_v0(acc, kb_, fa[0]);
         else mfma_v(acc, kb_, fa[ks % (QA + 1)]);
         __builtin_amdgcn_sched_barrier(0);

@@ -10,25 +10,25 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-PLLM_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+PL_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-PLLM_DEV s16x4 ds_tr(const uint16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
-PLLM_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
+PL_DEV s16x4 ds_tr(const uint16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
+PL_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
   s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
-PLLM_DEV bf16x8 as_frag(const u32x4& v) { return __builtin_bit_cast(bf16x8, v); }
-PLLM_DEV bf16x8 zero_frag() { return __builtin_bit_cast(bf16x8, u32x4{0u, 0u, 0u, 0u}); }
-PLLM_DEV f32x16 zero16() {
+PL_DEV bf16x8 as_frag(const u32x4& v) { return __builtin_bit_cast(bf16x8, v); }
+PL_DEV bf16x8 zero_frag() { return __builtin_bit_cast(bf16x8, u32x4{0u, 0u, 0u, 0u}); }
+PL_DEV f32x16 zero16() {
   f32x16 z;
 #pragma unroll
   for (int i = 0; i < 16; ++i) z[i] = 0.f;
   return z;
 }
 // element i of a 32x32 accumulator lives at row (i&3) + 8*(i>>2) + 4*half, column lane&31
-PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
-PLLM_DEV bf16x8 pack_frag(const f32x16& x, int s) {
+PL_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
+PL_DEV bf16x8 pack_frag(const f32x16& x, int s) {
   bf16x8 f;
 #pragma unroll
   for (int j = 0; j < 8; ++j) f[j] = (bf16)x[8 * s + j];
@@ -42,7 +42,7 @@ PLLM_DEV bf16x8 pack_frag(const f32x16& x, int s) {
 // the final stores, so the packed QKV tensor and its gradient stay unrotated and no separate
 // RoPE pass over [B, T, H, D] exists in forward or backward.
 // Rotates 8 + 8 bf16 values (a = elements i0..i0+7, b = i0+D/2..) held as two 16-B chunks.
-PLLM_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, float dir) {
+PL_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, float dir) {
   float a[8], b[8], c[8], sn[8];
   unpack8(lo, a);
   unpack8(hi, b);
@@ -72,7 +72,7 @@ PLLM_DEV void rope8(u32x4& lo, u32x4& hi, const float* cosr, const float* sinr, 
 // stores one contiguous 16-B chunk per pair: 2*NDB dwordx4 stores instead of 4*NDB dwordx2 (the
 // store tail is issue-bound, per instruction).  row: 16-B aligned.
 template <int NDB>
-PLLM_DEV void store_row_bf16(uint16_t* row, const f32x16 (&acc)[NDB], float sc, int hh) {
+PL_DEV void store_row_bf16(uint16_t* row, const f32x16 (&acc)[NDB], float sc, int hh) {
   u32x2 pk[4 * NDB];
 #pragma unroll
   for (int db = 0; db < NDB; ++db)
@@ -105,7 +105,7 @@ PLLM_DEV void store_row_bf16(uint16_t* row, const f32x16 (&acc)[NDB], float sc, 
 // ---------------------------------------------------------------------------
 template <int W>
 struct Img {
-  static PLLM_DEV int f(int r) {
+  static PL_DEV int f(int r) {
     if constexpr (W == 128) return ((r & 3) << 2) | ((r >> 2) & 3);
     else if constexpr (W == 64) {
       const int b = (r >> 1) & 7;
@@ -113,11 +113,11 @@ struct Img {
     } else return (r >> 2) & 3;
   }
   // element offset of (row, col); col's 8-aligned chunk is swizzled, col&7 kept
-  static PLLM_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+  static PL_DEV int off(int r, int col) { return r * W + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
   // a row's two RoPE-partner halves (chunks c and c + W/16) stored so that every 8-lane group
   // of ds_write_b128 (bank = byte address mod 128) covers 128 distinct bytes: at W = 64 rows 2k
   // and 2k+1 share f, so an odd row stores its upper half first (same image, same reads)
-  static PLLM_DEV void st_pair(uint16_t* base, int r, int c, const u32x4& lo, const u32x4& hi) {
+  static PL_DEV void st_pair(uint16_t* base, int r, int c, const u32x4& lo, const u32x4& hi) {
     constexpr int H = W / 16;
     const bool sw = W == 64 && (r & 1);
     st16(base + off(r, (sw ? c + H : c) * 8), sw ? hi : lo);
@@ -133,8 +133,8 @@ struct Img {
 // the former 8-B dS stores a 2-way conflict on every store (16 rows per ds_write_b64 group onto
 // 8 slots mod 128 B): ~64 conflict cycles per wave and iteration (profiles/r3_pmc_attn_*_bwd.md).
 struct ImgS {
-  static PLLM_DEV int f(int r) { return ((r & 1) ? 4 : 0) ^ ((r & 2) ? 9 : 0) ^ ((r & 4) ? 2 : 0); }
-  static PLLM_DEV int off(int r, int col) { return r * 128 + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
+  static PL_DEV int f(int r) { return ((r & 1) ? 4 : 0) ^ ((r & 2) ? 9 : 0) ^ ((r & 4) ? 2 : 0); }
+  static PL_DEV int off(int r, int col) { return r * 128 + (((col >> 3) ^ f(r)) << 3) + (col & 7); }
 };
 
 constexpr float kLog2e = 1.4426950408889634f;
@@ -149,25 +149,25 @@ constexpr float kLog2e = 1.4426950408889634f;
 // first MFMA after its VALU-initialised accumulator); A / B from LDS reads and C from the chain's
 // previous MFMA need none (s_nop 1 on all 80 MFMAs of a slice cost ~160 issue cycles per wave)
 template <bool NOP = false>
-PLLM_DEV void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+PL_DEV void mfma_v(f32x16& acc, const bf16x8& a, const bf16x8& b) {
   if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(acc) : "v"(a), "v"(b));
 }
 template <bool NOP = false>
-PLLM_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B
+PL_DEV void mfma_v0(f32x16& acc, const bf16x8& a, const bf16x8& b) {  // acc = A B
   if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, 0" : "=&v"(acc) : "v"(a), "v"(b));
 }
 // ... with the accumulator pinned to the accumulator file.  B (the packed P / dS fragments) was written
 // by VALU at least one pipelined step (>= 2 MFMAs) earlier; the accumulators' zero init is far back
 template <bool NOP = false>
-PLLM_DEV void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
+PL_DEV void mfma_a(f32x16& acc, const bf16x8& a, const bf16x8& b) {
   if constexpr (NOP) asm volatile("s_nop 1\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
   else asm volatile("v_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
 }
 // an MFMA result read by anything but the next MFMA of its chain: 16-pass XDL -> 18 wait states
-PLLM_DEV void mfma_settle(f32x16& x) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x)); }
-PLLM_DEV void mfma_settle(f32x16& x, f32x16& y) {
+PL_DEV void mfma_settle(f32x16& x) { asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x)); }
+PL_DEV void mfma_settle(f32x16& x, f32x16& y) {
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" : "+v"(x), "+v"(y));
 }
 

@@ -223,7 +223,7 @@ void attn_decode(const DecodeArgs& a, hipStream_t st) {
     case 128: dispatch_g<128>(a, st); break;
     default: break;
   }
-  PLLM_CHECK_LAUNCH();
+  PL_CHECK_LAUNCH();
 }
 
 }  // namespace pllm

@@ -23,6 +23,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+
+#include "ab.h"
 #include <torch/library.h>
 
 #include <algorithm>
@@ -144,7 +146,7 @@ int autotune(DevState& ds, Plan& p, const Tensor& w, const Tensor& x, void* y, c
     (void)hipEventSynchronize(e1);
     float ms = 0.f;
     (void)hipEventElapsedTime(&ms, e0, e1);
-    if (std::getenv("PLLM_LT_VERBOSE"))
+    if (pllm::ab_int("lt_verbose", 0) != 0)
       fprintf(stderr, "gemm_lt autotune M=%lld N=%lld K=%lld candidate %d: %.1f us\n", (long long)p.M,
               (long long)p.N, (long long)p.K, i, ms * 1e3f / 3);
     if (ms < best_ms) best_ms = ms, best = i;

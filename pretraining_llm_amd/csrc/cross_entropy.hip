@@ -9,6 +9,7 @@
 // so no probability tensor and no second logits-sized buffer ever exist.
 #include <cstdlib>
 
+#include "ab.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(CE_THREADS) void ce_kernel(const uint16_t* __restri
     s = sb;
 #pragma unroll
     for (int k = 0; k < CH; ++k) asm volatile("" : "+v"(v[k]));
-    if (threadIdx.x == 0) PLLM_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
+    if (threadIdx.x == 0) PL_DCHECK(t == (int64_t)ignore_index || (t >= 0 && t < V), "target in [0, vocab) or ignore_index", t);
     if (threadIdx.x == 0) loss[row] = valid ? (__logf(s) + m - xt) : 0.f;
     if (!WRITE_GRAD) return;
     __syncthreads();  // lane 0's target-logit read (consumed by the loss above) precedes every store
@@ -163,9 +164,9 @@ void ce_launch(const void* logits, int64_t ld, const int64_t* targets, int N, in
 
 void cross_entropy(const void* logits, int64_t ld, const int64_t* targets, int N, int V, int ignore_index,
                    float* loss, void* dlogits, const float* inv_n, hipStream_t st) {
-  // non-temporal gradient stores: 2,493 vs 2,524 us at 65536 x 50304 (PLLM_CE_NT=0: plain stores);
+  // non-temporal gradient stores: 2,493 vs 2,524 us at 65536 x 50304 (PLLM_AB=ce_nt=0: plain stores);
   // 256- / 1024-thread blocks measured 2,533 / 2,641 us (scripts/gpu/r4_ce2.sh, 3 interleaved rounds)
-  static const bool nts = !std::getenv("PLLM_CE_NT") || std::atoi(std::getenv("PLLM_CE_NT")) != 0;
+  static const bool nts = pllm::ab_int("ce_nt", 1) != 0;
   if (nts) ce_launch<CE_THREADS, true>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
   else ce_launch<CE_THREADS, false>(logits, ld, targets, N, V, ignore_index, loss, dlogits, inv_n, st);
 }

@@ -16,7 +16,7 @@
 
 namespace {
 
-PLLM_DEV float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+PL_DEV float sigmoid_f(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 inline int ew_grid(size_t n_vec) {
   size_t g = (n_vec + 255) / 256;

@@ -19,7 +19,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
     const int64_t n = i / cv;
     const int c = (int)(i - n * cv);
     const int64_t tok = idx[n];
-    if (c == 0) PLLM_DCHECK(tok >= 0 && tok < V, "token id in [0, vocab)", tok);
+    if (c == 0) PL_DCHECK(tok >= 0 && tok < V, "token id in [0, vocab)", tok);
     // out-of-range ids read nothing (row of zeros) instead of faulting the GPU
     u32x4 v = (tok >= 0 && tok < V) ? ld16(wte + tok * C + c * 8) : u32x4{0u, 0u, 0u, 0u};
     if (wpe) {

@@ -48,13 +48,13 @@ constexpr int GNT = 512;            // 8 waves
 constexpr int GIMG = GT * GBK;      // elements of one operand image [256][64]
 constexpr int GSTAGE = 2 * GIMG;    // A image then B image: 64 KiB
 
-PLLM_DEV int gswz(int row) { return (row >> 1) & 7; }
-PLLM_DEV int gimg_off(int row, int chunk) { return row * GBK + ((chunk ^ gswz(row)) << 3); }
-PLLM_DEV bf16x8 lds_frag(const uint16_t* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
-PLLM_DEV int acc_row32(int e, int half) { return (e & 3) + 8 * (e >> 2) + 4 * half; }
+PL_DEV int gswz(int row) { return (row >> 1) & 7; }
+PL_DEV int gimg_off(int row, int chunk) { return row * GBK + ((chunk ^ gswz(row)) << 3); }
+PL_DEV bf16x8 lds_frag(const uint16_t* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
+PL_DEV int acc_row32(int e, int half) { return (e & 3) + 8 * (e >> 2) + 4 * half; }
 
 // grouped tile order: GROUP_M m-tiles x all n-tiles, m fastest inside a group
-PLLM_DEV void tile_of(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+PL_DEV void tile_of(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
   const int per_group = gm * tiles_n;
   const int grp = t / per_group, first_m = grp * gm, gsize = min(gm, tiles_m - first_m);
   tm = first_m + (t % per_group) % gsize;
@@ -64,10 +64,10 @@ PLLM_DEV void tile_of(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn)
 // buffer store / load of 16 B at a per-lane byte offset; an offset past the descriptor's range
 // drops the store / reads zeros, so every lane issues every instruction (exact vmcnt counts)
 constexpr uint32_t kOff = 0x80000000u;  // an offset past every descriptor built here (< 2 GiB)
-PLLM_DEV void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
+PL_DEV void bst16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
-PLLM_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+PL_DEV u32x2 bld8(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
 }
 
@@ -82,11 +82,11 @@ constexpr int kEpiOps = EPI == 5 ? 63
                         : EPI == 1 ? 32 + (MF == 32 ? 8 : 4)
                                    : (EPI >= 3 ? 16 + 16 + 2 : 16 + (MF == 32 ? 8 : 4));
 
-PLLM_DEV float swiglu_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+PL_DEV float swiglu_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // (acc columns fragments [I0, I0 + NIE) are the wave's 64 columns)
 template <int MF, int EPI, int I0 = 0, typename Acc, int NIA, int NJ>
-PLLM_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pllm::GemmArgs& g,
+PL_DEV void gemm_epilogue(const Acc (&acc)[NIA][NJ], uint16_t* tile, const pllm::GemmArgs& g,
                             const __amdgpu_buffer_rsrc_t& brs, int tm, int tn, int wm, int wn, int lane) {
   constexpr int NI = MF == 32 ? 2 : 4;
   static_assert(I0 + NI <= NIA, "column fragments");
@@ -381,10 +381,10 @@ __global__ __launch_bounds__(GNT) void gemm_tn_kernel(pllm::GemmArgs g) {
 namespace pllm {
 
 static int g_gemm_mfma = 16;
-#ifndef PLLM_GEMM_GROUP_M
-#define PLLM_GEMM_GROUP_M 4  // m-tiles per tile group (L2 reuse of the B panels; A/B builds)
+#ifndef PL_GEMM_GROUP_M
+#define PL_GEMM_GROUP_M 4  // m-tiles per tile group (L2 reuse of the B panels; A/B builds)
 #endif
-static int g_gemm_group_m = PLLM_GEMM_GROUP_M;
+static int g_gemm_group_m = PL_GEMM_GROUP_M;
 // 0: every wave issues its DMA pieces; 2: the asymmetric DMA (waves 0-3 issue all).  Measured and
 // removed (profiles/r3_gemm_tn.md): 1 = two k32 phases per K-tile with counted vmcnt across raw
 // barriers (3-12 % slower), 3 = one wave per SIMD with 128x128 per wave and the DMA pinned between
@@ -445,30 +445,30 @@ void gemm_tn(const GemmArgs& a0, int epi, hipStream_t st) {
     return;
   }
   const int tiles = ntiles < ctas ? ntiles : ctas;
-#define PLLM_GEMM_CASE(MFV, E)                                                       \
+#define PL_GEMM_CASE(MFV, E)                                                       \
   do {                                                                               \
     if (g_gemm_phased == 2)                                                          \
       hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, true>), dim3(tiles), dim3(GNT), 0, st, a); \
     else                                                                             \
       hipLaunchKernelGGL((gemm_tn_kernel<MFV, E, false>), dim3(tiles), dim3(GNT), 0, st, a); \
   } while (0)
-#define PLLM_GEMM_EPIS(MFV)          \
+#define PL_GEMM_EPIS(MFV)          \
   switch (epi) {                     \
-    case 0: PLLM_GEMM_CASE(MFV, 0); break; \
-    case 1: PLLM_GEMM_CASE(MFV, 1); break; \
-    case 2: PLLM_GEMM_CASE(MFV, 2); break; \
-    case 3: PLLM_GEMM_CASE(MFV, 3); break; \
-    case 4: PLLM_GEMM_CASE(MFV, 4); break; \
-    case 5: PLLM_GEMM_CASE(MFV, 5); break; \
-    default: PLLM_GEMM_CASE(MFV, 6); break; \
+    case 0: PL_GEMM_CASE(MFV, 0); break; \
+    case 1: PL_GEMM_CASE(MFV, 1); break; \
+    case 2: PL_GEMM_CASE(MFV, 2); break; \
+    case 3: PL_GEMM_CASE(MFV, 3); break; \
+    case 4: PL_GEMM_CASE(MFV, 4); break; \
+    case 5: PL_GEMM_CASE(MFV, 5); break; \
+    default: PL_GEMM_CASE(MFV, 6); break; \
   }
   if (g_gemm_mfma == 16) {
-    PLLM_GEMM_EPIS(16)
+    PL_GEMM_EPIS(16)
   } else {
-    PLLM_GEMM_EPIS(32)
+    PL_GEMM_EPIS(32)
   }
-#undef PLLM_GEMM_EPIS
-#undef PLLM_GEMM_CASE
+#undef PL_GEMM_EPIS
+#undef PL_GEMM_CASE
 }
 
 }  // namespace pllm

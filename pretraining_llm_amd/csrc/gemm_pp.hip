@@ -44,7 +44,7 @@
 // Measured and removed in round 5 (records kept in profiles/): a desynchronising tile split (odd
 // workgroups run half of their last tile first and park it; slower, r4_gemm_pp_split_ab.jsonl), a
 // start-time stagger of odd workgroups, the K-tile DMA pieces issued among the MFMAs instead of in the
-// LOAD segment (PLLM_PP_DMA_MFMA), a static priority for waves 4-7 instead of per-segment flips, and the
+// LOAD segment, a static priority for waves 4-7 instead of per-segment flips, and the
 // ablation / s_memtime-stamp diagnostic builds.
 
 namespace {
@@ -58,22 +58,22 @@ constexpr int PIMG = PT * PBK;     // elements of one operand image [256][64]
 constexpr int PSLOT = 2 * PIMG;    // A image then B image: 64 KiB
 constexpr uint32_t kPOff = 0x80000000u;  // a byte offset past every descriptor built here
 
-PLLM_DEV bf16x8 ldsf(const uint16_t* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
-PLLM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+PL_DEV bf16x8 ldsf(const uint16_t* p) { return __builtin_bit_cast(bf16x8, *reinterpret_cast<const u32x4*>(p)); }
+PL_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-PLLM_DEV void pp_barrier() {
+PL_DEV void pp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int N>
-PLLM_DEV void pp_vmwait() {
+PL_DEV void pp_vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
 // grouped tile order: GROUP_M m-tiles x all n-tiles, m fastest inside a group
-PLLM_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+PL_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
   const int per_group = gm * tiles_n;
   const int grp = t / per_group, first_m = grp * gm, gsize = min(gm, tiles_m - first_m);
   tm = first_m + (t % per_group) % gsize;
@@ -105,18 +105,18 @@ constexpr int kStQ(int q) {
   return EPI == 1 ? 8 : (EPI == 3 || EPI == 4) ? 6 : EPI == 6 ? ((q & 1) ? 8 : 4) : 4;
 }
 
-PLLM_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
+PL_DEV void pp_st16(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
   __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 0);
 }
-PLLM_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
-PLLM_DEV float pp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+PL_DEV float bfr(float x) { return bf2f(f2bf_bits(x)); }  // round to bf16 and back
+PL_DEV float pp_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 
 // ---------------------------------------------------------------------------------------------
 // Epilogue of one 256x256 tile, straight from the accumulators.  Lane (r16 = lane & 15,
 // g = lane >> 4) holds, for row tile j and column pair p, output row wr*128 + 16j + r16 and the 8
 // columns wc*64 + 32p + 8g + [0, 8): acc[2p][j][0..3] then acc[2p+1][j][0..3].
 template <int EPI>
-PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc, int lane) {
+PL_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc, int lane) {
   const int M = g.M, N = g.N;
   const int m0 = tm * PT, n0 = tn * PT;
   const int rows_ok = min(PT, M - m0);
@@ -295,7 +295,7 @@ PLLM_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, i
 // EPI 7 epilogue (end of tile): per row tile the lane's gate (pair 0) and up (pair 1) values of
 // columns n0 + wc*32 + 8g + [0, 8) -> [g | u] rounded to bf16 into aux [M, 2F] and
 // a = silu(g) * u from those bf16 values (swiglu_fwd_kernel's numerics) into C [M, F]: 24 stores
-PLLM_DEV void pp_epilogue_swiglu(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc,
+PL_DEV void pp_epilogue_swiglu(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int tn, int wr, int wc,
                                  int lane) {
   const int M = g.M, F = g.N;
   const int m0 = tm * PT, n0 = tn * 128;
@@ -356,7 +356,7 @@ struct PPSrd {
   i32x4v a, b, b2;  // b2: EPI 7's up-row panel (piece group 2)
 };
 template <int EPI>
-PLLM_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
+PL_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
   const pllm::GemmArgs& g = *c.g;
   constexpr int NT = kNT<EPI>;
   const int ra = min(PT, g.M - tm * PT), rb = min(NT, g.N - tn * NT);
@@ -375,14 +375,14 @@ PLLM_DEV PPSrd pp_srds(const PPCtx& c, int tm, int tn, int kt, bool valid) {
 // first use: 0 = A rows 0-63 of both row halves, 1 = B image rows of column pair 0 of every wave,
 // 2 = B column pair 1, 3 = A rows 64-127 (distances to first use: 4, 3, 3, 3 phases).
 template <int PH>
-PLLM_DEV int pp_blk0(int w) {
+PL_DEV int pp_blk0(int w) {
   return PH == 0 ? 2 * w + 8 * (w >> 2)
          : PH == 1 ? 8 * (w >> 1) + 2 * (w & 1)
          : PH == 2 ? 4 + 8 * (w >> 1) + 2 * (w & 1)
                    : 8 + 2 * w + 8 * (w >> 2);
 }
 // shift a descriptor's base by `bytes` (its range shrinks by as much, clamped at 0)
-PLLM_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
+PL_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
   const uint64_t a = ((uint64_t)(uint32_t)r[1] << 32 | (uint32_t)r[0]) + bytes;
   i32x4v o;  // (readfirstlane: the asm operand must provably live in SGPRs)
   o[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
@@ -393,7 +393,7 @@ PLLM_DEV i32x4v srd_shift(const i32x4v& r, uint32_t bytes) {
 }
 // the descriptor and LDS address of piece group PH (pieces q = 0, 1 at + 1 KiB)
 template <int PH, int EPI = 0>
-PLLM_DEV void pp_group(const PPCtx& c, const PPSrd& srd, int sl, i32x4v& r, unsigned& lds0) {
+PL_DEV void pp_group(const PPCtx& c, const PPSrd& srd, int sl, i32x4v& r, unsigned& lds0) {
   // (c.lds: the LDS array's own address, so the DMA asm visibly writes it)
   constexpr bool isA = PH == 0 || PH == 3;
   const int blk0 = pp_blk0<PH>(c.w);
@@ -406,12 +406,12 @@ PLLM_DEV void pp_group(const PPCtx& c, const PPSrd& srd, int sl, i32x4v& r, unsi
                                               (uint32_t)(isA ? 64 * c.g->lda * 2 : 32 * c.g->ldb * 2));
 }
 template <int PH>
-PLLM_DEV void pp_piece(const PPCtx& c, const i32x4v& r, unsigned lds0, int q) {
+PL_DEV void pp_piece(const PPCtx& c, const i32x4v& r, unsigned lds0, int q) {
   constexpr bool isA = PH == 0 || PH == 3;
   blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
 }
 template <int PH, int EPI = 0>
-PLLM_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
+PL_DEV void pp_issue(const PPCtx& c, const PPSrd& srd, int sl) {
   i32x4v r;
   unsigned lds0;
   pp_group<PH, EPI>(c, srd, sl, r, lds0);
@@ -432,7 +432,7 @@ constexpr int pp_qjh(int q) { return q >> 1; }
 constexpr int pp_qp(int q) { return (q == 1 || q == 2) ? 1 : 0; }
 
 template <int EPI, int Q>
-PLLM_DEV void pp_aux_issue(const PPCtx& c, const PPEpi& e) {
+PL_DEV void pp_aux_issue(const PPCtx& c, const PPEpi& e) {
   const pllm::GemmArgs& g = *c.g;
   constexpr int jh = pp_qjh(Q), p = pp_qp(Q);
   const int col0 = e.tn * PT + c.wc * 64 + 32 * p;
@@ -458,7 +458,7 @@ PLLM_DEV void pp_aux_issue(const PPCtx& c, const PPEpi& e) {
 // the pair-1 quadrant that follows it.  EPI 3 / 4 write the quadrant's column sums to colpart
 // row 4 tm + 2 wr + jh (gemm_colsum_groups = 4 per tile row with this kernel).
 template <int EPI, int Q>
-PLLM_DEV void pp_epi_quad(f32x4 (&acc)[4][8], const PPCtx& c, const PPEpi& e, const u32x4 (&ax)[4],
+PL_DEV void pp_epi_quad(f32x4 (&acc)[4][8], const PPCtx& c, const PPEpi& e, const u32x4 (&ax)[4],
                           float (&dsum)[4]) {
   const pllm::GemmArgs& g = *c.g;
   constexpr int jh = pp_qjh(Q), p = pp_qp(Q);
@@ -583,7 +583,7 @@ PLLM_DEV void pp_epi_quad(f32x4 (&acc)[4][8], const PPCtx& c, const PPEpi& e, co
 // read quadrant aux / bias out of the wave's LDS area (and make sure the reads have returned
 // before the next quadrant's DMA overwrites the area)
 template <int EPI>
-PLLM_DEV void pp_aux_read(const PPCtx& c, u32x4 (&ax)[4]) {
+PL_DEV void pp_aux_read(const PPCtx& c, u32x4 (&ax)[4]) {
   const int r16 = c.lane & 15, g4 = c.lane >> 4;
   if constexpr (EPI <= 2) {
     ax[0] = *reinterpret_cast<const u32x4*>(c.aux + 8 * g4);
@@ -626,7 +626,7 @@ constexpr int pp_aux_wait() {
 // PH, the counted wait), a barrier, the MFMA segment (16 MFMAs into quadrant PH), a barrier.
 // The epilogue goes first: the fragments it would otherwise overlap are not live yet.
 template <int PH, bool FIRST, bool LAST, int EPI, bool QE>
-PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+PL_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
                        const uint16_t* slotp, const uint16_t* nslotp, const PPSrd& srd, int nsl,
                        const PPEpi& pe, const PPEpi& ce, float (&dsum)[4]) {
   const int wr = c.wr, wc = c.wc;
@@ -692,7 +692,7 @@ PLLM_DEV void pp_phase(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
 }
 
 template <bool FIRST, bool LAST, int EPI, bool QE>
-PLLM_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
+PL_DEV void pp_ktile(const PPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2],
                        const uint16_t* smem, int s, int ntm, int ntn, int nkt, bool nvalid, const PPEpi& pe,
                        const PPEpi& ce, float (&dsum)[4]) {
   const uint16_t* slotp = smem + (s & 1) * PSLOT;
@@ -846,22 +846,22 @@ void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st) {
   if (ntiles == 0) return;
   const int grid = ntiles < ctas ? ntiles : ctas;
   const bool qe = gemm_pp_quad_epilogue(a.K, epi);
-#define PLLM_PP_CASE(E)                                                                          \
+#define PL_PP_CASE(E)                                                                          \
   do {                                                                                           \
     if (qe) hipLaunchKernelGGL((gemm_pp_kernel<E, E != 5 && E != 1>), dim3(grid), dim3(PNT), 0, st, a); \
     else hipLaunchKernelGGL((gemm_pp_kernel<E, false>), dim3(grid), dim3(PNT), 0, st, a);         \
   } while (0)
   switch (epi) {
-    case 0: PLLM_PP_CASE(0); break;
-    case 1: PLLM_PP_CASE(1); break;
-    case 2: PLLM_PP_CASE(2); break;
-    case 3: PLLM_PP_CASE(3); break;
-    case 4: PLLM_PP_CASE(4); break;
-    case 5: PLLM_PP_CASE(5); break;
-    case 6: PLLM_PP_CASE(6); break;
+    case 0: PL_PP_CASE(0); break;
+    case 1: PL_PP_CASE(1); break;
+    case 2: PL_PP_CASE(2); break;
+    case 3: PL_PP_CASE(3); break;
+    case 4: PL_PP_CASE(4); break;
+    case 5: PL_PP_CASE(5); break;
+    case 6: PL_PP_CASE(6); break;
     default: hipLaunchKernelGGL((gemm_pp_kernel<7, false>), dim3(grid), dim3(PNT), 0, st, a); break;
   }
-#undef PLLM_PP_CASE
+#undef PL_PP_CASE
 }
 
 }  // namespace pllm

@@ -59,23 +59,23 @@ namespace {
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
-PLLM_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+PL_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
-PLLM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+PL_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-PLLM_DEV s16x4 ds_tr(const uint16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
-PLLM_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
+PL_DEV s16x4 ds_tr(const uint16_t* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)p); }
+PL_DEV bf16x8 cat_tr(const s16x4& lo, const s16x4& hi) {
   s16x8 v = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, v);
 }
 // buffer-descriptor form (srd_of / blds16): common.h
-PLLM_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
+PL_DEV int acc_row(int i, int half) { return (i & 3) + 8 * (i >> 2) + 4 * half; }
 
 // [rows][128] bf16 image, 16-B chunk ch of row r at ch ^ f(r) (conflict-free tr reads)
-PLLM_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-PLLM_DEV int img_off(int r, int col) { return r * 128 + (((col >> 3) ^ swz(r)) << 3) + (col & 7); }
+PL_DEV int swz(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+PL_DEV int img_off(int r, int col) { return r * 128 + (((col >> 3) ^ swz(r)) << 3) + (col & 7); }
 
 constexpr int BT = 256;             // output tile (P and Q)
 constexpr int BKM = 64;             // tokens per stage
@@ -334,9 +334,10 @@ namespace pllm {
 static int g_wgrad_mfma = 0;
 static bool g_wgrad_pp = true;
 void wgrad_set_mfma(int mf) {
-  g_wgrad_pp = mf == 0;
+  g_wgrad_pp = mf == 0 || mf == 1;
+  wgrad_pp_set_ri(mf == 1);  // 1: the ping-pong kernel's reads-in-MFMA-segment form
   const int v = mf % 100;
-  g_wgrad_mfma = v == 0 ? 0 : (v == 16 ? 16 : 32);
+  g_wgrad_mfma = (v == 0 || mf == 1) ? 0 : (v == 16 ? 16 : 32);
 }
 
 // A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices
@@ -427,17 +428,17 @@ bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P
   // the bias gradient rides along only on the 16x16x32 kernel (see wgrad_kernel)
   const bool fuse_b = bpart != nullptr && bout != nullptr && mfma == 16;
   float* const bp = fuse_b ? bpart : nullptr;
-#define PLLM_WGRAD_LAUNCH(MFV, OF)                                                                           \
+#define PL_WGRAD_LAUNCH(MFV, OF)                                                                           \
   hipLaunchKernelGGL((wgrad_kernel<MFV, OF>), dim3(ntiles * S), dim3(NT), 0, st, (const uint16_t*)dy, lda, \
                      (const uint16_t*)x, ldb, M, P, Q, S, slice, part, out, (int)accumulate, bp)
   if (mfma == 16) {
-    if (out_f32) PLLM_WGRAD_LAUNCH(16, true);
-    else PLLM_WGRAD_LAUNCH(16, false);
+    if (out_f32) PL_WGRAD_LAUNCH(16, true);
+    else PL_WGRAD_LAUNCH(16, false);
   } else {
-    if (out_f32) PLLM_WGRAD_LAUNCH(32, true);
-    else PLLM_WGRAD_LAUNCH(32, false);
+    if (out_f32) PL_WGRAD_LAUNCH(32, true);
+    else PL_WGRAD_LAUNCH(32, false);
   }
-#undef PLLM_WGRAD_LAUNCH
+#undef PL_WGRAD_LAUNCH
   if (fuse_b) {  // bias gradient: the [S][P] partial rows summed in slice order into bout
     const dim3 bg((unsigned)((P / 8 + 255) / 256));
     if (bout_f32) hipLaunchKernelGGL(wgrad_reduce_kernel<true>, bg, dim3(256), 0, st, bpart, S, (int64_t)P, bout, 1);

@@ -83,11 +83,11 @@ __global__ __launch_bounds__(GV_THREADS) void gemv_kernel(const uint16_t* __rest
   }
 }
 
-PLLM_DEV float bf16_round(float v) { return bf2f(f2bf_bits(v)); }
+PL_DEV float bf16_round(float v) { return bf2f(f2bf_bits(v)); }
 
 // block-wide sums of M per-thread values (all threads get the totals); `red` holds NW x M floats
 template <int M, int NW>
-PLLM_DEV void block_sum(float (&v)[M], float* red) {
+PL_DEV void block_sum(float (&v)[M], float* red) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
@@ -304,7 +304,7 @@ void gemv(const GemvArgs& a, hipStream_t st) {
     else L(8);
 #undef L
   }
-  PLLM_CHECK_LAUNCH();
+  PL_CHECK_LAUNCH();
 }
 
 }  // namespace pllm

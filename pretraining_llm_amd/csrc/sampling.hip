@@ -15,14 +15,14 @@
 
 namespace {
 
-PLLM_DEV uint64_t mix64(uint64_t z) {
+PL_DEV uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
 
 // (value, index) argmax with lowest-index tie break
-PLLM_DEV void better(float& v, int& i, float v2, int i2) {
+PL_DEV void better(float& v, int& i, float v2, int i2) {
   if (v2 > v || (v2 == v && i2 < i)) {
     v = v2;
     i = i2;
@@ -30,11 +30,11 @@ PLLM_DEV void better(float& v, int& i, float v2, int i2) {
 }
 
 template <typename T>
-PLLM_DEV float load_logit(const T* p, int64_t i);
+PL_DEV float load_logit(const T* p, int64_t i);
 template <>
-PLLM_DEV float load_logit<float>(const float* p, int64_t i) { return p[i]; }
+PL_DEV float load_logit<float>(const float* p, int64_t i) { return p[i]; }
 template <>
-PLLM_DEV float load_logit<uint16_t>(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
+PL_DEV float load_logit<uint16_t>(const uint16_t* p, int64_t i) { return bf2f(p[i]); }
 
 template <typename T>
 __global__ __launch_bounds__(1024) void sample_kernel(const T* __restrict__ logits, int64_t ld, int V, float inv_temp,

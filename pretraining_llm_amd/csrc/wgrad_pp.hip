@@ -46,28 +46,28 @@ constexpr int WIMG = WBK * 32;   // elements of one [64][32] image (4 KiB)
 constexpr int WSLOT = 16 * WIMG; // 8 dY images then 8 X images: 64 KiB
 constexpr uint32_t kWOff = 0x80000000u;  // a byte offset past every descriptor built here
 
-PLLM_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+PL_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
-PLLM_DEV s16x4 ds_tr(const char* p) {
+PL_DEV s16x4 ds_tr(const char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(const uint16_t*)p);
 }
-PLLM_DEV bf16x8 frag_tr(const char* p) {
+PL_DEV bf16x8 frag_tr(const char* p) {
   // rows r and r + 4 of the image (+256 B): 8 consecutive tokens of the lane's column
   const s16x4 lo = ds_tr(p), hi = ds_tr(p + 256);
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
-PLLM_DEV void wp_barrier() {
+PL_DEV void wp_barrier() {
   __builtin_amdgcn_sched_barrier(0);
   asm volatile("s_barrier" ::: "memory");
   __builtin_amdgcn_sched_barrier(0);
 }
 template <int N>
-PLLM_DEV void wp_vmwait() {
+PL_DEV void wp_vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 // buffer resource from wave-uniform values, provably so (no waterfall loop around its users)
-PLLM_DEV __amdgpu_buffer_rsrc_t wp_rsrc(const void* base, int bytes) {
+PL_DEV __amdgpu_buffer_rsrc_t wp_rsrc(const void* base, int bytes) {
   const uint64_t a = (uint64_t)(uintptr_t)base;
   const uint64_t u = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(a >> 32)) << 32) |
                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)a);
@@ -75,7 +75,7 @@ PLLM_DEV __amdgpu_buffer_rsrc_t wp_rsrc(const void* base, int bytes) {
                                            0x00020000);
 }
 // chunk position of logical 16-B chunk c (0..3) in image row r
-PLLM_DEV int wp_swz(int r) { return ((r >> 3) & 1) << 1; }
+PL_DEV int wp_swz(int r) { return ((r >> 3) & 1) << 1; }
 
 struct WPArgs {
   const uint16_t* A;  // dY [M, P], row stride lda
@@ -121,7 +121,7 @@ struct WPSrd {
   i32x4v a, b;
 };
 // descriptors of K-tile kt's dY / X panels (64 token rows from the tile's first column)
-PLLM_DEV WPSrd wp_srds(const WPArgs& g, int tp, int tq, int kt) {
+PL_DEV WPSrd wp_srds(const WPArgs& g, int tp, int tq, int kt) {
   const int64_t r0 = (int64_t)kt * WBK;
   const int pc = g.P - tp * WT, qc = g.Q - tq * WT;
   WPSrd r;
@@ -130,7 +130,7 @@ PLLM_DEV WPSrd wp_srds(const WPArgs& g, int tp, int tq, int kt) {
   return r;
 }
 // shift a descriptor's base by `bytes` (its range shrinks by as much)
-PLLM_DEV i32x4v wp_shift(const i32x4v& r, uint32_t bytes) {
+PL_DEV i32x4v wp_shift(const i32x4v& r, uint32_t bytes) {
   const uint64_t a = ((uint64_t)(uint32_t)r[1] << 32 | (uint32_t)r[0]) + bytes;
   i32x4v o;
   o[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
@@ -140,18 +140,18 @@ PLLM_DEV i32x4v wp_shift(const i32x4v& r, uint32_t bytes) {
   return o;
 }
 template <int PH>
-PLLM_DEV void wp_group(const WPCtx& c, const WPSrd& srd, int sl, i32x4v& r, unsigned& lds0) {
+PL_DEV void wp_group(const WPCtx& c, const WPSrd& srd, int sl, i32x4v& r, unsigned& lds0) {
   lds0 = c.lds + (unsigned)(sl * WSLOT + wp_img<PH>(c.w) * WIMG + (c.w & 1) * 1024) * 2u;
   // groups 3 / 2: the images of groups 0 / 1 shifted by 64 (dY) / 32 (X) columns
   r = PH == 0 ? srd.a : PH == 1 ? srd.b : PH == 3 ? wp_shift(srd.a, 128u) : wp_shift(srd.b, 64u);
 }
 template <int PH>
-PLLM_DEV void wp_piece(const WPCtx& c, const i32x4v& r, unsigned lds0, int q) {
+PL_DEV void wp_piece(const WPCtx& c, const i32x4v& r, unsigned lds0, int q) {
   constexpr bool isA = PH == 0 || PH == 3;
   blds16(r, c.vo[isA ? 0 : 1][q], lds0 + 1024u * (unsigned)q);
 }
 template <int PH>
-PLLM_DEV void wp_issue(const WPCtx& c, const WPSrd& srd, int sl) {
+PL_DEV void wp_issue(const WPCtx& c, const WPSrd& srd, int sl) {
   i32x4v r;
   unsigned lds0;
   wp_group<PH>(c, srd, sl, r, lds0);
@@ -167,14 +167,112 @@ constexpr int wp_dma_wait() {
   return 4 + ((F && PH < 2) ? 32 : 0);
 }
 
+// fragment reads of the weight-gradient loop (quadrant helpers shared by both loop forms):
+// dY row tile 4 jh + jj, K-step k -> fa; X column tile 2 p + ii, K-step k -> fb
+template <int JH>
+PL_DEV bf16x8 wp_rd_a(const WPCtx& c, const char* slotp, int k, int jj) {
+  return frag_tr(slotp + c.rd[jj & 1] + (unsigned)((4 * c.wr + 2 * JH + (jj >> 1)) * WIMG * 2 + 2048 * k));
+}
+template <int P>
+PL_DEV bf16x8 wp_rd_b(const WPCtx& c, const char* slotp, int k, int ii) {
+  return frag_tr(slotp + c.rd[ii] + (unsigned)((8 + 2 * c.wc + P) * WIMG * 2 + 2048 * k));
+}
+
+// Round 6, reads-in-MFMA-segment form (RI): each phase's LOAD segment keeps only its two DMA pieces, the
+// counted wait and the barrier; the fragment reads the NEXT phase needs are issued inside this wave's own
+// MFMA segment, one register group right after the MFMAs that last read it (no extra registers):
+//   MFMA 0 (fa jh0, fb pair 0) + reads fb pair 1          MFMA 1 (fa jh0, fb 1) + reads fa jh1
+//   MFMA 2 (fa jh1, fb 1)                                 MFMA 3 (fa jh1, fb 0) + reads fa jh0, fb 0 of the
+//                                                         next K-tile (next slot: DMA groups 0 / 1, waited and
+//                                                         barriered in phases 2 / 3)
+// so the partner wave's MFMA segment no longer waits on 24 / 8 / 16 / 0 transposed reads in this wave's LOAD
+// segment; the reads fill the MFMA gaps (at most 1.5 per 16-cycle MFMA).
+template <int PH, bool FIRST, bool BIAS>
+PL_DEV void wp_phase_ri(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
+                        f32x4 (&bacc)[2], bool dob, const char* slotp, const char* nslotp, const WPSrd& srd,
+                        int nsl) {
+  constexpr int jh = PH >> 1;
+  constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
+  bf16x8 (&fb)[2][2] = fbp[p];
+  i32x4v gr;
+  unsigned glds;
+  wp_group<PH>(c, srd, nsl, gr, glds);
+  wp_piece<PH>(c, gr, glds, 0);
+  wp_piece<PH>(c, gr, glds, 1);
+  wp_vmwait<wp_dma_wait<FIRST, PH>()>();
+  wp_barrier();
+  __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii) {
+        f32x4& a = acc[2 * p + ii][4 * jh + jj];
+        if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
+        else a = mfma16(fb[k][ii], fa[k][jj], a);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // reads for the next phase, each right after the last MFMA that reads the register group it replaces
+      if constexpr (PH == 0) {
+        if (jj < 2) fbp[1][k][jj] = wp_rd_b<1>(c, slotp, k, jj);
+      } else if constexpr (PH == 1) {
+        fa[k][jj] = wp_rd_a<1>(c, slotp, k, jj);
+      } else if constexpr (PH == 3) {
+        fa[k][jj] = wp_rd_a<0>(c, nslotp, k, jj);
+        if (k == 0 && jj == 3) {
+          fbp[0][0][0] = wp_rd_b<0>(c, nslotp, 0, 0);
+          fbp[0][0][1] = wp_rd_b<0>(c, nslotp, 0, 1);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if constexpr (PH == 3) {
+    fbp[0][1][0] = wp_rd_b<0>(c, nslotp, 1, 0);
+    fbp[0][1][1] = wp_rd_b<0>(c, nslotp, 1, 1);
+  }
+  if constexpr (BIAS && (PH == 0 || PH == 2)) {
+    if (dob) {
+      const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
+      bf16x8 f0 = fa[0][0], f1 = fa[1][0];
+#pragma unroll
+      for (int jj = 1; jj < 4; ++jj)
+        if (c.wc == jj) {
+          f0 = fa[0][jj];
+          f1 = fa[1][jj];
+        }
+      bacc[jh] = mfma16(ones, f0, bacc[jh]);
+      bacc[jh] = mfma16(ones, f1, bacc[jh]);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  wp_barrier();
+}
+
+// the RI form's first reads (phase 0's fragments of a slot): before the first K-tile
+PL_DEV void wp_read_ph0(const WPCtx& c, bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2], const char* slotp) {
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) fa[k][jj] = wp_rd_a<0>(c, slotp, k, jj);
+#pragma unroll
+    for (int ii = 0; ii < 2; ++ii) fbp[0][k][ii] = wp_rd_b<0>(c, slotp, k, ii);
+  }
+}
+
 // One phase: fragment reads of quadrant PH (rows half jh, column pair p; snake order (0,0) (0,1)
 // (1,1) (1,0)), the next K-tile's piece group PH, the counted wait, a barrier, 16 MFMAs (+ the
 // bias MFMAs), a barrier.
-template <int PH, bool FIRST, bool BIAS>
-PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
-                       f32x4 (&bacc)[2], bool dob, const char* slotp, const WPSrd& srd, int nsl) {
+template <int PH, bool FIRST, bool BIAS, bool RI>
+PL_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
+                     f32x4 (&bacc)[2], bool dob, const char* slotp, const char* nslotp, const WPSrd& srd, int nsl) {
   constexpr int jh = PH >> 1;
   constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
+  if constexpr (RI) {
+    wp_phase_ri<PH, FIRST, BIAS>(c, acc, fa, fbp, bacc, dob, slotp, nslotp, srd, nsl);
+    return;
+  }
   if constexpr (PH == 0 || PH == 2) {
     // dY row tiles 4 jh + jj of the wave: image 4 wr + 2 jh + jj / 2, columns 16 (jj & 1)
 #pragma unroll
@@ -230,20 +328,21 @@ PLLM_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], b
   wp_barrier();
 }
 
-template <bool FIRST, bool BIAS>
-PLLM_DEV void wp_ktile(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
-                       f32x4 (&bacc)[2], bool dob, const uint16_t* smem, int s, const WPSrd& srd) {
+template <bool FIRST, bool BIAS, bool RI>
+PL_DEV void wp_ktile(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
+                     f32x4 (&bacc)[2], bool dob, const uint16_t* smem, int s, const WPSrd& srd) {
   const char* slotp = reinterpret_cast<const char*>(smem + (s & 1) * WSLOT);
   const int nsl = (s + 1) & 1;
-  wp_phase<0, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
-  wp_phase<1, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
-  wp_phase<2, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
-  wp_phase<3, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
+  const char* nslotp = reinterpret_cast<const char*>(smem + nsl * WSLOT);
+  wp_phase<0, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
+  wp_phase<1, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
+  wp_phase<2, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
+  wp_phase<3, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
 }
 
 // work item i -> (slice, P tile, Q tile); slice-major, so the items that share a slice's panels
 // are neighbours (one XCD's L2 after xcd_remap)
-PLLM_DEV void wp_item(const WPArgs& g, int i, int tiles_q, int ntiles, int& sidx, int& tp, int& tq) {
+PL_DEV void wp_item(const WPArgs& g, int i, int tiles_q, int ntiles, int& sidx, int& tp, int& tq) {
   sidx = i / ntiles;
   const int t = i - sidx * ntiles;
   tp = t / tiles_q;
@@ -252,7 +351,7 @@ PLLM_DEV void wp_item(const WPArgs& g, int i, int tiles_q, int ntiles, int& sidx
 
 // segment i of workgroup lid (G workgroups; tiles_q tiles per row band, ntiles tiles)
 template <bool HY>
-PLLM_DEV WPSeg wp_seg(const WPArgs& g, int lid, int G, int i, int tiles_q, int ntiles) {
+PL_DEV WPSeg wp_seg(const WPArgs& g, int lid, int G, int i, int tiles_q, int ntiles) {
   WPSeg s;
   if constexpr (HY) {
     const int it = lid + i * G;
@@ -283,7 +382,7 @@ PLLM_DEV WPSeg wp_seg(const WPArgs& g, int lid, int G, int i, int tiles_q, int n
 
 // segments of workgroup lid
 template <bool HY>
-PLLM_DEV int wp_nseg(const WPArgs& g, int lid, int G, int ntiles) {
+PL_DEV int wp_nseg(const WPArgs& g, int lid, int G, int ntiles) {
   const int items = HY ? g.hy_full + g.hy_rem * g.hy_s : ntiles * g.S;
   return lid < items ? (items - lid + G - 1) / G : 0;
 }
@@ -292,7 +391,7 @@ PLLM_DEV int wp_nseg(const WPArgs& g, int lid, int G, int ntiles) {
 // columns out of range go to an offset past the descriptor).  Into the gradient (+= when
 // accumulating), the slice's slab, or a stream-K piece slot (tile-local [256][256], no bounds)
 template <bool HY>
-PLLM_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], const WPSeg& sg) {
+PL_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], const WPSeg& sg) {
   const WPArgs& g = *c.g;
   const int r16 = c.lane & 15, g4 = c.lane >> 4;
   const bool piece = HY && sg.dest >= 0;
@@ -328,7 +427,7 @@ PLLM_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], const WPSeg& sg) {
   }
 }
 
-template <bool BIAS, bool HY = false>
+template <bool BIAS, bool HY = false, bool RI = false>
 __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * WSLOT];
   const int tiles_p = (g.P + WT - 1) / WT, tiles_q = (g.Q + WT - 1) / WT, ntiles = tiles_p * tiles_q;
@@ -383,6 +482,7 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
   bf16x8 fb[2][2][2];
+  if constexpr (RI) wp_read_ph0(c, fa, fb, reinterpret_cast<const char*>(smem));
   int s = 0;
   for (int i = 0; i < R; ++i) {
     const bool dob = BIAS && sg.tq == 0;
@@ -400,8 +500,8 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
       } else {
         srd = WPSrd{srd_of(g.A, 0u), srd_of(g.B, 0u)};
       }
-      if (kt == sg.kb) wp_ktile<true, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
-      else wp_ktile<false, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
+      if (kt == sg.kb) wp_ktile<true, BIAS, RI>(c, acc, fa, fb, bacc, dob, smem, s, srd);
+      else wp_ktile<false, BIAS, RI>(c, acc, fa, fb, bacc, dob, smem, s, srd);
     }
     wp_epilogue<HY>(c, acc, sg);
     if constexpr (BIAS) {
@@ -441,6 +541,10 @@ __global__ __launch_bounds__(256) void wgrad_hy_reduce_kernel(const float* __res
 }  // namespace
 
 namespace pllm {
+
+// A/B (wgrad_set_mfma(1)): the reads-in-MFMA-segment loop form (RI, wp_phase_ri)
+static int g_wp_ri = 0;
+void wgrad_pp_set_ri(int on) { g_wp_ri = on; }
 
 // hybrid plan: with more tiles than workgroups, whole tiles for the whole rounds of the grid and the
 // remaining tiles as slices filling the last round (>= 2 K-tiles each); false when it does not apply
@@ -485,7 +589,9 @@ void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M,
   g.hy_s = S;
   g.kst = M / WBK;
   const int items = full + rem * S;
-  hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), dim3(items < ctas ? items : ctas), dim3(WNT), 0, st, g);
+  const dim3 grid(items < ctas ? items : ctas);
+  if (g_wp_ri) hipLaunchKernelGGL((wgrad_pp_kernel<false, true, true>), grid, dim3(WNT), 0, st, g);
+  else hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), grid, dim3(WNT), 0, st, g);
   if (rem > 0)
     hipLaunchKernelGGL(wgrad_hy_reduce_kernel, dim3(rem, WT / 4), dim3(256), 0, st, part, out, P, Q,
                        (Q + WT - 1) / WT, full, rem, S, g.accumulate);
@@ -519,8 +625,13 @@ void wgrad_pp(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, in
   const int ntiles = ((P + WT - 1) / WT) * ((Q + WT - 1) / WT);
   const int items = ntiles * S;
   const int grid = items < ctas ? items : ctas;
-  if (bpart != nullptr) hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(grid), dim3(WNT), 0, st, g);
-  else hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(grid), dim3(WNT), 0, st, g);
+  if (g_wp_ri) {
+    if (bpart != nullptr) hipLaunchKernelGGL((wgrad_pp_kernel<true, false, true>), dim3(grid), dim3(WNT), 0, st, g);
+    else hipLaunchKernelGGL((wgrad_pp_kernel<false, false, true>), dim3(grid), dim3(WNT), 0, st, g);
+  } else {
+    if (bpart != nullptr) hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(grid), dim3(WNT), 0, st, g);
+    else hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(grid), dim3(WNT), 0, st, g);
+  }
 }
 
 }  // namespace pllm

@@ -127,7 +127,8 @@ class _LinearFn(torch.autograd.Function):
         ctx.has_res = res is not None
         if res is not None:  # + the residual stream, added by the GEMM (resid_gemm_ok)
             N = weight.shape[0]
-            return _ops().gemm_lt(x.reshape(-1, x.shape[-1]), weight, bias, 0,
+            # (gemm_lt takes contiguous operands only; reshape of a strided view can stay strided)
+            return _ops().gemm_lt(x.reshape(-1, x.shape[-1]).contiguous(), weight, bias, 0,
                                   not torch.are_deterministic_algorithms_enabled(),
                                   res.reshape(-1, N))[0].view(*x.shape[:-1], N)
         return F.linear(x, weight, bias)
@@ -167,6 +168,8 @@ class _LinearFn(torch.autograd.Function):
 
 import os as _os
 
+from ..ab import ab as _ab
+
 # weight-gradient GEMM engine: "hip" = hand-written split-K MFMA kernel (csrc/gemm_wgrad.hip),
 # default: 824-1114 TFLOP/s at M=65536 vs 432-1003 for hipBLASLt's token-major "NT" kernels
 # (bench/gemm_bench.py, profiles/r1_wgrad_v2_gemm_bench.jsonl); "blas" = hipBLASLt/rocBLAS
@@ -182,8 +185,8 @@ WGRAD_BLAS_SHAPES = {(16384, 6144, 2048), (16384, 2048, 5504), (16384, 50304, 20
 # another, sporadic 2.5-3x slower runs; profiles/r1_wgrad_side_stream_ab.txt.)
 # A linear layer's bias gradient computed inside its weight-gradient GEMM (csrc/gemm_wgrad.hip: MFMAs
 # against an all-ones operand by the first Q-tile's workgroups) instead of a separate column-sum pass
-# over dy (the GPT-2 QKV projection); PLLM_WGRAD_BIAS=0 for the separate pass
-FUSED_WGRAD_BIAS = _os.environ.get("PLLM_WGRAD_BIAS", "1") == "1"
+# over dy (the GPT-2 QKV projection); PLLM_AB=wgrad_bias=0 for the separate pass
+FUSED_WGRAD_BIAS = _ab("wgrad_bias", True)
 
 
 def _dgrad(dy, weight):
@@ -273,13 +276,13 @@ def gemm_config(reserve_cus: Optional[int] = None, persistent: Optional[bool] = 
 _FM = _os.environ.get("PLLM_FUSED_MLP", "bwd")
 FUSED_MLP = _FM in ("1", "all", "bwd")
 FUSED_MLP_FWD = _FM in ("1", "all")
-# PLLM_FUSED_SWIGLU_FWD=1|0: the llama up-projection with its SwiGLU in the GEMM epilogue (epilogue 7)
-FUSED_SWIGLU_FWD = _os.environ.get("PLLM_FUSED_SWIGLU_FWD", "1") == "1"
-# PLLM_LT_RELU=1|0: the ReLU MLP's up-projection (reference architecture) with bias + ReLU in hipBLASLt's
+# PLLM_AB fused_swiglu_fwd=1|0: the llama up-projection with its SwiGLU in the GEMM epilogue (epilogue 7)
+FUSED_SWIGLU_FWD = _ab("fused_swiglu_fwd", True)
+# PLLM_AB lt_relu=1|0: the ReLU MLP's up-projection (reference architecture) with bias + ReLU in hipBLASLt's
 # epilogue (csrc/blaslt.cpp) instead of the library GEMM + act_fwd pass (bench/gelu_epi_bench.py:
 # 394 vs 494 us at the ref-3b shape).  GELU has no such path: the library build that ships with torch has
 # no GELU epilogue with the pre-activation output the backward needs (HIPBLASLT_EPILOGUE_GELU_AUX*)
-LT_RELU_FWD = _os.environ.get("PLLM_LT_RELU", "1") == "1"
+LT_RELU_FWD = _ab("lt_relu", True)
 
 
 def fused_mlp_ok(x, w1, b1, w2, act: str) -> bool:
@@ -390,16 +393,20 @@ def fused_mlp(x, w1, b1, w2, b2, act: str, out_bias_ext: bool = False, residual=
     return _FusedMLPFn.apply(x, w1, b1, w2, b2, act == "gelu", ext, residual)
 
 
-# PLLM_RESID_GEMM=1|0: a block's residual add (reference: x = x + attn(ln1(x)); x = x + mlp(ln2(x)),
+# PLLM_AB resid_gemm=1|0: a block's residual add (reference: x = x + attn(ln1(x)); x = x + mlp(ln2(x)),
 # /root/reference/src/models/transformer_block.py:44,46) done by its output projection's GEMM (hipBLASLt beta = 1,
 # s = residual + x W^T + b in one rounding, csrc/blaslt.cpp gemm_lt) instead of by the next norm, which
 # then reads one stream instead of two and writes one instead of two.  Round-4 measurement
 # (profiles/r4_residual_in_gemm_negative.md): -3.9 / -15.9 us per GPT-2 layer (attention out / MLP down),
 # -14.5 us at llama's attention output projection, but +105 us at its down projection (2048 x 5504: no fast
-# beta = 1 solution among hipBLASLt's candidates), so weights of at most RESID_GEMM_MAX_W elements only
-# (every measured-good shape: GPT-2 small / medium projections, llama's W_o; not llama / ref-3b MLP downs).
-RESID_GEMM = _os.environ.get("PLLM_RESID_GEMM", "1") == "1"
-RESID_GEMM_MAX_W = 2048 * 3072
+# beta = 1 solution among hipBLASLt's candidates), so weights of at most RESID_GEMM_MAX_W elements only.
+# The size rule is a heuristic fitted to the measured shapes: its bound (4,194,304 = 2048 x 2048 = 1024 x 4096)
+# admits exactly the measured-good ones among the presets -- GPT-2 small (768 x 768, 768 x 3072) and medium
+# (1024 x 1024, 1024 x 4096) projections, llama's W_o (2048 x 2048) -- and none of the MLP downs of llama / ref-3b
+# (2048 x 5504, 2048 x 8192) nor unmeasured mid-size ones (1024 x 5504, 1536 x 4096).  A new preset with a
+# projection under the bound should have its beta = 1 GEMM re-measured (bench/residual_gemm_bench.py).
+RESID_GEMM = _ab("resid_gemm", True)
+RESID_GEMM_MAX_W = 2048 * 2048
 
 
 def resid_gemm_ok(res, w) -> bool:
@@ -767,8 +774,8 @@ class _AttnProjFn(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None, dw, db, None, (dy if ctx.has_res else None)
 
 
-# PLLM_ATTN_PROJ_FUSED=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
-FUSED_ATTN_PROJ = os.environ.get("PLLM_ATTN_PROJ_FUSED", "1") == "1"
+# PLLM_AB attn_proj_fused=0: the output projection's backward on hipBLASLt + the attention's delta pre-pass
+FUSED_ATTN_PROJ = _ab("attn_proj_fused", True)
 # head dims served by it: 64.  (D = 128 -- two 64-column delta halves per head -- measured 0.5 % slower on
 # llama-1.3B, profiles/r4_attn_experiments.md, and was removed: the D = 128 backward, csrc/attn_bwd_ks.hip,
 # forms delta itself)
@@ -815,7 +822,7 @@ def _attn_ws(device):
 
 
 # RoPE for the HIP attention: pre-pass rotation (default) or rotation inside the kernels' tile loops
-_ROPE_PREPASS = os.environ.get("PLLM_ROPE_PREPASS", "1") == "1"
+_ROPE_PREPASS = _ab("rope_prepass", True)
 
 
 class _RopePackedFn(torch.autograd.Function):
@@ -1066,7 +1073,7 @@ def embedding(idx, wte, wpe=None, pos_offset: int = 0):
 # 75.7 / 68.5 / 66.6 ms vs 60.5 ms per step (scripts/gpu/r2_cesub.sh, profiles/r2_ce_subchunk_negative.txt).
 # The workspace budget is a quarter of the HBM the device can still give (utils/memory.py),
 # capped at those 8 GiB and floored at 256 MiB; PLLM_CE_WORKSPACE_MB fixes it instead.
-CE_CHUNK_ROWS = int(_os.environ.get("PLLM_CE_CHUNK_ROWS", "0"))
+CE_CHUNK_ROWS = _ab("ce_chunk_rows", 0)
 CE_WORKSPACE_MB = float(_os.environ["PLLM_CE_WORKSPACE_MB"]) if "PLLM_CE_WORKSPACE_MB" in _os.environ else None
 
 

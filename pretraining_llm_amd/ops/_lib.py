@@ -43,18 +43,18 @@ def load(raise_on_error: bool = False) -> bool:
                 torch.ops.load_library(SO_PATH)
                 from . import fake  # meta implementations for FakeTensor tracing (torch.compile)
                 fake.register()
-                # PLLM_WGRAD_VARIANT: weight-gradient kernel variant for A/B runs (csrc/gemm_wgrad.hip)
-                if os.environ.get("PLLM_WGRAD_VARIANT"):
-                    torch.ops.pllm.wgrad_set_mfma(int(os.environ["PLLM_WGRAD_VARIANT"]))
-                # PLLM_WGRAD_HY=0|1: weight gradients with more tiles than CUs as whole tiles + a sliced last
-                # round (csrc/wgrad_pp.hip hybrid) instead of uniform split-K slices
-                if os.environ.get("PLLM_WGRAD_HY") and hasattr(torch.ops.pllm, "wgrad_set_hy"):
-                    torch.ops.pllm.wgrad_set_hy(int(os.environ["PLLM_WGRAD_HY"]))
+                from ..ab import ab
+                # A/B (ab.py): weight-gradient kernel variant (csrc/gemm_wgrad.hip) and the hybrid
+                # whole-tile + sliced-last-round split (csrc/wgrad_pp.hip) against uniform split-K slices
+                if ab("wgrad_variant", -1) >= 0:
+                    torch.ops.pllm.wgrad_set_mfma(ab("wgrad_variant", -1))
+                if ab("wgrad_hy", -1) >= 0:
+                    torch.ops.pllm.wgrad_set_hy(ab("wgrad_hy", -1))
                 # PLLM_GEMM_RESERVE_CUS=n: CUs the persistent GEMM grids leave to concurrent RCCL kernels
                 res = os.environ.get("PLLM_GEMM_RESERVE_CUS")
-                per = os.environ.get("PLLM_GEMM_PERSISTENT")  # 0|1: persistent GEMM grids
-                if res or per:
-                    torch.ops.pllm.gemm_set_config(0, 0, -1, int(res) if res else -1, int(per) if per else -1)
+                per = ab("gemm_persistent", -1)  # 0|1: persistent GEMM grids
+                if res or per >= 0:
+                    torch.ops.pllm.gemm_set_config(0, 0, -1, int(res) if res else -1, per)
                 _loaded = True
                 _err = None
             except Exception as e:  # pragma: no cover - depends on the box

@@ -67,9 +67,10 @@ def gemm_persistent_policy(world: int, setting="auto") -> bool:
     start there would hold its whole tile list back (a workgroup of these kernels fills a CU's
     registers, so nothing shares the CU with it)."""
     if setting in (None, "auto"):
-        env = os.environ.get("PLLM_GEMM_PERSISTENT")  # A/B override of the automatic choice
-        if env:
-            return env == "1"
+        from ..ab import ab
+        env = ab("gemm_persistent", -1)  # A/B override of the automatic choice (ab.py)
+        if env >= 0:
+            return env == 1
         return world <= 1
     if isinstance(setting, str):
         return setting.lower() in ("1", "true", "yes", "on")

@@ -39,6 +39,7 @@ import torch.nn as nn
 
 from .. import ops as _ops_mod
 from ..ops import _lib
+from ..ab import ab as _ab
 
 ALIGN = 64  # elements; keeps every segment 16 B aligned for bf16 and fp32
 
@@ -126,8 +127,7 @@ class FlatAdamW:
         # data-gradient GEMMs read W^T contiguously (ops._dgrad), the layout hipBLASLt serves
         # faster.  One extra bf16 copy of the matrices (~250 MB for GPT-2 small).
         if transposed_shadow is None:
-            import os as _os
-            transposed_shadow = self.use_hip and _os.environ.get("PLLM_WT_SHADOW", "1") == "1"
+            transposed_shadow = self.use_hip and _ab("wt_shadow", True)
         self.shadowed = [p for p in params if transposed_shadow and p.dim() == 2
                          and not getattr(p, "_pllm_no_shadow", False)]
         sh_off, o = [], 0
@@ -153,8 +153,7 @@ class FlatAdamW:
         # as zeros.  Any other writer zeroes a fresh slot before adding (ops._acc_target); a slot no
         # writer touched is zeroed before the step reads it (_clear_unwritten).
         if lazy_zero is None:
-            import os as _os
-            lazy_zero = _os.environ.get("PLLM_LAZY_ZERO", "1") == "1"
+            lazy_zero = _ab("lazy_zero", True)
         # (fp32 gradients of bf16 params only: with grad dtype == param dtype autograd may accumulate
         # into p.grad, which aliases the slot)
         self.lazy_zero = bool(lazy_zero) and self.use_hip and not self.grad_is_param_grad

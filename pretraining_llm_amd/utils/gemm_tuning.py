@@ -18,6 +18,8 @@ import tempfile
 
 import torch
 
+from ..ab import ab as _ab
+
 # PLLM_TUNING_DIR: an alternative table directory (A/B of tables)
 TUNING_DIR = os.environ.get("PLLM_TUNING_DIR") or os.path.join(
     os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning")
@@ -72,8 +74,8 @@ def enable_tuned_gemms(device_index: int = 0, tune_missing: bool = False, out_di
     tunable.tuning_enable(bool(tune_missing))
     if tune_missing:
         # bound the per-shape search (hundreds of hipBLASLt/rocBLAS candidates per shape)
-        tunable.set_max_tuning_duration(int(os.environ.get("PLLM_TUNE_MS", "4")))
-        tunable.set_max_tuning_iterations(int(os.environ.get("PLLM_TUNE_ITERS", "8")))
+        tunable.set_max_tuning_duration(_ab("tune_ms", 4))
+        tunable.set_max_tuning_iterations(_ab("tune_iters", 8))
     tunable.set_filename(base, insert_device_ordinal=True)
     if loaded:
         tunable.read_file(per_dev)

@@ -66,10 +66,11 @@ def main(argv=None):
     ap.add_argument("--lr", type=float, default=6e-4)
     ap.add_argument("--backends", default="auto,torch", help="comma list of backend[:dtype] (auto = HIP kernels)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--tail", type=int, default=100, help="steps averaged for the plateau summary (tail_mean)")
     ap.add_argument("--seed", type=int, default=1234, help="init / data-order seed (the synthetic shard stays the same)")
     args = ap.parse_args(argv)
     out = open(args.out, "w") if args.out else sys.stdout
-    finals = {}
+    finals, tails = {}, {}
     for be in args.backends.split(","):
         # "backend[:dtype]", e.g. torch:float32 = stock ops in fp32 (the numerics ground truth)
         name, _, dt = be.partition(":")
@@ -79,11 +80,16 @@ def main(argv=None):
             out.write(json.dumps({"backend": be, "model": args.model, "step": step, "train_loss": round(tl, 5),
                                   "val_loss": None if vl != vl else round(vl, 5)}) + "\n")
         finals[be] = curve[-1][1]
+        tail = [tl for step, tl, _ in curve if step > args.steps - args.tail]  # the last `tail` steps' logged losses
+        tails[be] = sum(tail) / max(1, len(tail))
         print(f"[convergence] backend={be} final train loss {curve[-1][1]:.4f} ({wall:.1f} s)", file=sys.stderr)
     if len(finals) >= 2:
         a, b = list(finals.values())[:2]
         gap = (a - b) / b  # signed: > 0 when the first backend ends higher
+        ta, tb = list(tails.values())[:2]
         out.write(json.dumps({"summary": True, "final_loss": finals, "rel_gap": round(gap, 5),
+                              "tail_mean": {k: round(v, 5) for k, v in tails.items()}, "tail_steps": args.tail,
+                              "tail_rel_gap": round((ta - tb) / tb, 5), "seed": args.seed,
                               "steps": args.steps, "batch": args.batch, "seq": args.seq}) + "\n")
         print(f"[convergence] final-loss relative gap (first - second) / second {100 * gap:+.2f} %", file=sys.stderr)
     if out is not sys.stdout:

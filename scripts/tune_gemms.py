@@ -27,8 +27,9 @@ def main():
     ap.add_argument("--tune-ms", default="30")
     ap.add_argument("--fresh", action="store_true", help="ignore the shipped tables (re-tune every shape)")
     args = ap.parse_args()
-    os.environ["PLLM_TUNE_MS"] = args.tune_ms
-    os.environ.setdefault("PLLM_TUNE_ITERS", "20")
+    from pretraining_llm_amd.ab import ab, ab_set
+    ab_set("tune_ms", args.tune_ms)
+    ab_set("tune_iters", ab("tune_iters", 20))
     import torch
     import torch.cuda.tunable as tunable
     from pretraining_llm_amd import ops

@@ -179,3 +179,69 @@ def test_zero1_on_hip_kernels():
     err = (out["dp"][:n] - out["zero"][:n]).abs().max().item()
     assert err <= 1e-2, err  # bf16 weights; grad-norm summation order differs
     assert out["zero_state"] * 2 <= out["dp_state"] + 2 * 64 * world
+
+
+def _lazy_worker(rank, world, port, outdir):
+    """Weight ``b`` is used on rank 0 in every step and on rank 1 only in step 0, so from step 1 on rank 1's
+    lazily-zeroed slot of ``b`` still holds its step-0 gradient unless the bucket launch clears it
+    (parallel/dp.py DataParallelEngine._launch -> FlatAdamW._clear_unwritten)."""
+    import torch.nn as nn
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.parallel.dp import DataParallelEngine, params_checksum
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    ops._lib.require()
+    dev = torch.device("cuda", 0)
+
+    class Two(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.a = nn.Linear(128, 128, bias=False)
+            self.b = nn.Linear(128, 128, bias=False)
+
+    out = {}
+    for lazy in (False, True):
+        torch.manual_seed(0)
+        m = Two().to(dev, torch.bfloat16)
+        opt = FlatAdamW(m, lr=1e-2, lazy_zero=lazy)
+        assert opt.lazy_zero == lazy
+        eng = DataParallelEngine(opt, bucket_mb=0.01, first_bucket_mb=0.01)
+        g = torch.Generator(device="cpu").manual_seed(7 + rank)
+        sums = []
+        for step in range(4):
+            x = torch.randn(64, 128, generator=g).to(dev).bfloat16()
+            opt.zero_grad()
+            h = ops.linear(x, m.a.weight)
+            if rank == 0 or step == 0:
+                h = ops.linear(h, m.b.weight)
+            h.float().square().mean().backward()
+            opt.step(grad_scale=eng.finish_grad_sync())
+            cs = params_checksum(opt.params).cpu()
+            allc = [torch.zeros_like(cs) for _ in range(world)]
+            dist.all_gather(allc, cs)
+            sums.append([c.item() for c in allc])
+        eng.remove_hooks()
+        torch.cuda.synchronize()
+        out["lazy" if lazy else "full"] = (opt.master.detach().float().cpu().clone(), sums)
+    if rank == 0:
+        torch.save({k: v[0] for k, v in out.items()} | {k + "_sums": v[1] for k, v in out.items()},
+                   os.path.join(outdir, "lazy.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_dp_lazy_zero_weight_unused_on_one_rank():
+    """World 2, lazy gradient zeroing, a weight unused on ONE rank after step 0: the replicas stay identical and
+    follow the fully-zeroed trajectory (a stale slot would add rank 1's step-0 gradient into every later sum)."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_lazy_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        out = torch.load(os.path.join(d, "lazy.pt"), weights_only=True)
+    for key in ("full_sums", "lazy_sums"):
+        for step_sums in out[key]:
+            assert step_sums[0] == step_sums[1], (key, step_sums)
+    rel = ((out["lazy"] - out["full"]).norm() / out["full"].norm()).item()
+    assert rel < 1e-6, rel

@@ -321,6 +321,19 @@ def test_resid_gemm_block_matches_norm_side_add(preset, monkeypatch):
     assert abs(l1.item() - l0.item()) < 1e-2 * abs(l0.item())
     for i, (a, b) in enumerate(zip(g1, g0)):
         assert _rel(a, b) < 3e-2, (i, _rel(a, b))
+    # and against fp32 math on stock torch ops (the same weights in fp32, ops backend "torch")
+    import copy
+    m32 = copy.deepcopy(model).float()
+    m32.zero_grad(set_to_none=True)
+    with ops.backend("torch"), torch.enable_grad():
+        m, r = m32.attn_blocks[0](x0.float(), r0.float(), rope, None, True)
+        s32 = m if r is None else m + r
+        _, l32 = m32(idx, tgt)
+        l32.backward()
+    assert _rel(s1, s32) < 1.5e-2, _rel(s1, s32)
+    assert abs(l1.item() - l32.item()) < 1e-2 * abs(l32.item()), (l1.item(), l32.item())
+    for i, (a, p32) in enumerate(zip(g1, m32.parameters())):
+        assert _rel(a, p32.grad) < 5e-2, (i, _rel(a, p32.grad))
 
 
 def test_resid_gemm_under_activation_checkpointing():

@@ -1141,3 +1141,74 @@ def test_attention_bwd_key_stationary(D, T, S, H, Hkv, B, causal):
     finally:
         torch.ops.pllm.attn_bwd_set_workspace_mb(4096)
         torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
+
+
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("T,S", [(200, 264), (300, 340)])
+def test_attention_bwd_key_stationary_rope_offset(D, T, S):
+    """In-kernel RoPE (rope_in=True) with queries aligned to the END of longer key rows (S > T; offsets 64 and
+    40, the latter not a multiple of 32): the key-stationary backward runs on copies the binding pre-rotates
+    (queries at positions t + S - T, keys at s), then rotates dq / dk back.  Against fp32 rotate-half RoPE +
+    causal attention, gradients w.r.t. the UNROTATED q / k."""
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.ops import reference as ref
+    torch.manual_seed(T + S + D + 5)
+    B, H, Hkv = 2, 4, 2
+    q = (torch.randn(B, T, H, D, device=DEV) * 0.8).bfloat16()
+    k = (torch.randn(B, S, Hkv, D, device=DEV) * 0.8).bfloat16()
+    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16()
+    do = torch.randn(B, T, H, D, device=DEV).bfloat16()
+    cos, sin = ops.rope_cache(S + 32, D, 10000.0, DEV)
+    scale = 1 / math.sqrt(D)
+    qf, kf, vf = (t.float().requires_grad_() for t in (q, k, v))
+    qr = ref.rope(qf, cos[S - T:S], sin[S - T:S])
+    kr = ref.rope(kf, cos[:S], sin[:S])
+    of, _ = _attn_ref(qr, kr, vf, True, scale)
+    of.backward(do.float())
+    try:
+        torch.ops.pllm.attn_bwd_set_ks(3)  # key-stationary at D = 64 and 128
+        o, lse = torch.ops.pllm.attn_fwd(q, k, v, True, scale, cos, sin)
+        assert _rel(o, of) < 1.5e-2, _rel(o, of)
+        got = [torch.empty_like(t) for t in (q, k, v)]
+        torch.ops.pllm.attn_bwd(do, q, k, v, o, lse, *got, True, scale, cos, sin, True)
+        for a, b, n in zip(got, (qf.grad, kf.grad, vf.grad), ("dq", "dk", "dv")):
+            assert not a.isnan().any(), n
+            assert _rel(a, b) < 3e-2, (n, _rel(a, b))
+    finally:
+        torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
+
+
+@pytest.mark.parametrize("M,P,Q", [(65536 // 8, 50304, 768), (4096, 4096, 8192), (8192, 2304, 768), (2048, 200, 136),
+                                   (1024, 4352, 4096)])
+def test_wgrad_pp_reads_in_mfma_segment(M, P, Q):
+    """wgrad_set_mfma(1): the ping-pong weight-gradient loop with the next phase's fragment reads inside the MFMA
+    segments (csrc/wgrad_pp.hip wp_phase_ri) -- the same MFMAs in the same order, so bit-identical to the shipped
+    loop: accumulate, overwrite of a NaN target, the bias-gradient kernel, the hybrid and the slice plans."""
+    torch.manual_seed(43)
+    dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
+    x = torch.randn(M, Q, device=DEV).bfloat16()
+    w0 = torch.randn(P, Q, device=DEV)
+    b0 = torch.randn(P, device=DEV)
+    outs = {}
+    try:
+        for v in (0, 1):
+            torch.ops.pllm.wgrad_set_mfma(v)
+            acc = w0.clone()
+            torch.ops.pllm.wgrad(dy, x, acc)
+            ow = torch.full((P, Q), float("nan"), device=DEV)
+            torch.ops.pllm.wgrad(dy, x, ow, None, True)
+            accb, bacc = w0.clone(), b0.clone()
+            torch.ops.pllm.wgrad(dy, x, accb, bacc)
+            torch.ops.pllm.wgrad_set_hy(0)
+            accs = w0.clone()
+            torch.ops.pllm.wgrad(dy, x, accs)
+            torch.ops.pllm.wgrad_set_hy(1)
+            outs[v] = (acc, ow, accb, bacc, accs)
+    finally:
+        torch.ops.pllm.wgrad_set_mfma(0)
+        torch.ops.pllm.wgrad_set_hy(1)
+    ref = w0.double() + dy.double().t() @ x.double()
+    assert _rel(outs[1][0].double(), ref) < 1e-5
+    assert not outs[1][1].isnan().any()
+    for a, b, n in zip(outs[1], outs[0], ("acc", "overwrite", "acc+bias", "bias", "slices")):
+        assert torch.equal(a, b), n

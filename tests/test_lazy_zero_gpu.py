@@ -31,7 +31,7 @@ def test_lazy_zero_matches_full_zero(preset, compile_, tmp_path, monkeypatch):
                 grad_accum_steps=2, compile=compile_)
     out = {}
     for lazy in ("0", "1"):
-        monkeypatch.setenv("PLLM_LAZY_ZERO", lazy)
+        monkeypatch.setenv("PLLM_AB", f"lazy_zero={lazy}")
         recs = []
         tr = Trainer(dict(base), log=lambda *_: None)
         assert tr.opt.lazy_zero == (lazy == "1")
