@@ -334,10 +334,9 @@ namespace pllm {
 static int g_wgrad_mfma = 0;
 static bool g_wgrad_pp = true;
 void wgrad_set_mfma(int mf) {
-  g_wgrad_pp = mf == 0 || mf == 1;
-  wgrad_pp_set_ri(mf == 1);  // 1: the ping-pong kernel's reads-in-MFMA-segment form
+  g_wgrad_pp = mf == 0;
   const int v = mf % 100;
-  g_wgrad_mfma = (v == 0 || mf == 1) ? 0 : (v == 16 ? 16 : 32);
+  g_wgrad_mfma = v == 0 ? 0 : (v == 16 ? 16 : 32);
 }
 
 // A/B switch for slice-count sweeps (bench/wgrad_slices.py): > 0 forces that many slices

@@ -152,8 +152,7 @@ bool wgrad_hy_plan(int M, int P, int Q, int ctas, int* full, int* rem, int* S, i
 int64_t wgrad_pp_hy_ws_floats(int M, int P, int Q, int ctas);
 void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part,
                  float* out, bool accumulate, int ctas, hipStream_t st);
-void wgrad_set_hy(int on);
-void wgrad_pp_set_ri(int on);  // A/B: reads in the MFMA segments (wgrad_pp.hip wp_phase_ri)  // A/B: hybrid weight gradients where they apply
+void wgrad_set_hy(int on);  // A/B: hybrid weight gradients where they apply
 // workspace floats wgrad() needs for this call (slice slabs or stream-K pieces)
 int64_t wgrad_ws_floats(int M, int P, int Q, bool out_f32, bool bias);
 bool wgrad(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, int P, int Q, float* part, void* out,

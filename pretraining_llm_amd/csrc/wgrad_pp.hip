@@ -167,112 +167,14 @@ constexpr int wp_dma_wait() {
   return 4 + ((F && PH < 2) ? 32 : 0);
 }
 
-// fragment reads of the weight-gradient loop (quadrant helpers shared by both loop forms):
-// dY row tile 4 jh + jj, K-step k -> fa; X column tile 2 p + ii, K-step k -> fb
-template <int JH>
-PL_DEV bf16x8 wp_rd_a(const WPCtx& c, const char* slotp, int k, int jj) {
-  return frag_tr(slotp + c.rd[jj & 1] + (unsigned)((4 * c.wr + 2 * JH + (jj >> 1)) * WIMG * 2 + 2048 * k));
-}
-template <int P>
-PL_DEV bf16x8 wp_rd_b(const WPCtx& c, const char* slotp, int k, int ii) {
-  return frag_tr(slotp + c.rd[ii] + (unsigned)((8 + 2 * c.wc + P) * WIMG * 2 + 2048 * k));
-}
-
-// Round 6, reads-in-MFMA-segment form (RI): each phase's LOAD segment keeps only its two DMA pieces, the
-// counted wait and the barrier; the fragment reads the NEXT phase needs are issued inside this wave's own
-// MFMA segment, one register group right after the MFMAs that last read it (no extra registers):
-//   MFMA 0 (fa jh0, fb pair 0) + reads fb pair 1          MFMA 1 (fa jh0, fb 1) + reads fa jh1
-//   MFMA 2 (fa jh1, fb 1)                                 MFMA 3 (fa jh1, fb 0) + reads fa jh0, fb 0 of the
-//                                                         next K-tile (next slot: DMA groups 0 / 1, waited and
-//                                                         barriered in phases 2 / 3)
-// so the partner wave's MFMA segment no longer waits on 24 / 8 / 16 / 0 transposed reads in this wave's LOAD
-// segment; the reads fill the MFMA gaps (at most 1.5 per 16-cycle MFMA).
-template <int PH, bool FIRST, bool BIAS>
-PL_DEV void wp_phase_ri(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
-                        f32x4 (&bacc)[2], bool dob, const char* slotp, const char* nslotp, const WPSrd& srd,
-                        int nsl) {
-  constexpr int jh = PH >> 1;
-  constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
-  bf16x8 (&fb)[2][2] = fbp[p];
-  i32x4v gr;
-  unsigned glds;
-  wp_group<PH>(c, srd, nsl, gr, glds);
-  wp_piece<PH>(c, gr, glds, 0);
-  wp_piece<PH>(c, gr, glds, 1);
-  wp_vmwait<wp_dma_wait<FIRST, PH>()>();
-  wp_barrier();
-  __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) {
-#pragma unroll
-      for (int ii = 0; ii < 2; ++ii) {
-        f32x4& a = acc[2 * p + ii][4 * jh + jj];
-        if (FIRST && k == 0) a = mfma16(fb[k][ii], fa[k][jj], f32x4{0.f, 0.f, 0.f, 0.f});
-        else a = mfma16(fb[k][ii], fa[k][jj], a);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      // reads for the next phase, each right after the last MFMA that reads the register group it replaces
-      if constexpr (PH == 0) {
-        if (jj < 2) fbp[1][k][jj] = wp_rd_b<1>(c, slotp, k, jj);
-      } else if constexpr (PH == 1) {
-        fa[k][jj] = wp_rd_a<1>(c, slotp, k, jj);
-      } else if constexpr (PH == 3) {
-        fa[k][jj] = wp_rd_a<0>(c, nslotp, k, jj);
-        if (k == 0 && jj == 3) {
-          fbp[0][0][0] = wp_rd_b<0>(c, nslotp, 0, 0);
-          fbp[0][0][1] = wp_rd_b<0>(c, nslotp, 0, 1);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  if constexpr (PH == 3) {
-    fbp[0][1][0] = wp_rd_b<0>(c, nslotp, 1, 0);
-    fbp[0][1][1] = wp_rd_b<0>(c, nslotp, 1, 1);
-  }
-  if constexpr (BIAS && (PH == 0 || PH == 2)) {
-    if (dob) {
-      const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3f803f80u, 0x3f803f80u, 0x3f803f80u, 0x3f803f80u});
-      bf16x8 f0 = fa[0][0], f1 = fa[1][0];
-#pragma unroll
-      for (int jj = 1; jj < 4; ++jj)
-        if (c.wc == jj) {
-          f0 = fa[0][jj];
-          f1 = fa[1][jj];
-        }
-      bacc[jh] = mfma16(ones, f0, bacc[jh]);
-      bacc[jh] = mfma16(ones, f1, bacc[jh]);
-    }
-  }
-  __builtin_amdgcn_s_setprio(0);
-  wp_barrier();
-}
-
-// the RI form's first reads (phase 0's fragments of a slot): before the first K-tile
-PL_DEV void wp_read_ph0(const WPCtx& c, bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2], const char* slotp) {
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) fa[k][jj] = wp_rd_a<0>(c, slotp, k, jj);
-#pragma unroll
-    for (int ii = 0; ii < 2; ++ii) fbp[0][k][ii] = wp_rd_b<0>(c, slotp, k, ii);
-  }
-}
-
 // One phase: fragment reads of quadrant PH (rows half jh, column pair p; snake order (0,0) (0,1)
 // (1,1) (1,0)), the next K-tile's piece group PH, the counted wait, a barrier, 16 MFMAs (+ the
 // bias MFMAs), a barrier.
-template <int PH, bool FIRST, bool BIAS, bool RI>
+template <int PH, bool FIRST, bool BIAS>
 PL_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fbp)[2][2][2],
-                     f32x4 (&bacc)[2], bool dob, const char* slotp, const char* nslotp, const WPSrd& srd, int nsl) {
+                       f32x4 (&bacc)[2], bool dob, const char* slotp, const WPSrd& srd, int nsl) {
   constexpr int jh = PH >> 1;
   constexpr int p = (PH == 1 || PH == 2) ? 1 : 0;
-  if constexpr (RI) {
-    wp_phase_ri<PH, FIRST, BIAS>(c, acc, fa, fbp, bacc, dob, slotp, nslotp, srd, nsl);
-    return;
-  }
   if constexpr (PH == 0 || PH == 2) {
     // dY row tiles 4 jh + jj of the wave: image 4 wr + 2 jh + jj / 2, columns 16 (jj & 1)
 #pragma unroll
@@ -328,16 +230,15 @@ PL_DEV void wp_phase(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf1
   wp_barrier();
 }
 
-template <bool FIRST, bool BIAS, bool RI>
+template <bool FIRST, bool BIAS>
 PL_DEV void wp_ktile(const WPCtx& c, f32x4 (&acc)[4][8], bf16x8 (&fa)[2][4], bf16x8 (&fb)[2][2][2],
-                     f32x4 (&bacc)[2], bool dob, const uint16_t* smem, int s, const WPSrd& srd) {
+                       f32x4 (&bacc)[2], bool dob, const uint16_t* smem, int s, const WPSrd& srd) {
   const char* slotp = reinterpret_cast<const char*>(smem + (s & 1) * WSLOT);
   const int nsl = (s + 1) & 1;
-  const char* nslotp = reinterpret_cast<const char*>(smem + nsl * WSLOT);
-  wp_phase<0, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
-  wp_phase<1, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
-  wp_phase<2, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
-  wp_phase<3, FIRST, BIAS, RI>(c, acc, fa, fb, bacc, dob, slotp, nslotp, srd, nsl);
+  wp_phase<0, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
+  wp_phase<1, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
+  wp_phase<2, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
+  wp_phase<3, FIRST, BIAS>(c, acc, fa, fb, bacc, dob, slotp, srd, nsl);
 }
 
 // work item i -> (slice, P tile, Q tile); slice-major, so the items that share a slice's panels
@@ -427,7 +328,7 @@ PL_DEV void wp_epilogue(const WPCtx& c, f32x4 (&acc)[4][8], const WPSeg& sg) {
   }
 }
 
-template <bool BIAS, bool HY = false, bool RI = false>
+template <bool BIAS, bool HY = false>
 __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   __shared__ __attribute__((aligned(1024))) uint16_t smem[2 * WSLOT];
   const int tiles_p = (g.P + WT - 1) / WT, tiles_q = (g.Q + WT - 1) / WT, ntiles = tiles_p * tiles_q;
@@ -482,7 +383,6 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
   f32x4 acc[4][8];
   bf16x8 fa[2][4];
   bf16x8 fb[2][2][2];
-  if constexpr (RI) wp_read_ph0(c, fa, fb, reinterpret_cast<const char*>(smem));
   int s = 0;
   for (int i = 0; i < R; ++i) {
     const bool dob = BIAS && sg.tq == 0;
@@ -500,8 +400,8 @@ __global__ __launch_bounds__(WNT) void wgrad_pp_kernel(WPArgs g) {
       } else {
         srd = WPSrd{srd_of(g.A, 0u), srd_of(g.B, 0u)};
       }
-      if (kt == sg.kb) wp_ktile<true, BIAS, RI>(c, acc, fa, fb, bacc, dob, smem, s, srd);
-      else wp_ktile<false, BIAS, RI>(c, acc, fa, fb, bacc, dob, smem, s, srd);
+      if (kt == sg.kb) wp_ktile<true, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
+      else wp_ktile<false, BIAS>(c, acc, fa, fb, bacc, dob, smem, s, srd);
     }
     wp_epilogue<HY>(c, acc, sg);
     if constexpr (BIAS) {
@@ -541,10 +441,6 @@ __global__ __launch_bounds__(256) void wgrad_hy_reduce_kernel(const float* __res
 }  // namespace
 
 namespace pllm {
-
-// A/B (wgrad_set_mfma(1)): the reads-in-MFMA-segment loop form (RI, wp_phase_ri)
-static int g_wp_ri = 0;
-void wgrad_pp_set_ri(int on) { g_wp_ri = on; }
 
 // hybrid plan: with more tiles than workgroups, whole tiles for the whole rounds of the grid and the
 // remaining tiles as slices filling the last round (>= 2 K-tiles each); false when it does not apply
@@ -589,9 +485,7 @@ void wgrad_pp_hy(const void* dy, int64_t lda, const void* x, int64_t ldb, int M,
   g.hy_s = S;
   g.kst = M / WBK;
   const int items = full + rem * S;
-  const dim3 grid(items < ctas ? items : ctas);
-  if (g_wp_ri) hipLaunchKernelGGL((wgrad_pp_kernel<false, true, true>), grid, dim3(WNT), 0, st, g);
-  else hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), grid, dim3(WNT), 0, st, g);
+  hipLaunchKernelGGL((wgrad_pp_kernel<false, true>), dim3(items < ctas ? items : ctas), dim3(WNT), 0, st, g);
   if (rem > 0)
     hipLaunchKernelGGL(wgrad_hy_reduce_kernel, dim3(rem, WT / 4), dim3(256), 0, st, part, out, P, Q,
                        (Q + WT - 1) / WT, full, rem, S, g.accumulate);
@@ -625,13 +519,8 @@ void wgrad_pp(const void* dy, int64_t lda, const void* x, int64_t ldb, int M, in
   const int ntiles = ((P + WT - 1) / WT) * ((Q + WT - 1) / WT);
   const int items = ntiles * S;
   const int grid = items < ctas ? items : ctas;
-  if (g_wp_ri) {
-    if (bpart != nullptr) hipLaunchKernelGGL((wgrad_pp_kernel<true, false, true>), dim3(grid), dim3(WNT), 0, st, g);
-    else hipLaunchKernelGGL((wgrad_pp_kernel<false, false, true>), dim3(grid), dim3(WNT), 0, st, g);
-  } else {
-    if (bpart != nullptr) hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(grid), dim3(WNT), 0, st, g);
-    else hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(grid), dim3(WNT), 0, st, g);
-  }
+  if (bpart != nullptr) hipLaunchKernelGGL(wgrad_pp_kernel<true>, dim3(grid), dim3(WNT), 0, st, g);
+  else hipLaunchKernelGGL(wgrad_pp_kernel<false>, dim3(grid), dim3(WNT), 0, st, g);
 }
 
 }  // namespace pllm

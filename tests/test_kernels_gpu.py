@@ -1176,39 +1176,3 @@ def test_attention_bwd_key_stationary_rope_offset(D, T, S):
             assert _rel(a, b) < 3e-2, (n, _rel(a, b))
     finally:
         torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
-
-
-@pytest.mark.parametrize("M,P,Q", [(65536 // 8, 50304, 768), (4096, 4096, 8192), (8192, 2304, 768), (2048, 200, 136),
-                                   (1024, 4352, 4096)])
-def test_wgrad_pp_reads_in_mfma_segment(M, P, Q):
-    """wgrad_set_mfma(1): the ping-pong weight-gradient loop with the next phase's fragment reads inside the MFMA
-    segments (csrc/wgrad_pp.hip wp_phase_ri) -- the same MFMAs in the same order, so bit-identical to the shipped
-    loop: accumulate, overwrite of a NaN target, the bias-gradient kernel, the hybrid and the slice plans."""
-    torch.manual_seed(43)
-    dy = (torch.randn(M, P, device=DEV) * 0.3).bfloat16()
-    x = torch.randn(M, Q, device=DEV).bfloat16()
-    w0 = torch.randn(P, Q, device=DEV)
-    b0 = torch.randn(P, device=DEV)
-    outs = {}
-    try:
-        for v in (0, 1):
-            torch.ops.pllm.wgrad_set_mfma(v)
-            acc = w0.clone()
-            torch.ops.pllm.wgrad(dy, x, acc)
-            ow = torch.full((P, Q), float("nan"), device=DEV)
-            torch.ops.pllm.wgrad(dy, x, ow, None, True)
-            accb, bacc = w0.clone(), b0.clone()
-            torch.ops.pllm.wgrad(dy, x, accb, bacc)
-            torch.ops.pllm.wgrad_set_hy(0)
-            accs = w0.clone()
-            torch.ops.pllm.wgrad(dy, x, accs)
-            torch.ops.pllm.wgrad_set_hy(1)
-            outs[v] = (acc, ow, accb, bacc, accs)
-    finally:
-        torch.ops.pllm.wgrad_set_mfma(0)
-        torch.ops.pllm.wgrad_set_hy(1)
-    ref = w0.double() + dy.double().t() @ x.double()
-    assert _rel(outs[1][0].double(), ref) < 1e-5
-    assert not outs[1][1].isnan().any()
-    for a, b, n in zip(outs[1], outs[0], ("acc", "overwrite", "acc+bias", "bias", "slices")):
-        assert torch.equal(a, b), n
