@@ -39,8 +39,6 @@ def main():
     ap.add_argument("--ks-ab", action="store_true",
                     help="backward only: key-stationary kernel (attn_bwd_set_ks(3)) vs the previous kernels "
                          "(set_ks(0)), interleaved rounds")
-    ap.add_argument("--fwd-pp-ab", action="store_true",
-                    help="forward only: the ping-pong D = 64 kernel (attn_fwd_set_pp(1)) vs the 4-wave kernel, interleaved")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
@@ -79,18 +77,6 @@ def main():
             res["prepass_us"] = min(1e6 * timeit(pre) for _ in range(args.rounds))
             res["prepass_fwd_us"] = min(1e6 * timeit(f_) for _ in range(args.rounds))
             res["prepass_bwd_us"] = min(1e6 * timeit(b_) for _ in range(args.rounds))
-            print(json.dumps(res), flush=True)
-            continue
-        if args.fwd_pp_ab:
-            flops_f = 2 * 2 * B * H * T * T * D / 2
-            res = {"cfg": cfg, "pp_fwd_us": [], "old_fwd_us": []}
-            for _ in range(args.rounds):
-                torch.ops.pllm.attn_fwd_set_pp(1)
-                res["pp_fwd_us"].append(round(1e6 * timeit(ours_f), 1))
-                torch.ops.pllm.attn_fwd_set_pp(0)
-                res["old_fwd_us"].append(round(1e6 * timeit(ours_f), 1))
-            for k_ in ("pp", "old"):
-                res[k_ + "_tflops"] = round(flops_f / (min(res[k_ + "_fwd_us"]) * 1e-6) / 1e12, 1)
             print(json.dumps(res), flush=True)
             continue
         if args.ks_ab:

@@ -18,7 +18,6 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--phased", type=int, default=0, help="gemm_set_config phased (4 = ping-pong kernel)")
     ap.add_argument("--no-blas", action="store_true")
-    ap.add_argument("--w1", action="store_true", help="the one-wave-per-SIMD kernel (gemm_1w) instead of gemm_tn")
     ap.add_argument("--time", action="store_true", help="print the median microseconds of the hand-written GEMM")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
@@ -27,9 +26,8 @@ def main():
     a = torch.empty(args.M, args.K, device="cuda").uniform_(-1, 1).bfloat16()
     w = (torch.empty(args.N, args.K, device="cuda").uniform_(-1, 1) / args.K ** 0.5).bfloat16()
     b = torch.randn(args.N, device="cuda").bfloat16()
-    own = (lambda: torch.ops.pllm.gemm_1w(a, w, b)) if args.w1 else (lambda: torch.ops.pllm.gemm_tn(a, w, b, 0))
     for _ in range(args.reps):
-        own()
+        torch.ops.pllm.gemm_tn(a, w, b, 0)
         if not args.no_blas:
             F.linear(a, w, b)
     torch.cuda.synchronize()
@@ -41,7 +39,7 @@ def main():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(5):
-                own()
+                torch.ops.pllm.gemm_tn(a, w, b, 0)
             torch.cuda.synchronize()
             ts.append((time.perf_counter() - t0) / 5 * 1e6)
         print(f"M={args.M} N={args.N} K={args.K} phased={args.phased} so={os.environ.get('PLLM_SO', 'in-tree')} "

@@ -51,9 +51,6 @@ namespace {
 // past T, e.g. decode) skips its MFMAs and softmax on a wave-uniform branch.
 // lazy-max threshold of the forward's online softmax, log2 units (p <= 2^8)
 constexpr float kLazyThr = 8.f;
-#ifndef PL_FWD_PRIO
-#define PL_FWD_PRIO 0  // A/B build: s_setprio 1 around the forward's MFMA runs (partner wave's softmax yields)
-#endif
 #ifndef PLLM_FWD_STAMPS
 #define PLLM_FWD_STAMPS 0  // diagnostic: per-phase s_memtime sums of the forward loop
 #endif
@@ -267,7 +264,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
       f32x16 s[QB][2];
 #pragma unroll
       for (int j = 0; j < QB; ++j) s[j][0] = s[j][1] = zero16();
-      if (PL_FWD_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -288,10 +284,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
           __builtin_amdgcn_sched_group_barrier(0x100, 1, 2);
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 2);
-      }
-      if (PL_FWD_PRIO) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
       }
       PL_STAMP(1);
       bf16x8 pf[QB][4];
@@ -352,10 +344,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
         }
       }
       PL_STAMP(2);
-      if (PL_FWD_PRIO) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
-      }
 #pragma unroll
       for (int kst = 0; kst < 4; ++kst) {
 #pragma unroll
@@ -376,10 +364,6 @@ __global__ __launch_bounds__(64 * FwdCfg<D>::NW, FwdCfg<D>::MINB) void attn_fwd_
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 3);
         }
         __builtin_amdgcn_sched_group_barrier(0x008, 4, 3);
-      }
-      if (PL_FWD_PRIO) {
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(0);
       }
     };
     if (mask == 3) tile(std::integral_constant<int, 3>{});
@@ -1532,10 +1516,6 @@ static void attn_bwd_r(const AttnBwdArgs& a, hipStream_t st) {
 }
 
 void attn_fwd(const AttnFwdArgs& a, hipStream_t st) {
-  if (attn_fwd_pp_applies(a)) {  // head dim 64, no in-kernel RoPE: the ping-pong kernel (attn_fwd_pp.hip)
-    attn_fwd_pp(a, st);
-    return;
-  }
   if (a.D == 32) attn_fwd_t<32>(a, st);
   else if (a.D == 64) attn_fwd_t<64>(a, st);
   else attn_fwd_t<128>(a, st);

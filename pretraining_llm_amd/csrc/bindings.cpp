@@ -222,42 +222,6 @@ Tensor wgrad(const Tensor& dy, const Tensor& x, const std::optional<Tensor>& out
 }
 
 // ---------------------------------------------------------------- fused-epilogue GEMM
-// one-wave-per-SIMD TN GEMM (csrc/gemm_1w.hip): out [M, N] = a [M, K] b [N, K]^T (+ bias), bf16
-Tensor gemm_1w(const Tensor& a, const Tensor& b, const std::optional<Tensor>& bias) {
-  check_bf16(a, "a");
-  check_bf16(b, "b");
-  TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.size(1) == b.size(1), "gemm_1w: a [M, K], b [N, K]");
-  TORCH_CHECK(a.stride(1) == 1 && b.is_contiguous(), "gemm_1w: K-contiguous operands");
-  const int64_t M = a.size(0), K = a.size(1), N = b.size(0);
-  TORCH_CHECK(pllm::gemm_1w_supported((int)M, (int)N, (int)K), "gemm_1w: K % 64 == 0, K >= 128, N % 8 == 0");
-  TORCH_CHECK(a.stride(0) % 8 == 0 && M < (1 << 30) && N < (1 << 30), "gemm_1w: lda % 8, dims");
-  TORCH_CHECK((int64_t)(std::min<int64_t>(M, 256) - 1) * a.stride(0) * 2 + K * 2 < (1ll << 31) &&
-                  (int64_t)(std::min<int64_t>(N, 256) - 1) * K * 2 + K * 2 < (1ll << 31),
-              "gemm_1w: a 256-row panel must span < 2 GiB");
-  check_aligned16(a, "a");
-  check_aligned16(b, "b");
-  if (bias) {
-    check_bf16(*bias, "bias");
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous(), "gemm_1w: bias [N]");
-    check_aligned16(*bias, "bias");
-  }
-  Tensor out = at::empty({M, N}, a.options());
-  pllm::GemmArgs g{};
-  g.A = (const uint16_t*)a.data_ptr();
-  g.B = (const uint16_t*)b.data_ptr();
-  g.C = (uint16_t*)out.data_ptr();
-  g.bias = bias ? (const uint16_t*)bias->data_ptr() : nullptr;
-  g.lda = a.stride(0);
-  g.ldb = K;
-  g.ldc = N;
-  g.M = (int)M;
-  g.N = (int)N;
-  g.K = (int)K;
-  g.group_m = 4;
-  if (M > 0 && N > 0) pllm::gemm_tn_1w(g, pllm::gemm_grid_cap(), cur_stream());
-  return out;
-}
-
 // a [M, K] (row stride lda), b [N, K] contiguous -> [out [M, N], aux]:
 // epi 0: out = a b^T (+ bias); 1: out = gelu(pre), aux = pre = a b^T + bias; 2: out = relu(a b^T + bias);
 // 3 / 4: out = (a b^T) * gelu'(aux) / * (aux > 0), and when bias_acc is given its column sums are
@@ -1080,7 +1044,6 @@ TORCH_LIBRARY(pllm, m) {
   m.def("norm_bwd_acc(Tensor dy, Tensor s, Tensor weight, Tensor mean, Tensor rstd, Tensor? ds, bool has_bias, bool rms, Tensor(a!) dw_acc, Tensor(b!)? db_acc=None, Tensor(c!)? xb_acc=None) -> Tensor");
   m.def("bias_grad(Tensor dy, Tensor(a!)? out_acc=None) -> Tensor");
   m.def("wgrad(Tensor dy, Tensor x, Tensor(a!)? out_acc=None, Tensor(b!)? bias_acc=None, bool overwrite=False) -> Tensor");
-  m.def("gemm_1w(Tensor a, Tensor b, Tensor? bias=None) -> Tensor");
   m.def("gemm_tn(Tensor a, Tensor b, Tensor? bias, int epi, Tensor? aux=None, Tensor(a!)? bias_acc=None, int T=0) -> (Tensor, Tensor)");
   m.def("gemm_uses_pp(int K, int epi) -> bool", [](int64_t K, int64_t epi) { return pllm::gemm_uses_pp((int)K, (int)epi, 16); });
   m.def("gemm_set_config(int mfma, int group_m, int phased=-1, int reserve_cus=-1, int persistent=-1) -> ()",
@@ -1090,7 +1053,6 @@ TORCH_LIBRARY(pllm, m) {
   m.def("wgrad_set_mfma(int mf) -> ()", [](int64_t mf) { pllm::wgrad_set_mfma((int)mf); });
   m.def("wgrad_set_hy(int on) -> ()", [](int64_t on) { pllm::wgrad_set_hy((int)on); });
   m.def("attn_bwd_set_ks(int mask) -> ()", [](int64_t m) { pllm::attn_bwd_set_ks((int)m); });
-  m.def("attn_fwd_set_pp(int on) -> ()", [](int64_t on) { pllm::attn_fwd_set_pp((int)on); });
   m.def("wgrad_force_slices(int s) -> ()", [](int64_t s) { pllm::wgrad_force_slices((int)s); });
   m.def("attn_bwd_set_workspace_mb(float mb) -> ()", [](double mb) { g_attn_ws_bytes = (int64_t)(mb * (1 << 20)); });
   m.def("gemv(Tensor x, Tensor w, Tensor? bias, Tensor? res=None, Tensor? gamma=None, Tensor? beta=None, float eps=1e-5, int rms=0, int act=0, Tensor(a!)? kc=None, Tensor(b!)? vc=None, Tensor? pos=None, int q_cols=0) -> (Tensor, Tensor)");
@@ -1125,7 +1087,6 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("bias_grad", bias_grad);
   m.impl("wgrad", wgrad);
   m.impl("gemm_tn", gemm_tn);
-  m.impl("gemm_1w", gemm_1w);
   m.impl("act_fwd", act_fwd);
   m.impl("act_bwd", act_bwd);
   m.impl("act_bwd_bias", act_bwd_bias);

@@ -131,9 +131,6 @@ void gemm_set_config(int mfma, int group_m, int phased, int reserve_cus = -1, in
 // workgroup cap of the persistent GEMM grids (CUs minus reserve_cus; 2^30 when non-persistent)
 int gemm_grid_cap();
 void gemm_tn_pp(const GemmArgs& a, int epi, int ctas, hipStream_t st);  // gemm_pp.hip
-// gemm_1w.hip: one-wave-per-SIMD TN GEMM (+ bias)
-bool gemm_1w_supported(int M, int N, int K);
-void gemm_tn_1w(const GemmArgs& a, int ctas, hipStream_t st);
 int gemm_pp_colsum_groups(int M, int K);
 bool gemm_pp_quad_epilogue(int K, int epi);
 int gemm_colsum_groups(int M, int K);  // column-sum partial rows (epi 3 / 4) of the kernel serving K
@@ -209,10 +206,6 @@ bool attn_bwd_uses_ks(int D);    // the key-stationary backward serves head dim 
 // attn_bwd_ks.hip: keys per workgroup; one pass of the key-stationary main kernel (AttnBwdArgs as attn_bwd)
 int attn_bwd_ks_key_block();
 
-// attn_fwd_pp.hip: the ping-pong D = 64 forward (8 waves, MFMA / softmax phases alternating per SIMD)
-void attn_fwd_pp(const AttnFwdArgs& a, hipStream_t st);
-bool attn_fwd_pp_applies(const AttnFwdArgs& a);
-void attn_fwd_set_pp(int on);  // A/B: 1 = the ping-pong forward where it applies
 void attn_bwd_set_ks(int mask);  // A/B: bit 0 = D 64, bit 1 = D 128 on the key-stationary kernel
 void attn_bwd_ks_launch(const AttnBwdArgs& a, hipStream_t st);
 // attn_decode.hip: split-KV single-query attention over a KV cache

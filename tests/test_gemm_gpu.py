@@ -517,21 +517,3 @@ def test_relu_mlp_lt_forward(lt, monkeypatch):
     assert _rel(y1, y0) < 2e-3
     for a, b in zip(g1, g0):
         assert _rel(a, b) < 2e-3
-
-
-@pytest.mark.parametrize("M,N,K", [(512, 768, 768), (300, 520, 128), (777, 264, 192), (8448, 2056, 256),
-                                   (4096, 3072, 768), (2304, 768, 3072), (1000, 50304 // 8, 128)])
-@pytest.mark.parametrize("bias", [False, True])
-def test_gemm_1w(M, N, K, bias):
-    """The one-wave-per-SIMD TN GEMM (csrc/gemm_1w.hip): persistent tiles (more tiles than CUs at the bigger
-    shapes), ragged M / N edges, the K-tile stream running across tile boundaries; vs fp32 math, deterministic."""
-    torch.manual_seed(M + N + K)
-    big = torch.randn(M, K + 64, device=DEV).bfloat16()
-    a = big[:, 32:32 + K]  # row-strided A
-    b = (torch.randn(N, K, device=DEV) / K ** 0.5).bfloat16()
-    bb = (0.5 * torch.randn(N, device=DEV)).bfloat16() if bias else None
-    out = torch.ops.pllm.gemm_1w(a, b, bb)
-    ref = a.float() @ b.float().t() + (bb.float() if bias else 0.0)
-    assert out.shape == (M, N)
-    assert _rel(out, ref) < 5e-3, _rel(out, ref)
-    assert torch.equal(torch.ops.pllm.gemm_1w(a, b, bb), out)

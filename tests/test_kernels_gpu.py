@@ -1176,33 +1176,3 @@ def test_attention_bwd_key_stationary_rope_offset(D, T, S):
             assert _rel(a, b) < 3e-2, (n, _rel(a, b))
     finally:
         torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
-
-
-@pytest.mark.parametrize("B,H,Hkv,T,S,causal", [(2, 4, 4, 1024, 1024, True), (1, 2, 1, 200, 200, True),
-                                                (2, 2, 2, 1000, 1000, True), (1, 4, 2, 2048, 2048, True),
-                                                (2, 2, 2, 512, 512, False), (1, 2, 2, 300, 340, True),
-                                                (1, 2, 1, 96, 700, False), (1, 1, 1, 4096, 4096, True)])
-def test_attention_fwd_pingpong_d64(B, H, Hkv, T, S, causal):
-    """The ping-pong D = 64 forward (csrc/attn_fwd_pp.hip: 8 waves, MFMA and softmax phases alternating between
-    the two waves of each SIMD, K / V rings filled three tiles ahead): vs fp32 math and vs the 4-wave kernel of
-    attention.hip -- ragged T, S > T offsets (32-aligned and not), non-causal, GQA, fully masked blocks."""
-    torch.manual_seed(T + S + H)
-    D = 64
-    q = torch.randn(B, T, H, D, device=DEV).bfloat16()
-    k = torch.randn(B, S, Hkv, D, device=DEV).bfloat16()
-    v = torch.randn(B, S, Hkv, D, device=DEV).bfloat16()
-    scale = 1 / math.sqrt(D)
-    try:
-        torch.ops.pllm.attn_fwd_set_pp(0)
-        o0, l0 = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
-        torch.ops.pllm.attn_fwd_set_pp(1)
-        o1, l1 = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
-        o2, _ = torch.ops.pllm.attn_fwd(q, k, v, causal, scale)
-    finally:
-        torch.ops.pllm.attn_fwd_set_pp(0)
-    ref_o, ref_l = _attn_ref(q, k, v, causal, scale)
-    assert not o1.isnan().any()
-    assert _rel(o1, ref_o) < 1e-2, _rel(o1, ref_o)
-    assert _rel(l1, ref_l) < 1e-4, _rel(l1, ref_l)
-    assert _rel(o1, o0) < 5e-3, _rel(o1, o0)
-    assert torch.equal(o1, o2)  # deterministic
