@@ -110,6 +110,13 @@ class DataParallelEngine:
         cur_bytes = 0
         for i in reversed(order):
             nbytes = params[i].numel() * esz
+            if cur and nbytes >= cap:
+                # a parameter at least a bucket in size gets a bucket of its own: the tied embedding (the
+                # last gradient of the backward, 154 MiB fp32 at GPT-2 small) would otherwise hold back the
+                # first block's parameters in the un-overlappable tail bucket (195 MiB -> 154 MiB)
+                self._close_bucket(cur)
+                cur, cur_bytes = [], 0
+                cap = int(bucket_mb * 2 ** 20)
             cur.append(i)
             cur_bytes += nbytes
             if cur_bytes >= cap:

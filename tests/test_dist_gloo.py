@@ -259,3 +259,25 @@ def test_step_policy_decisions():
         assert not g.gemm_persistent_policy(world)
         assert g.gemm_persistent_policy(world, "1") and g.gemm_persistent_policy(world, True)
     assert not g.gemm_persistent_policy(1, "0")
+
+
+def test_dp_buckets_isolate_oversized_params():
+    """A parameter at least a bucket in size gets its own bucket (parallel/dp.py): the tied embedding --
+    the last gradient of the backward -- must not drag the first block's parameters into the un-overlappable
+    tail bucket.  Buckets still tile the flat gradient buffer in reverse layout order."""
+    from pretraining_llm_amd.models import GPT
+    from pretraining_llm_amd.parallel.dp import DataParallelEngine
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    torch.manual_seed(0)
+    model = GPT(_tiny_cfg().replace(vocab_size=2048))  # 2048 x 64 fp32 embedding = 0.5 MiB
+    opt = FlatAdamW(model, lr=1e-3)
+    eng = DataParallelEngine(opt, bucket_mb=0.25, first_bucket_mb=0.01, broadcast_params=False)
+    wte = next(i for i, p in enumerate(opt.params) if p.numel() == 2048 * 64)
+    own = [b for b in eng.buckets if wte in b["params"]]
+    assert len(own) == 1 and own[0]["params"] == [wte]
+    # contiguous, non-overlapping, covering every parameter once
+    spans = sorted((b["start"], b["end"]) for b in eng.buckets)
+    for (s0, e0), (s1, e1) in zip(spans, spans[1:]):
+        assert e0 <= s1
+    assert sorted(i for b in eng.buckets for i in b["params"]) == list(range(len(opt.params)))
+    assert max(eng.bucket_sizes_mb()) <= 0.5 + 1e-6
