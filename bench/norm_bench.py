@@ -48,9 +48,21 @@ def main():
         ts = [timeit(fn) for _ in range(args.rounds)]
         nbytes = N * C * 2 * (2 + (2 if res else 0))
         med = statistics.median(ts)
-        print(json.dumps({"N": N, "C": C, "rms": rms, "res": res, "us": round(med, 1), "min_us": round(min(ts), 1),
-                          "tbs": round(nbytes / med / 1e6, 2), "rel_err": round(err, 5),
-                          "so": os.environ.get("PLLM_SO", "in-tree")}), flush=True)
+        rec = {"N": N, "C": C, "rms": rms, "res": res, "us": round(med, 1), "min_us": round(min(ts), 1),
+               "tbs": round(nbytes / med / 1e6, 2), "rel_err": round(err, 5)}
+        # backward: dy, s and the residual-stream gradient ds in, dx out (+ weight / bias column partials)
+        mean, rstd = out[-2], out[-1]
+        s_in = out[1] if res else x
+        dy = torch.randn(N, C, device="cuda").bfloat16()
+        ds = torch.randn(N, C, device="cuda").bfloat16()
+        fb = lambda: P.norm_bwd(dy, s_in, w, mean, rstd, ds, not rms, rms)  # noqa: E731
+        for _ in range(3):
+            fb()
+        tb = [timeit(fb) for _ in range(args.rounds)]
+        medb = statistics.median(tb)
+        rec.update({"bwd_us": round(medb, 1), "bwd_tbs": round(N * C * 2 * 4 / medb / 1e6, 2),
+                    "so": os.environ.get("PLLM_SO", "in-tree")})
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

@@ -135,7 +135,14 @@ __global__ __launch_bounds__(256) void norm_bwd_kernel(
     for (int k = 0; k < K; ++k) {
       const int c = lane + 64 * k;
       const bool in = c < nch;
-      S[k] = in ? ld16(s + base + c * 8) : zero4;
+#ifndef PL_NORM_NTS
+#define PL_NORM_NTS 1
+#endif
+      // the forward's residual stream, cold by now, by non-temporal loads: 79-82 vs 86-88 us at 65536 x 768,
+      // 103 vs 107.5 us at 32768 x 2048 (profiles/r6_norm_bwd_nt_loads.log)
+      S[k] = in ? (PL_NORM_NTS ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(s + base + c * 8))
+                               : ld16(s + base + c * 8))
+                : zero4;
       Dy[k] = in ? ld16(dy + base + c * 8) : zero4;
       R[k] = (in && ds) ? ld16(ds + base + c * 8) : zero4;
     }
