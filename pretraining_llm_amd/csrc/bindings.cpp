@@ -525,12 +525,15 @@ Tensor rope(const Tensor& x, const Tensor& cos, const Tensor& sin, int64_t n_hea
   return out;
 }
 
+// x *= s in place (x bf16 or fp32, contiguous; s a 1-element fp32 GPU tensor); no pass at all when s == 1
 void scale_(Tensor& x, const Tensor& s) {
-  check_bf16(x, "x");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "scale_: x bf16 or fp32");
   check_contig(x, "x");
   TORCH_CHECK(s.scalar_type() == at::kFloat && s.numel() == 1 && s.is_cuda(), "scale must be a 1-element fp32 GPU tensor");
   TORCH_CHECK(x.numel() % 8 == 0, "scale_: numel % 8");
-  if (x.numel()) pllm::scale_bf16(x.data_ptr(), s.data_ptr<float>(), x.numel(), cur_stream());
+  check_aligned16(x, "x");
+  if (x.numel())
+    pllm::scale_inplace(x.data_ptr(), x.scalar_type() == at::kFloat, s.data_ptr<float>(), x.numel(), cur_stream());
 }
 
 // ring attention: fold a partial block result (o [B, T, H, D] bf16, lse [B, H, T] fp32) into the

@@ -190,14 +190,27 @@ __global__ __launch_bounds__(256) void rope_kernel(const uint16_t* __restrict__ 
   }
 }
 
-__global__ __launch_bounds__(256) void scale_kernel(uint16_t* __restrict__ x, const float* __restrict__ s, size_t nvec) {
+// x *= s[0] in place (bf16 or fp32), a no-op launch when s[0] == 1 (x * 1 == x bit for bit): the LM-head
+// backward's scale by the upstream gradient is 1 in every plain training step, so the 100-250 MB pass it
+// used to cost (torch mul) is read only when a loss scale / accumulation factor makes it needed
+template <bool F32>
+__global__ __launch_bounds__(256) void scale_kernel(void* __restrict__ xv, const float* __restrict__ s, size_t nvec) {
   const float sc = *s;
+  if (sc == 1.f) return;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nvec; i += (size_t)gridDim.x * blockDim.x) {
-    float f[8];
-    unpack8(ld16(x + i * 8), f);
+    if constexpr (F32) {
+      f32x4* x = reinterpret_cast<f32x4*>(xv) + 2 * i;
+      f32x4 a = x[0], b = x[1];
+      x[0] = a * sc;
+      x[1] = b * sc;
+    } else {
+      uint16_t* x = reinterpret_cast<uint16_t*>(xv);
+      float f[8];
+      unpack8(ld16(x + i * 8), f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] *= sc;
-    st16(x + i * 8, pack8(f));
+      for (int j = 0; j < 8; ++j) f[j] *= sc;
+      st16(x + i * 8, pack8(f));
+    }
   }
 }
 
@@ -323,9 +336,10 @@ void rope(const void* in, void* out, const float* cosb, const float* sinb, size_
                      sinb, rows, T, n_heads_total, n_rot, D, pos_offset, inverse ? -1.f : 1.f, out_heads);
 }
 
-void scale_bf16(void* x, const float* s, size_t n, hipStream_t st) {
+void scale_inplace(void* x, bool f32, const float* s, size_t n, hipStream_t st) {
   const size_t nv = n / 8;
-  hipLaunchKernelGGL(scale_kernel, dim3(ew_grid(nv)), dim3(256), 0, st, (uint16_t*)x, s, nv);
+  if (f32) hipLaunchKernelGGL(scale_kernel<true>, dim3(ew_grid(nv)), dim3(256), 0, st, x, s, nv);
+  else hipLaunchKernelGGL(scale_kernel<false>, dim3(ew_grid(nv)), dim3(256), 0, st, x, s, nv);
 }
 
 void lse_merge(float* o_acc, float* lse_acc, const void* o, const float* lse, const int64_t* st, int B, int T, int H,

@@ -81,7 +81,7 @@ void swiglu_fwd(const void* gu, void* y, size_t rows, int F, hipStream_t st);
 void swiglu_bwd(const void* dy, const void* gu, void* dgu, size_t rows, int F, hipStream_t st);
 void rope(const void* in, void* out, const float* cosb, const float* sinb, size_t rows, int T, int n_heads_total,
           int n_rot, int D, int pos_offset, bool inverse, hipStream_t st, int out_heads = 0);
-void scale_bf16(void* x, const float* s, size_t n, hipStream_t st);
+void scale_inplace(void* x, bool f32, const float* s, size_t n, hipStream_t st);  // x *= s[0] (no-op when 1)
 // ring-attention LSE merge; st: element strides of o_acc (b, t, h), lse_acc (b, h, t), o (b, t, h), lse (b, h, t)
 // zero n byte ranges of buf (desc int64 [n][3] on the device = start, end, bytes of the ranges before; 16-B
 // aligned); total_bytes: all ranges together

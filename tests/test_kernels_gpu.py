@@ -909,6 +909,15 @@ def test_lm_head_ce_chunked(chunk, with_bias, monkeypatch):
     ops.lm_head_cross_entropy(h, W, b, t).backward()
     assert W.grad is None
     assert _rel(W._pllm_gradbuf.double() - 1, 2 * Wf.grad.double()) < 3e-2
+    # an untouched slot (lazy zeroing's first writer of the step): the chunks write straight into it during the
+    # forward -- over stale NaN -- and the backward scales it in place by the upstream gradient (3 here; and 1)
+    for up in (3.0, 1.0):
+        W._pllm_gradbuf = torch.full((V, C), float("nan"), device=DEV)
+        W._pllm_grad_fresh = True
+        (ops.lm_head_cross_entropy(h, W, b, t) * up).backward()
+        assert W._pllm_grad_fresh is False and W.grad is None
+        assert not W._pllm_gradbuf.isnan().any()
+        assert _rel(W._pllm_gradbuf.double(), 2 * up * Wf.grad.double()) < 3e-2
 
 
 @pytest.mark.parametrize("D,T,H,Hkv,B", [(32, 1024, 4, 4, 2), (64, 2048, 4, 2, 1), (64, 4096, 2, 2, 1),
@@ -1176,3 +1185,18 @@ def test_attention_bwd_key_stationary_rope_offset(D, T, S):
             assert _rel(a, b) < 3e-2, (n, _rel(a, b))
     finally:
         torch.ops.pllm.attn_bwd_set_ks(2)  # the shipped default: D = 128 only
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_scale_inplace_unit_fast_path(dtype):
+    """torch.ops.pllm.scale_ (the LM-head backward's upstream-gradient scale): x *= s in place for bf16 / fp32,
+    and a bit-exact no-op when s == 1 (the kernel returns before touching x)."""
+    torch.manual_seed(5)
+    x = (torch.randn(1 << 20, device=DEV) * 3).to(dtype)
+    x[::7] = float("nan")
+    ref = x.clone()
+    torch.ops.pllm.scale_(x, torch.tensor([1.0], device=DEV))
+    assert torch.equal(x.isnan(), ref.isnan()) and torch.equal(x[~x.isnan()], ref[~ref.isnan()])
+    torch.ops.pllm.scale_(x, torch.tensor([-0.375], device=DEV))
+    want = (ref.float() * -0.375).to(dtype)
+    assert torch.equal(x.isnan(), want.isnan()) and torch.equal(x[~x.isnan()], want[~want.isnan()])
