@@ -121,9 +121,29 @@ __global__ __launch_bounds__(256) void sumsq_kernel(const void* __restrict__ x, 
   if (threadIdx.x == 0) part[blockIdx.x] = acc;
 }
 
+// gradient-norm finish + clip coefficient in ONE launch (it was seven torch kernels: sum of the partials, sqrt,
+// scale, add, reciprocal, mul, clamp): out[0] = sqrt(sum(part)) * grad_scale, out[1] = min(max_norm /
+// (out[0] + 1e-6), 1).  One 256-thread block; the partials are summed in a fixed order (deterministic).
+__global__ __launch_bounds__(256) void clip_coef_kernel(const float* __restrict__ part, int G, float grad_scale,
+                                                        float max_norm, float* __restrict__ out) {
+  __shared__ float scratch[4];
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < G; i += 256) acc += part[i];
+  acc = block_sum<4>(acc, scratch);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(acc) * grad_scale;
+    out[0] = norm;
+    out[1] = fminf(max_norm / (norm + 1e-6f), 1.f);
+  }
+}
+
 }  // namespace
 
 namespace pllm {
+
+void clip_coef(const float* part, int G, float grad_scale, float max_norm, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(256), 0, st, part, G, grad_scale, max_norm, out);
+}
 
 void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void* grad, bool grad_f32, size_t n,
                 float lr, float b1, float b2, float eps, float wd, int step, float grad_scale,

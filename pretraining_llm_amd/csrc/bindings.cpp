@@ -668,6 +668,22 @@ Tensor sumsq(const Tensor& x) {
   return part.sum();
 }
 
+// gradient norm and clip coefficient of a flat gradient in two launches (partial sums of squares, then one
+// single-block finish): returns [norm * grad_scale, min(max_norm / (norm * grad_scale + 1e-6), 1)] (fp32, GPU)
+Tensor grad_norm_clip(const Tensor& x, double grad_scale, double max_norm) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.is_contiguous() && x.numel() % 8 == 0, "grad_norm_clip: contiguous, numel % 8");
+  const bool f32 = x.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32 || x.scalar_type() == at::kBFloat16, "grad_norm_clip dtype");
+  const int G = pllm::sumsq_blocks(x.numel());
+  Tensor part = at::empty({G}, x.options().dtype(at::kFloat));
+  Tensor out = at::empty({2}, x.options().dtype(at::kFloat));
+  if (x.numel()) pllm::sumsq(x.data_ptr(), f32, x.numel(), part.data_ptr<float>(), cur_stream());
+  else part.zero_();
+  pllm::clip_coef(part.data_ptr<float>(), G, (float)grad_scale, (float)max_norm, out.data_ptr<float>(), cur_stream());
+  return out;
+}
+
 // ---------------------------------------------------------------- embedding
 Tensor embedding_fwd(const Tensor& idx, const Tensor& wte, const std::optional<Tensor>& wpe, int64_t pos_offset) {
   check_bf16(wte, "wte");
@@ -1072,6 +1088,7 @@ TORCH_LIBRARY(pllm, m) {
   m.def("cross_entropy(Tensor logits, Tensor targets, Tensor(a!)? dlogits, int ignore_index, Tensor? inv_n=None) -> Tensor");
   m.def("adamw_(Tensor(a!) param, Tensor(b!) master, Tensor(c!) m, Tensor(d!) v, Tensor grad, float lr, float b1, float b2, float eps, float wd, int step, float grad_scale, Tensor? scale, Tensor? wd_mask, Tensor? hyper=None) -> ()");
   m.def("sumsq(Tensor x) -> Tensor");
+  m.def("grad_norm_clip(Tensor x, float grad_scale, float max_norm) -> Tensor");
   m.def("embedding_fwd(Tensor idx, Tensor wte, Tensor? wpe, int pos_offset) -> Tensor");
   m.def("embedding_bwd(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe) -> (Tensor, Tensor)");
   m.def("embedding_bwd_acc(Tensor dx, Tensor idx, int V, int n_pos, bool has_wpe, Tensor(a!) dwte_acc, Tensor(b!)? dwpe_acc=None) -> ()");
@@ -1103,6 +1120,7 @@ TORCH_LIBRARY_IMPL(pllm, CUDA, m) {
   m.impl("cross_entropy", cross_entropy);
   m.impl("adamw_", adamw_);
   m.impl("sumsq", sumsq);
+  m.impl("grad_norm_clip", grad_norm_clip);
   m.impl("embedding_fwd", embedding_fwd);
   m.impl("embedding_bwd", embedding_bwd_op);
   m.impl("embedding_bwd_acc", embedding_bwd_acc_op);

@@ -100,6 +100,8 @@ void adamw_flat(void* param_bf16, float* master, float* m, float* v, const void*
                 const float* scale_ptr, const uint8_t* wd_blocks, const float* hyper, hipStream_t st);
 int sumsq_blocks(size_t n);
 void sumsq(const void* x, bool f32, size_t n, float* part, hipStream_t st);
+// out[0] = sqrt(sum(part[0..G))) * grad_scale (the gradient norm), out[1] = min(max_norm / (out[0] + 1e-6), 1)
+void clip_coef(const float* part, int G, float grad_scale, float max_norm, float* out, hipStream_t st);
 
 // embedding.hip
 void embedding_fwd(const int64_t* idx, const void* wte, const void* wpe, void* out, int64_t N, int T, int C,

@@ -124,6 +124,10 @@ def register() -> None:
     def _(x):
         return x.new_empty((), dtype=f32)
 
+    @_reg("grad_norm_clip")
+    def _(x, grad_scale, max_norm):
+        return x.new_empty((2,), dtype=f32)
+
     @_reg("embedding_fwd")
     def _(idx, wte, wpe, pos_offset):
         return wte.new_empty((idx.shape[0], idx.shape[1], wte.shape[1]))

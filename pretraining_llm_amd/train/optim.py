@@ -302,9 +302,16 @@ class FlatAdamW:
         self._clear_unwritten()
         clip = None
         if self.max_grad_norm and self.max_grad_norm > 0:
-            norm = self.grad_norm(grad_scale)
-            self.last_grad_norm = norm
-            clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).to(torch.float32).reshape(1)
+            if (self.use_hip and _ops_mod.get_backend() == "auto" and getattr(self, "tp", 1) <= 1
+                    and self.flat_grad.numel() % 8 == 0):
+                # norm and clip coefficient in two launches (partial sums of squares + one finishing block)
+                nc = _lib.require().grad_norm_clip(self.flat_grad, float(grad_scale), float(self.max_grad_norm))
+                self.last_grad_norm = nc[0]
+                clip = nc[1:2]
+            else:
+                norm = self.grad_norm(grad_scale)
+                self.last_grad_norm = norm
+                clip = torch.clamp(self.max_grad_norm / (norm + 1e-6), max=1.0).to(torch.float32).reshape(1)
         b1, b2 = self.betas
         if self.use_hip and _ops_mod.get_backend() == "auto":
             _lib.require().adamw_(self.flat_param, self.master, self.exp_avg, self.exp_avg_sq, self.flat_grad,

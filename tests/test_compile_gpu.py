@@ -47,6 +47,7 @@ def _op_cases():
         ("cross_entropy", (r(N, V), torch.randint(0, V, (N,), device=DEV), r(N, V), -100,
                            torch.full((1,), 1.0 / N, device=DEV))),
         ("sumsq", (r(4096, dt=f32),)),
+        ("grad_norm_clip", (r(4096, dt=f32), 0.5, 1.0)),
         ("embedding_fwd", (idx, r(V, C), r(T, C), 0)),
         ("embedding_bwd", (r(B, T, C), idx, V, T, True)),
         ("embedding_bwd_acc", (r(B, T, C), idx, V, T, True, torch.zeros(V, C, device=DEV),
@@ -62,7 +63,7 @@ def _op_cases():
     ]
 
 
-@pytest.mark.parametrize("i", range(27))
+@pytest.mark.parametrize("i", range(28))
 def test_opcheck_fake_matches_kernel(i):
     torch.manual_seed(i)
     cases = _op_cases()

@@ -1200,3 +1200,18 @@ def test_scale_inplace_unit_fast_path(dtype):
     torch.ops.pllm.scale_(x, torch.tensor([-0.375], device=DEV))
     want = (ref.float() * -0.375).to(dtype)
     assert torch.equal(x.isnan(), want.isnan()) and torch.equal(x[~x.isnan()], want[~want.isnan()])
+
+
+def test_grad_norm_clip_matches_torch():
+    """torch.ops.pllm.grad_norm_clip (the optimizer's norm + clip coefficient in two launches) vs the torch
+    expression it replaced: norm = sqrt(sum g^2) * grad_scale, clip = min(max_norm / (norm + 1e-6), 1); both
+    the clipping and the non-clipping side; deterministic."""
+    torch.manual_seed(9)
+    g = torch.randn(3 * 2 ** 20 + 64, device=DEV)
+    for scale, max_norm in ((0.5, 1.0), (1.0, 1e6)):
+        out = torch.ops.pllm.grad_norm_clip(g, scale, max_norm)
+        norm = g.double().pow(2).sum().sqrt() * scale
+        clip = min(max_norm / (norm.item() + 1e-6), 1.0)
+        assert abs(out[0].item() - norm.item()) < 1e-5 * norm.item()
+        assert abs(out[1].item() - clip) < 1e-5 * clip
+        assert torch.equal(torch.ops.pllm.grad_norm_clip(g, scale, max_norm), out)
