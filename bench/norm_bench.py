@@ -29,7 +29,7 @@ def main():
     _lib.require()
     P = torch.ops.pllm
     for N, C, rms, res in ((65536, 768, False, False), (65536, 768, False, True), (32768, 2048, True, False),
-                           (16384, 1024, False, False)):
+                           (16384, 1024, False, False), (32768, 1024, False, False), (32768, 2048, True, True)):
         x = torch.randn(N, C, device="cuda").bfloat16()
         r = torch.randn(N, C, device="cuda").bfloat16() if res else None
         w = torch.randn(C, device="cuda").bfloat16()

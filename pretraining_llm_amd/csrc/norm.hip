@@ -23,6 +23,7 @@ namespace {
 
 constexpr int ROWS_PER_BLOCK = 4;  // 4 waves, one row each
 
+// One row per wave, full grid (C > 1024 or few rows: measured faster there than the persistent form below)
 template <int K>  // chunks of 8 elements per lane (C <= 512*K)
 __global__ __launch_bounds__(256) void norm_fwd_kernel(
     const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
@@ -94,6 +95,108 @@ __global__ __launch_bounds__(256) void norm_fwd_kernel(
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
+  }
+}
+
+
+// One wave per row, rows strided over a persistent grid (8 blocks of 4 waves per CU); the NEXT row's x (and
+// residual) loads are issued before the current row is reduced, so every wave keeps two rows of loads in flight
+// at full occupancy (one row per wave at a time ran at ~4 TB/s at 65536 x 768; two rows per wave with half the
+// waves was slower still, profiles/r6_norm_fwd_two_rows_negative.log).  The weight / bias chunks are loaded once
+// before the loop: a load issued after the prefetch would make its wait drain the prefetch too.
+template <int K>  // chunks of 8 elements per lane (C <= 512*K)
+__global__ __launch_bounds__(256) void norm_fwd_pf_kernel(
+    const uint16_t* __restrict__ x, const uint16_t* __restrict__ res, const uint16_t* __restrict__ w,
+    const uint16_t* __restrict__ b, uint16_t* __restrict__ y, uint16_t* __restrict__ s_out,
+    float* __restrict__ mean_out, float* __restrict__ rstd_out, int N, int C, float eps, int rms) {
+  const int lane = threadIdx.x & 63;
+  const int stride = gridDim.x * ROWS_PER_BLOCK;
+  int row = blockIdx.x * ROWS_PER_BLOCK + (threadIdx.x >> 6);
+  if (row >= N) return;
+  const int nch = C >> 3;
+  const u32x4 zero4 = u32x4{0u, 0u, 0u, 0u};
+  u32x4 wv[K], bv[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int c = lane + 64 * k;
+    wv[k] = c < nch ? ld16(w + c * 8) : zero4;
+    bv[k] = (b && c < nch) ? ld16(b + c * 8) : zero4;
+  }
+  // loads of row min(r, N - 1): always issued (no conditional VMEM, so the compiler's counted waits stay exact)
+  auto load = [&](int r, u32x4* X, u32x4* R) __attribute__((always_inline)) {
+    const size_t base = (size_t)min(r, N - 1) * C;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      X[k] = c < nch ? ld16(x + base + c * 8) : zero4;
+      R[k] = (res && c < nch) ? ld16(res + base + c * 8) : zero4;
+    }
+  };
+  const float invC = 1.f / (float)C;
+  auto process = [&](int row, const u32x4* cx, const u32x4* cr) __attribute__((always_inline)) {
+    const size_t base = (size_t)row * C;
+    float v[K][8];
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      unpack8(cx[k], v[k]);
+      if (c < nch) {
+        if (res) {
+          float r8[8];
+          unpack8(cr[k], r8);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[k][j] += r8[j];
+          u32x4 sv = pack8(v[k]);
+          st16(s_out + base + c * 8, sv);
+          unpack8(sv, v[k]);  // normalise exactly the bf16 value that backward will see
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sum += v[k][j];
+      }
+    }
+    float mean = 0.f;
+    if (!rms) mean = wave_sum(sum) * invC;
+    float sq = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float d = v[k][j] - mean;
+          sq += d * d;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(sq) * invC + eps);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nch) {
+        float w8[8], b8[8], o[8];
+        unpack8(wv[k], w8);
+        unpack8(bv[k], b8);  // (zeros without a bias)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = (v[k][j] - mean) * rstd * w8[j] + b8[j];
+        st16(y + base + c * 8, pack8(o));
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  };
+  // two register sets, rows alternating between them: while one row is reduced the next one's loads (and the
+  // one after, issued right after the reduce) are in flight -- no register copies, so no vmcnt(0) at the latch
+  u32x4 ax[K], ar[K], bx[K], br[K];
+  load(row, ax, ar);
+  load(row + stride, bx, br);
+  for (; row < N; row += 2 * stride) {
+    process(row, ax, ar);
+    load(row + 2 * stride, ax, ar);
+    if (row + stride < N) process(row + stride, bx, br);
+    load(row + 3 * stride, bx, br);
   }
 }
 
@@ -326,12 +429,24 @@ namespace pllm {
 
 void norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* s, float* mean,
               float* rstd, int N, int C, float eps, bool rms, hipStream_t st) {
-  dim3 grid((N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK), block(256);
+  const int blocks = (N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
   const int K = (C + 511) / 512;
-#define L(KK)                                                                                           \
-  hipLaunchKernelGGL(norm_fwd_kernel<KK>, grid, block, 0, st, (const uint16_t*)x, (const uint16_t*)res, \
-                     (const uint16_t*)w, (const uint16_t*)b, (uint16_t*)y, (uint16_t*)s, mean, rstd, N, C, eps, \
-                     (int)rms)
+  // rows of <= 1,024 elements and >= 4 rows per wave of the persistent grid (8 blocks of 4 waves per CU):
+  // the persistent two-row-prefetch kernel -- 36-37 vs 41-43 us at 65536 x 768 -- else one row per wave, full
+  // grid (32768 x 2048: 45 vs 47 us; 16384 x 1024: 14.7 vs 15.4 us) (profiles/r6_norm_fwd_prefetch.log)
+  const bool pf = K <= 2 && blocks >= 4 * 2048;
+  dim3 grid(pf ? 2048 : blocks), block(256);
+#define L(KK)                                                                                                  \
+  do {                                                                                                         \
+    if (pf)                                                                                                    \
+      hipLaunchKernelGGL(norm_fwd_pf_kernel<KK>, grid, block, 0, st, (const uint16_t*)x, (const uint16_t*)res, \
+                         (const uint16_t*)w, (const uint16_t*)b, (uint16_t*)y, (uint16_t*)s, mean, rstd, N, C,  \
+                         eps, (int)rms);                                                                       \
+    else                                                                                                       \
+      hipLaunchKernelGGL(norm_fwd_kernel<KK>, grid, block, 0, st, (const uint16_t*)x, (const uint16_t*)res,    \
+                         (const uint16_t*)w, (const uint16_t*)b, (uint16_t*)y, (uint16_t*)s, mean, rstd, N, C,  \
+                         eps, (int)rms);                                                                       \
+  } while (0)
   if (K <= 1) L(1);
   else if (K <= 2) L(2);
   else if (K <= 4) L(4);

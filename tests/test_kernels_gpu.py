@@ -74,6 +74,33 @@ def test_norm_fwd_bwd(C, rms, with_res):
         assert _rel(r.grad, rf.grad) < 2e-2
 
 
+@pytest.mark.parametrize("C", [768, 1024])
+@pytest.mark.parametrize("rms", [False, True])
+@pytest.mark.parametrize("with_res", [False, True])
+def test_norm_fwd_prefetch_path(C, rms, with_res):
+    """>= 32768 rows of <= 1024 elements take the persistent two-row-prefetch forward; a ragged row count checks
+    the clamped tail loads and the odd last row of each wave."""
+    from pretraining_llm_amd import ops
+    torch.manual_seed(1)
+    N = 40001
+    x = torch.randn(N, C, device=DEV, dtype=torch.bfloat16)
+    r = torch.randn(N, C, device=DEV, dtype=torch.bfloat16) if with_res else None
+    w = (1 + 0.1 * torch.randn(C, device=DEV)).bfloat16()
+    b = None if rms else (0.1 * torch.randn(C, device=DEV)).bfloat16()
+    with torch.no_grad():
+        y, s = ops.rms_norm(x, w, 1e-5, r) if rms else ops.layer_norm(x, w, b, 1e-5, r)
+    sq = (x.float() + r.float()).bfloat16().float() if with_res else x.float()
+    if rms:
+        yf = sq * torch.rsqrt(sq.pow(2).mean(-1, keepdim=True) + 1e-5) * w.float()
+    else:
+        yf = F.layer_norm(sq, (C,), w.float(), b.float(), 1e-5)
+    assert _rel(y, yf) < 1e-2
+    # every row written (a skipped row would leave garbage / zeros far from the reference)
+    assert ((y.float() - yf).abs().amax(-1) < 0.1).all()
+    if with_res:
+        assert torch.equal(s, sq.bfloat16())
+
+
 # ----------------------------------------------------------------- activations
 @pytest.mark.parametrize("kind", ["gelu", "relu"])
 def test_activation(kind):
