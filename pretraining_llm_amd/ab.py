@@ -18,6 +18,7 @@ choice on the same box without a rebuild.  The C++ side reads the same variable 
 | wgrad_variant | -- | weight-gradient kernel variant id (torch.ops.pllm.wgrad_set_mfma) | r2_wgrad_4wave_negative.jsonl and the other r2_wgrad_* records |
 | wgrad_hy | -- | 0 / 1: hybrid whole-tile + sliced-last-round weight-gradient split | r4_wgrad_hybrid.md |
 | gemm_persistent | -- | 0 / 1: persistent GEMM grids (default: automatic, train/graph.py) | r4_gemm_persistent_ab.txt |
+| dp_world1 | 0 | 1: the DP engine's gradient hooks + bucketed all-reduces at world 1 (a one-rank RCCL rehearsal of the world > 1 step) | tests/test_dp_gpu.py |
 | lazy_zero | 1 | 0: zero the whole flat gradient every step | r4_lazy_zero_ab.md |
 | ce_chunk_rows | 0 | rows per LM-head + CE chunk (0: automatic) | r2_ce_chunk_sweep.jsonl |
 | ce_nt | 1 | 0: plain (not non-temporal) dlogits stores in the CE kernel | csrc/cross_entropy.hip (2,493 vs 2,524 us) |

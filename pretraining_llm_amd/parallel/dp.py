@@ -32,6 +32,8 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ..ab import ab as _ab
+
 
 class CommTimer:
     """Where a DP step's communication time went, from HIP events on the compute stream (no host
@@ -93,6 +95,10 @@ class DataParallelEngine:
         self.opt = optimizer
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        # whether gradients are all-reduced: world > 1, or (PLLM_AB dp_world1=1, debug only) a world-1 process
+        # group -- the hooks, bucket launches and waits of the world > 1 step then run over a one-rank RCCL
+        # communicator, a rehearsal of the multi-GPU path on a one-GPU box (tests/test_dp_gpu.py)
+        self.sync = self.world > 1 or (dist.is_initialized() and _ab("dp_world1", False))
         self.overlap = overlap
         self.timer = CommTimer(timing and optimizer.flat_grad.is_cuda)
         self.enabled = True
@@ -138,10 +144,10 @@ class DataParallelEngine:
         self._expected: Optional[List[int]] = None
         self._events = [0] * len(params)
         self._reset_counters()
-        if broadcast_params and self.world > 1:
+        if broadcast_params and self.sync:
             dist.broadcast(optimizer.flat_param, src=self._global_src(), group=process_group)
             optimizer.sync_master_from_params()
-        if self.world > 1 and overlap:
+        if self.sync and overlap:
             for i, p in enumerate(params):
                 h = self._make_hook(i)
                 self._hooks.append(p.register_post_accumulate_grad_hook(lambda _p, h=h: h()))
@@ -213,7 +219,7 @@ class DataParallelEngine:
         """Launch any bucket not yet launched (unused params, no-overlap mode) and wait for all.
         Returns the gradient scale the optimizer must apply (1/world)."""
         self.timer.backward_end()
-        if self.world > 1:
+        if self.sync:
             while self._next_launch < len(self.buckets):
                 self._launch(self._next_launch)
                 self._next_launch += 1

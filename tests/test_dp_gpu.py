@@ -245,3 +245,60 @@ def test_dp_lazy_zero_weight_unused_on_one_rank():
             assert step_sums[0] == step_sums[1], (key, step_sums)
     rel = ((out["lazy"] - out["full"]).norm() / out["full"].norm()).item()
     assert rel < 1e-6, rel
+
+
+def _rccl_worker(rank, world, port, outdir):
+    """One rank on RCCL (backend nccl): the engine with its world > 1 machinery forced on (hooks launching
+    bucketed all-reduces during the backward on the communicator's stream, waits, readiness learning) against
+    the plain world-1 engine, same seed and data."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from pretraining_llm_amd import ops
+    from pretraining_llm_amd.ab import ab_set
+    from pretraining_llm_amd.models import GPT
+    from pretraining_llm_amd.parallel.dp import DataParallelEngine, params_checksum
+    from pretraining_llm_amd.train.optim import FlatAdamW
+    ops._lib.require()
+    data = _data(1).to(dev)
+    x, y = data[:, :-1].contiguous(), data[:, 1:].contiguous()
+    out = {"backend": dist.get_backend()}
+    for forced in (False, True):
+        ab_set("dp_world1", forced)
+        torch.manual_seed(0)
+        model = GPT(_cfg()).to(device=dev, dtype=torch.bfloat16)
+        opt = FlatAdamW(model, lr=1e-3, max_grad_norm=1.0)
+        eng = DataParallelEngine(opt, bucket_mb=0.5, first_bucket_mb=0.1)
+        in_bwd, sums, grads = [], [], []
+        for step in range(4):
+            opt.zero_grad()
+            _, loss = model(x, y, return_logits=False)
+            loss.backward()
+            in_bwd.append(eng._next_launch)  # buckets launched by the hooks before the end of the backward
+            scale = eng.finish_grad_sync()
+            grads.append(opt.flat_grad.float().cpu().clone())
+            opt.step(grad_scale=scale)
+            sums.append(params_checksum(opt.params).item())
+        eng.remove_hooks()
+        torch.cuda.synchronize()
+        out["forced" if forced else "plain"] = {"sync": eng.sync, "nb": len(eng.buckets), "in_bwd": in_bwd,
+                                               "sums": sums, "g": torch.stack(grads)}
+    torch.save(out, os.path.join(outdir, "rccl.pt"))
+    dist.destroy_process_group()
+
+
+def test_dp_rccl_world1_rehearsal():
+    """The world > 1 data-parallel step over a real RCCL communicator (one rank: a one-GPU box cannot host two
+    RCCL ranks): bit-identical gradients and weights to the plain step, and the buckets after the first
+    (learning) step launched from the gradient hooks inside the backward."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_rccl_worker, args=(1, _free_port(), d), nprocs=1, join=True)
+        out = torch.load(os.path.join(d, "rccl.pt"), weights_only=True)
+    assert out["backend"] == "nccl"
+    f, p = out["forced"], out["plain"]
+    assert f["sync"] and not p["sync"]
+    assert f["in_bwd"][0] == 0 and all(n == f["nb"] for n in f["in_bwd"][1:]), f["in_bwd"]
+    assert torch.equal(f["g"], p["g"])
+    assert f["sums"] == p["sums"]
