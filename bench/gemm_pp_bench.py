@@ -19,6 +19,7 @@ import torch.nn.functional as F  # noqa: E402
 
 GPT2 = [(65536, 3072, 768), (65536, 768, 3072), (65536, 2304, 768), (65536, 768, 768)]
 LLAMA = [(32768, 11008, 2048), (32768, 2048, 5504), (32768, 6144, 2048), (32768, 2048, 2048)]
+HEAD = [(65536, 50304, 768), (32768, 50304, 2048)]  # the LM-head forwards (no bias)
 
 
 def once(fn, reps):
@@ -35,14 +36,19 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--fused", action="store_true", help="also the fused MLP epilogues (GELU fwd / dGELU+colsum)")
-    ap.add_argument("--shapes", default="all", choices=["gpt2", "llama", "all"])
+    ap.add_argument("--shapes", default="all", choices=["gpt2", "llama", "all", "head"])
+    ap.add_argument("--tuned", action="store_true", help="the shipped TunableOp GEMM selections on (as in bench.py)")
     ap.add_argument("--group", type=int, default=4)
     ap.add_argument("--no-r3", action="store_true", help="skip the round-3 kernel variants")
     args = ap.parse_args()
     from pretraining_llm_amd.ops import _lib
     _lib.require()
     P = torch.ops.pllm
-    shapes = (GPT2 if args.shapes != "llama" else []) + (LLAMA if args.shapes != "gpt2" else [])
+    shapes = HEAD if args.shapes == "head" else \
+        (GPT2 if args.shapes != "llama" else []) + (LLAMA if args.shapes != "gpt2" else [])
+    if args.tuned:
+        from pretraining_llm_amd.utils.gemm_tuning import enable_tuned_gemms
+        enable_tuned_gemms(0)
 
     def with_cfg(ph, fn):
         def run():
@@ -55,9 +61,14 @@ def main():
         a = torch.empty(M, K, device="cuda").uniform_(-1, 1, generator=g).bfloat16()
         w = (torch.empty(N, K, device="cuda").uniform_(-1, 1, generator=g) / K ** 0.5).bfloat16()
         b = torch.empty(N, device="cuda").uniform_(-1, 1, generator=g).bfloat16()
-        var = {"pp": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0)),
-               "r3": with_cfg(0, lambda: P.gemm_tn(a, w, b, 0)),
-               "blas": lambda: F.linear(a, w, b)}
+        if args.shapes == "head":
+            var = {"pp": with_cfg(4, lambda: P.gemm_tn(a, w, None, 0)),
+                   "r3": with_cfg(0, lambda: P.gemm_tn(a, w, None, 0)),
+                   "blas": lambda: torch.mm(a, w.t())}
+        else:
+            var = {"pp": with_cfg(4, lambda: P.gemm_tn(a, w, b, 0)),
+                   "r3": with_cfg(0, lambda: P.gemm_tn(a, w, b, 0)),
+                   "blas": lambda: F.linear(a, w, b)}
         extra = {}
         if args.fused and N > K:
             pre = torch.empty(M, N, device="cuda").uniform_(-2, 2, generator=g).bfloat16()
