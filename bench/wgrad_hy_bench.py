@@ -27,17 +27,20 @@ for M, Pd, Q in SHAPES:
     dy = (torch.randn(M, Pd, device="cuda") * 0.1).bfloat16()
     x = torch.randn(M, Q, device="cuda").bfloat16()
     tgt = torch.zeros(Pd, Q, device="cuda")
-    ts = {0: [], 1: []}
+    ts = {0: [], 1: [], 2: []}
     for r in range(7):
-        for sk in (0, 1):
-            P.wgrad_set_hy(sk)
+        for sk in (0, 1, 2):  # 2: the hybrid with its remainder as one round of slices (PLLM_AB wgrad_hy_cost=0)
+            P.wgrad_set_hy(min(sk, 1))
+            os.environ["PLLM_AB"] = "wgrad_hy_cost=0" if sk == 2 else ""
             f = lambda: P.wgrad(dy, x, tgt)
             f()
             ts[sk].append(once(f))
-    P.wgrad_set_hy(0)
+    os.environ["PLLM_AB"] = ""
+    P.wgrad_set_hy(1)
     fl = 2 * M * Pd * Q
     med = {k: statistics.median(v) for k, v in ts.items()}
     print(json.dumps({"M": M, "P": Pd, "Q": Q, "slices_us": round(med[0], 1), "hy_us": round(med[1], 1),
                       "slices_tflops": round(fl / med[0] / 1e6, 1), "hy_tflops": round(fl / med[1] / 1e6, 1),
-                      "speedup": round(med[0] / med[1], 3)}), flush=True)
+                      "speedup": round(med[0] / med[1], 3),
+                      "hy_one_round_us": round(med[2], 1), "cost_vs_one_round": round(med[2] / med[1], 3)}), flush=True)
     del dy, x, tgt

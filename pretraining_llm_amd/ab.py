@@ -16,6 +16,7 @@ choice on the same box without a rebuild.  The C++ side reads the same variable 
 | lt_relu | 1 | 0: ReLU MLP up-projection on torch + the activation kernel | r4_lt_relu_epilogue.md |
 | wgrad_bias | 1 | 0: bias gradients as a separate column-sum pass | r3s3_wgrad_fused_bias_ab.txt |
 | wgrad_variant | -- | weight-gradient kernel variant id (torch.ops.pllm.wgrad_set_mfma) | r2_wgrad_4wave_negative.jsonl and the other r2_wgrad_* records |
+| wgrad_hy_cost | 1 | 0: the hybrid weight gradient's remainder as one round of slices (ctas / rem) instead of the cost model's count | r6_wgrad_hy_cost.log |
 | wgrad_hy | -- | 0 / 1: hybrid whole-tile + sliced-last-round weight-gradient split | r4_wgrad_hybrid.md |
 | gemm_persistent | -- | 0 / 1: persistent GEMM grids (default: automatic, train/graph.py) | r4_gemm_persistent_ab.txt |
 | dp_world1 | 0 | 1: the DP engine's gradient hooks + bucketed all-reduces at world 1 (a one-rank RCCL rehearsal of the world > 1 step) | tests/test_dp_gpu.py |

@@ -31,6 +31,7 @@
 // Requires M % 64 == 0, P % 8 == 0, Q % 8 == 0, row strides % 8 == 0 (checked by the binding).
 #include <algorithm>
 
+#include "ab.h"
 #include "common.h"
 #include "kernels.h"
 
@@ -443,8 +444,11 @@ __global__ __launch_bounds__(256) void wgrad_hy_reduce_kernel(const float* __res
 namespace pllm {
 
 // hybrid plan: with more tiles than workgroups, whole tiles for the whole rounds of the grid and the
-// remaining tiles as slices filling the last round (>= 2 K-tiles each); false when it does not apply
-// (no more tiles than workgroups: wgrad_plan's uniform slices)
+// remaining tiles as slices (>= 2 K-tiles each); false when it does not apply (no more tiles than
+// workgroups: wgrad_plan's uniform slices).  The remainder's slice count comes from wgrad_plan's cost model
+// (rounds x K-tiles per slice x ~2 us, plus the tile pieces written and read back at ~4 TB/s) instead of
+// "one round of slices" (ctas / rem): llama's gate/up projection (344 tiles on 256 CUs, 88 left) takes 5
+// slices in 2 rounds (1.4 tile times) instead of 2 slices in 1 round (1.5) (profiles/r6_wgrad_hy_cost.log)
 bool wgrad_hy_plan(int M, int P, int Q, int ctas, int* full, int* rem, int* S, int* slice_kt) {
   const int kst = M / WBK;
   const int ntiles = ((P + WT - 1) / WT) * ((Q + WT - 1) / WT);
@@ -452,6 +456,18 @@ bool wgrad_hy_plan(int M, int P, int Q, int ctas, int* full, int* rem, int* S, i
   *full = ntiles / ctas * ctas;
   *rem = ntiles - *full;
   int s = *rem > 0 ? std::max(1, std::min(ctas / *rem, kst / 2)) : 1;
+  if (*rem > 0 && ab_int("wgrad_hy_cost", 1)) {
+    double best_t = 1e30;
+    for (int c = 1; c <= 16 && (c == 1 || kst / c >= 8); ++c) {
+      const int per = (kst + c - 1) / c;
+      const int rounds = (*rem * c + ctas - 1) / ctas;
+      const double t = rounds * (double)per * 2.0e-6 + (c > 1 ? (double)*rem * c * WT * WT * 4.0 * 2 / 4.0e12 : 0.0);
+      if (t < best_t * 0.98) {
+        best_t = t;
+        s = c;
+      }
+    }
+  }
   *slice_kt = (kst + s - 1) / s;
   *S = *rem > 0 ? (kst + *slice_kt - 1) / *slice_kt : 0;
   return true;

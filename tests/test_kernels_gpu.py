@@ -1016,7 +1016,8 @@ def _rope_case(D, Hkv):
 
 
 @pytest.mark.parametrize("M,P,Q", [(4096, 50304, 768), (2048, 50304, 2048), (1024, 11008, 2048), (8192, 65536, 256),
-                                   (4096, 4104, 4104), (1024, 4352, 4096)])
+                                   (4096, 4104, 4104), (1024, 4352, 4096),
+                                   (32768, 11008, 2048)])  # llama gate/up: the remainder in two rounds of 5 slices
 def test_wgrad_hybrid(M, P, Q):
     """Hybrid weight gradients (the default, csrc/wgrad_pp.hip: more tiles than workgroups -> whole tiles for
     the grid's whole rounds, the remaining tiles as slices of the last round, finished by the ordered fix-up;
@@ -1047,8 +1048,10 @@ def test_wgrad_hybrid(M, P, Q):
         torch.ops.pllm.wgrad(dy, x, ow3, None, True)
     finally:
         torch.ops.pllm.wgrad_set_hy(1)  # the shipped default
-    assert _rel(acc.double(), acc3.double()) < 1e-6
-    assert _rel(ow.double(), ow3.double()) < 1e-6
+    # two fp32 summation orders over M tokens (1.03e-6 apart at M = 32768)
+    tol = 1e-6 if M <= 8192 else 3e-6
+    assert _rel(acc.double(), acc3.double()) < tol
+    assert _rel(ow.double(), ow3.double()) < tol
 
 
 def test_lm_head_ce_overwrite_nan_buffer():
