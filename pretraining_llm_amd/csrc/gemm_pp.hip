@@ -90,6 +90,10 @@ PL_DEV void pp_tile(int t, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
 //    partials, the EPI 6 delta on the second column pair).  Measured: faster at K = 3072 / 5504
 //    (fewer, longer tiles), slower at K = 768 (the epilogue work lands in the critical LOAD
 //    segments of four phases per tile).
+#ifndef PL_PP_EPI5_PFD
+#define PL_PP_EPI5_PFD 2  // row tiles of SwiGLU-backward aux loads in flight ahead of the one processed
+#endif
+
 template <int EPI>
 constexpr int kEndStores = (EPI == 1 || EPI == 5) ? 32 : EPI == 7 ? 24 : 16;
 // EPI 7 (SwiGLU forward of the llama up-projection, W1 = [gate | up] rows): a tile is 128 output
@@ -149,7 +153,11 @@ PL_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int
   // and the scheduling barrier at the end of each tile keeps the compiler from hoisting all 16-32
   // loads to the top, where the 128 accumulators are still live (that spilled)
   constexpr int NAX = EPI >= 3 ? (EPI == 5 ? 4 : 2) : 0;
+  // EPI 5 (four loads per row tile; all 32 up front do not fit beside the accumulators): a ring of
+  // PFD + 1 row tiles, the loads of row tile j + PFD issued before tile j is processed
+  constexpr int PFD = PL_PP_EPI5_PFD;
   u32x4 axc[NAX > 0 ? NAX : 1], axn[NAX > 0 ? NAX : 1];
+  u32x4 axr[EPI == 5 ? PFD + 1 : 1][NAX > 0 ? NAX : 1];
   auto aux_load = [&](int j, u32x4* dst) {
     if constexpr (NAX > 0) {
       const int rt = wr * 128 + 16 * j + r16;
@@ -169,13 +177,20 @@ PL_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int
   if constexpr (PRE) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) aux_load(j, axall[j]);
+  } else if constexpr (EPI == 5 && PFD > 1) {
+#pragma unroll
+    for (int d = 0; d < PFD; ++d) aux_load(d, axr[d]);
   } else {
     aux_load(0, axc);
   }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int rt = wr * 128 + 16 * j + r16;  // row within the tile
-    if constexpr (!PRE) {
+    if constexpr (EPI == 5 && PFD > 1) {
+      if (j + PFD < 8) aux_load(j + PFD, axr[(j + PFD) % (PFD + 1)]);
+#pragma unroll
+      for (int x = 0; x < NAX; ++x) axc[x] = axr[j % (PFD + 1)][x];
+    } else if constexpr (!PRE) {
       if (j + 1 < 8) aux_load(j + 1, axn);
     } else {
       axc[0] = axall[j][0];
@@ -260,8 +275,10 @@ PL_DEV void pp_epilogue(f32x4 (&acc)[4][8], const pllm::GemmArgs& g, int tm, int
       __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, dsum), drs, doff, 0, 0);
     }
     if constexpr (NAX > 0 && !PRE) {
+      if constexpr (!(EPI == 5 && PFD > 1)) {
 #pragma unroll
-      for (int x = 0; x < NAX; ++x) axc[x] = axn[x];
+        for (int x = 0; x < NAX; ++x) axc[x] = axn[x];
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   }
