@@ -71,8 +71,8 @@ def parse(argv=None):
                     help="persistent ping-pong GEMM / weight-gradient grids; auto: at one GPU only "
                          "(train/graph.py gemm_persistent_policy)")
     ap.add_argument("--graph-collectives", action="store_true",
-                    help="with N > 1 and --cuda-graph auto: capture the RCCL all-reduces inside the step's hipGraph "
-                         "(opt-in, as the Trainer's graph_collectives=True; default: eager hook-overlapped step)")
+                    help="capture the RCCL all-reduces inside the step's hipGraph: refused by the step policy (the capture "
+                         "aborts in ProcessGroupNCCL's watchdog, train/graph.py); the eager hook-overlapped step runs")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"],
                     help="cpu: functional rehearsal on gloo (fp32, tiny shapes); never a measurement")
     ap.add_argument("--verbose", action="store_true")

@@ -90,7 +90,7 @@ default_config = {
     'rccl_env': None,                 # extra RCCL / torch-NCCL env, dict or 'KEY=VAL,...' (utils/dist.apply_rccl_env)
     'gemm_reserve_cus': 0,            # CUs the persistent fused-epilogue GEMM grid leaves to RCCL kernels (world > 1)
     'gemm_persistent': 'auto',        # persistent ping-pong GEMM grids: auto = world 1 only (train/graph.py)
-    'graph_collectives': False,       # world > 1: capture the RCCL all-reduces in the hipGraph step (default: eager step)
+    'graph_collectives': False,       # refused (eager step): capturing RCCL collectives aborts (train/graph.py)
     'activation_checkpointing': None,
     'override_preset_dims': False,    # with model_preset: the dims above (n_embed, n_head, n_blocks, ...) override the preset's
     'tuned_gemms': True,              # GPU: load the shipped TunableOp GEMM selections (pretraining_llm_amd/tuning/)

@@ -32,11 +32,12 @@ def graph_step_policy(*, cuda: bool, world: int, dist_backend: Optional[str], ze
     ``Trainer`` (TORCH_COMPILE default) and ``bench.py`` (``--cuda-graph auto``) so the path the
     driver's multi-GPU bench measures is the path ``torchrun scripts/train_transformer.py`` runs.
 
-    Returns ``(use_graph, reason_if_not)``.  With more than one rank the default is the EAGER
-    step: the bucketed RCCL all-reduces are launched from the backward hooks on RCCL's own stream
-    and overlap the rest of the backward.  Capturing those collectives inside the graph is an
-    explicit opt-in (``graph_collectives=True``): it cannot be exercised on a one-GPU box (two
-    RCCL ranks cannot share a device), so it is not the default of any launch path."""
+    Returns ``(use_graph, reason_if_not)``.  With more than one rank the step is EAGER: the bucketed
+    RCCL all-reduces are launched from the backward hooks on RCCL's own stream and overlap the rest of
+    the backward.  ``graph_collectives=True`` (capture those collectives inside the graph) is refused:
+    rehearsed over a one-rank RCCL communicator (PLLM_AB dp_world1=1, profiles/r6_graph_collectives_abort.log)
+    the capture aborts the process -- ProcessGroupNCCL's watchdog queries an event recorded in the capturing
+    stream (hipErrorCapturedEvent) -- so the option falls back to the eager step with that reason."""
     if not cuda:
         return False, "not a GPU run"
     if zero:
@@ -49,12 +50,13 @@ def graph_step_policy(*, cuda: bool, world: int, dist_backend: Optional[str], ze
         return False, "non-bf16 dtype (the graphed step runs the bf16 HIP kernels)"
     if not hip_ops:
         return False, "stock torch ops backend (PLLM_TORCH_OPS / set_backend)"
-    if world > 1:
-        if dist_backend != "nccl":
+    if world > 1 or graph_collectives:
+        if world > 1 and dist_backend != "nccl":
             return False, f"dist backend {dist_backend} (collectives cannot be captured)"
-        if not graph_collectives:
-            return False, ("world > 1: eager step with hook-launched RCCL buckets (the bench's multi-GPU path); "
-                           "graph_collectives=True captures the collectives too")
+        if graph_collectives:
+            return False, ("graph_collectives: capturing RCCL collectives aborts in ProcessGroupNCCL's watchdog "
+                           "(hipErrorCapturedEvent, profiles/r6_graph_collectives_abort.log); eager step")
+        return False, "world > 1: eager step with hook-launched RCCL buckets (the bench's multi-GPU path)"
     return True, None
 
 

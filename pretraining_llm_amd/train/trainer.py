@@ -160,7 +160,7 @@ class Trainer:
         self.fwd = self.model
         if self.compile:
             # the same policy bench.py applies (train/graph.py): at world > 1 the eager step with
-            # hook-launched RCCL buckets unless graph_collectives=True; on the CPU torch.compile
+            # hook-launched RCCL buckets (graph_collectives is refused); on the CPU torch.compile
             from . import graph as _graph
             ok, why = _graph.graph_step_policy(
                 cuda=self.device.type == "cuda", world=self.di.world_size,

@@ -215,7 +215,8 @@ def test_trainer_and_bench_take_the_same_step_path(mode, tmp_path):
     checked by what they DO: 2 gloo ranks (torch.distributed.run) with the step policy stubbed to the
     RCCL branch (GPU, nccl, HIP ops) and a recording eager stand-in for the hipGraph capture
     (tests/_policy_probe.py).  Default: both run the eager hook-overlapped step (no capture object
-    built); graph_collectives=True: both build the capture and step through it."""
+    built); graph_collectives=True: refused by the policy (it aborts on RCCL, train/graph.py), so both take
+    the eager step as well."""
     import json
     import subprocess
     import sys
@@ -228,18 +229,14 @@ def test_trainer_and_bench_take_the_same_step_path(mode, tmp_path):
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     recs = [json.loads(l.split("PROBE ", 1)[1]) for l in r.stdout.splitlines() if "PROBE " in l]
     assert sorted(x["rank"] for x in recs) == [0, 1], r.stdout
-    want = "graph" if mode == "graph_collectives" else "eager"
+    want = "eager"
     for x in recs:
         t, b = x["trainer"], x["bench"]
         assert t["step_mode"] == want, x
         assert b["rc"] in (None, 0), x
         if x["rank"] == 0:
             assert b["step_mode"] == want, x  # rank 0 prints the bench record
-        if want == "graph":
-            assert t["capture_objects"] == 1 and t["captured_steps"] == 2, x
-            assert b["capture_objects"] == 1 and b["captured_steps"] >= 3, x  # 2 warmup-less timed + capture
-        else:
-            assert t["capture_objects"] == 0 and b["capture_objects"] == 0, x
+        assert t["capture_objects"] == 0 and b["capture_objects"] == 0, x
 
 
 def test_step_policy_decisions():
@@ -248,8 +245,10 @@ def test_step_policy_decisions():
     for world in (2, 4, 8):
         ok, why = g.graph_step_policy(cuda=True, world=world, dist_backend="nccl")
         assert not ok and "eager" in why
-        assert g.graph_step_policy(cuda=True, world=world, dist_backend="nccl", graph_collectives=True)[0]
+        ok, why = g.graph_step_policy(cuda=True, world=world, dist_backend="nccl", graph_collectives=True)
+        assert not ok and "hipErrorCapturedEvent" in why
         assert not g.graph_step_policy(cuda=True, world=world, dist_backend="gloo", graph_collectives=True)[0]
+    assert not g.graph_step_policy(cuda=True, world=1, dist_backend="nccl", graph_collectives=True)[0]
     assert g.graph_step_policy(cuda=True, world=1, dist_backend=None) == (True, None)
     assert not g.graph_step_policy(cuda=True, world=1, dist_backend=None, zero=True)[0]
     assert not g.graph_step_policy(cuda=False, world=1, dist_backend=None)[0]
