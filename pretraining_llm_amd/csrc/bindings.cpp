@@ -105,7 +105,7 @@ std::vector<Tensor> norm_bwd(const Tensor& dy, const Tensor& s, const Tensor& w,
   Tensor dx = at::empty_like(dy);
   Tensor dw = acc ? *dw_acc : at::zeros({C}, w.options());
   Tensor db = has_bias ? (acc ? *db_acc : at::zeros({C}, w.options())) : Tensor();
-  const int G = pllm::norm_bwd_grid((int)N);
+  const int G = pllm::norm_bwd_grid((int)N, (int)C);
   auto f32 = dy.options().dtype(at::kFloat);
   Tensor dwp = at::empty({G, C}, f32);
   Tensor dbp = has_bias ? at::empty({G, C}, f32) : Tensor();

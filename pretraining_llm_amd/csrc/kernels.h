@@ -58,7 +58,7 @@ namespace pllm {
 // norm.hip
 void norm_fwd(const void* x, const void* res, const void* w, const void* b, void* y, void* s, float* mean,
               float* rstd, int N, int C, float eps, bool rms, hipStream_t st);
-int norm_bwd_grid(int N);
+int norm_bwd_grid(int N, int C);
 // xb_part/xb: optional column sums of dx (bias grad of the layer that produced x)
 // Gradient outputs (dw, db, xb, bias grads, wgrad, embedding grads) are bf16 or fp32 (grad_f32 /
 // out_f32: the optimizer's flat-gradient dtype); activations and their gradients are bf16.

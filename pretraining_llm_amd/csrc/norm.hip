@@ -454,9 +454,12 @@ void norm_fwd(const void* x, const void* res, const void* w, const void* b, void
 #undef L
 }
 
-int norm_bwd_grid(int N) {
+// rows of > 1,024 elements (K >= 4, 256 VGPRs): 256 workgroups -- 98-99 vs 102-104 us at 32768 x 2048 --
+// else 512 (at 65536 x 768: 78-85 us, 110 with 256, 92 with 1,024) (profiles/r6_norm_grid_sweep.log)
+int norm_bwd_grid(int N, int C) {
   int g = (N + ROWS_PER_BLOCK - 1) / ROWS_PER_BLOCK;
-  return g < 512 ? g : 512;
+  const int cap = C > 1024 ? 256 : 512;
+  return g < cap ? g : cap;
 }
 
 void col_reduce(const float* part, int G, int C, void* out, bool out_f32, bool accumulate, hipStream_t st) {
@@ -471,7 +474,7 @@ void col_reduce(const float* part, int G, int C, void* out, bool out_f32, bool a
 void norm_bwd(const void* dy, const void* s, const void* w, const float* mean, const float* rstd, const void* ds,
               void* dx, float* dw_part, float* db_part, void* dw, void* db, bool grad_f32, int N, int C, bool rms,
               bool accumulate, float* xb_part, void* xb, bool xb_accumulate, hipStream_t st) {
-  const int G = norm_bwd_grid(N);
+  const int G = norm_bwd_grid(N, C);
   const int K = (C + 511) / 512;
   const size_t lds = (size_t)4 * C * sizeof(float);
 #define L(KK, XBB)                                                                                              \
